@@ -1,0 +1,88 @@
+"""Build the HIP C-ABI library ``numpyro_amd/_lib/libnumpyro_amd.so`` for gfx950.
+
+Plain ``hipcc`` invocations (no CMake, no torch extension): every ``csrc/*.hip`` and
+``csrc/*.cpp`` is compiled to an object in ``build/``, then linked into one shared
+library in-tree, so the built ``.so`` travels to the GPU box with the repo snapshot.
+Objects are rebuilt only when a source or header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+LIB_DIR = os.path.join(HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libnumpyro_amd.so")
+ARCH = os.environ.get("NMX_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+COMMON_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-I" + os.path.join(ROOT, "include"),
+    "-I" + CSRC,
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+
+
+def _stale(obj: str, src: str, headers) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(p) > t for p in [src, *headers])
+
+
+def _compile(src: str, obj: str) -> None:
+    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    cmd = [HIPCC, *COMMON_FLAGS, *lang, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    headers = _headers()
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _stale(o, s, headers):
+            todo.append((s, o))
+    jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_compile, s, o) for s, o in todo]
+            for f in futs:
+                f.result()
+            if verbose:
+                for s, _ in todo:
+                    print("compiled", os.path.relpath(s, ROOT))
+    if todo or not os.path.exists(LIB_PATH):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print("linked", os.path.relpath(LIB_PATH, ROOT))
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)
