@@ -1,0 +1,190 @@
+"""Benchmark: NUTS leapfrog steps/s over vectorized chains of the covtype logistic
+regression (BASELINE.json metric), one process per GPU.
+
+A "step" is one MCMC transition of every chain (one NUTS tree each).  Protocol
+(notebooks/source/logistic_regression.ipynb:202-210): `--warmup` adaptation transitions
+untimed (mcmc.warmup), then exactly `--steps` sampling transitions timed (mcmc.run),
+bracketed by barrier + synchronize on every rank; value = sum(num_steps) over all chains
+and ranks / max-over-ranks wall time (useful leapfrogs, inputs resident in HBM).
+
+Launch for N GPUs:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MI355X_FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (matrix), dense
+MI355X_HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5, help="timed sampling transitions")
+    p.add_argument("--warmup", type=int, default=5, help="untimed warmup/adaptation transitions")
+    p.add_argument("--chains", type=int, default=4096, help="total chains over all GPUs")
+    p.add_argument("--rows", type=int, default=581012)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(X, y, seconds, seed=0):
+    """The oracle's per-chain NUTS (NumPy restatement of numpyro's sample kernel, float32)
+    on the full covtype data, for a bounded number of leapfrogs; returns leapfrogs/s."""
+    import numpy as np
+
+    from oracle import hmc_ref as H
+    from oracle import philox
+    from oracle import potentials as OP
+
+    pot = OP.LogisticRegression(X, y, dtype=np.float32)
+    count = [0]
+
+    def pe_grad(z):
+        count[0] += 1
+        return pot.pe_grad(z)
+
+    o = H.NUTSOracle(pe_grad, X.shape[1], 1000, max_tree_depth=10)
+    t0 = time.perf_counter()
+    st = o.init(philox.init_uniform(seed, 0, 0, X.shape[1]), seed, 0)
+    count[0] = 0
+    t0 = time.perf_counter()
+    leap = 0
+    while time.perf_counter() - t0 < seconds:
+        st = o.sample(st)
+        leap = count[0]
+    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": leap / dt, "unit": "leapfrog/s", "cores": threads, "kind": "port",
+            "sample": f"1 chain, full covtype {X.shape[0]}x{X.shape[1]} f32, NumPy oracle NUTS "
+                      f"(oracle/hmc_ref.py), {leap} leapfrogs in {dt:.1f}s, BLAS threads={threads}"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from numpyro_amd import datasets
+    from numpyro_amd import potentials as P
+    from numpyro_amd.infer import MCMC, NUTS, shard_chains
+
+    X, y = datasets.covtype_synthetic(n_rows=args.rows, seed=0)
+    lo, hi = shard_chains(args.chains, rank, world)
+    kernel = NUTS(P.logistic_regression)
+    mcmc = MCMC(kernel, num_warmup=args.warmup, num_samples=args.steps, num_chains=hi - lo,
+                chain_offset=lo, chain_method="vectorized", progress_bar=False,
+                sync_chains=args.sync_chains)
+    Xd = torch.from_numpy(X).to(device)
+    yd = torch.from_numpy(y).to(device)
+    # untimed: init + warmup adaptation
+    mcmc.warmup(args.seed, Xd, yd)
+    eng = mcmc._engine
+    pot = eng.potential
+    # time the potential launches inside the timed region with events on its stream
+    stream = torch.cuda.current_stream()
+    evs = []
+    orig_eval = pot.evaluate
+
+    def timed_eval(ev, s):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        orig_eval(ev, s)
+        b.record(stream)
+        evs.append((a, b))
+
+    pot.evaluate = timed_eval
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mcmc.run(args.seed + 1, Xd, yd, extra_fields=("num_steps",))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    pot.evaluate = orig_eval
+    elapsed = t1 - t0
+    num_steps = mcmc.get_extra_fields()["num_steps"].to(torch.float64).sum()
+    launches = mcmc.last_run_stats["launches"]
+    pot_ms = sum(a.elapsed_time(b) for a, b in evs)
+    stats = torch.tensor([num_steps.item(), elapsed, pot_ms, float(len(evs)), float(launches)],
+                         dtype=torch.float64, device=device)
+    if world > 1:
+        tot = stats.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        useful, elapsed = tot[0].item(), mx[1].item()
+    else:
+        useful = stats[0].item()
+    value = useful / elapsed
+    # dominant kernel: fused logreg potential (two f32 MFMA GEMMs), algorithmic FLOPs per
+    # chain-leapfrog = 4 N D; one launch evaluates every LEAF chain.
+    local_useful = stats[0].item()
+    flop = 4.0 * args.rows * X.shape[1] * local_useful
+    achieved = flop / (pot_ms * 1e-3) / 1e12 if pot_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        traffic = None
+    if rank == 0:
+        out = {
+            "metric": "leapfrog steps/sec across 4096 NUTS chains (covtype LR)",
+            "value": value,
+            "unit": "leapfrog/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic covtype (581012x54 N(0,1) standardized + intercept, y~Bernoulli(sigmoid(X@ref_coefs)))",
+            "config": {"workload": "covtype logistic regression NUTS, diag mass, max_tree_depth 10",
+                       "num_chains": args.chains, "rows": args.rows, "dim": int(X.shape[1]),
+                       "parallelism": f"chains sharded {world}-way (no data-path collective)",
+                       "schedule": "lockstep" if args.sync_chains else "per-chain async"},
+            "useful_leapfrogs": useful,
+            "leapfrog_launches": launches,
+            "potential_ms_per_launch": pot_ms / max(1, len(evs)),
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": MI355X_FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / MI355X_FP32_MFMA_PEAK_TFLOPS,
+                         "traffic": traffic},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(X, y, args.cpu_seconds)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

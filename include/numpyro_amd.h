@@ -37,6 +37,156 @@ enum nmx_status {
 
 int nmx_version(void);
 const char* nmx_last_error(void);
+/* sizeof of the ABI structs (0: nmx_nuts_config, 1: nmx_eval_batch), for binding checks. */
+size_t nmx_struct_size(int which);
+
+/* ======================================================================================
+ * Vectorized-chain NUTS / HMC engine (numpyro/infer/hmc.py + numpyro/infer/hmc_util.py)
+ * ====================================================================================== */
+
+#define NMX_MAX_WINDOWS 32
+#define NMX_MAX_TREE_DEPTH 12
+
+enum nmx_algo { NMX_ALGO_NUTS = 0, NMX_ALGO_HMC = 1 };
+
+/* Per-chain phase codes stored in the arena's `phase` field. */
+enum nmx_phase {
+  NMX_PH_DONE = 0,      /* finished iter_end transitions */
+  NMX_PH_WAIT = 1,      /* sync_chains: waiting for the other chains of this device */
+  NMX_PH_START = 2,     /* will start a new transition at the next nmx_nuts_step */
+  NMX_PH_LEAF = 3,      /* a leapfrog is pending: potential(z_eval) must be evaluated */
+  NMX_PH_INITEVAL = 4,  /* initial point pending evaluation */
+  NMX_PH_NEEDINIT = 5,  /* no valid initial point yet */
+};
+/* Potential kernels evaluate chains whose phase >= NMX_PH_LEAF. */
+
+/* Arena fields (SoA). Vector fields are [D][ldc] float; ckpt fields [max_depth][D][ldc]. */
+enum nmx_field {
+  /* per-chain int32 scalars */
+  NMX_F_PHASE = 0, NMX_F_ITER, NMX_F_DEPTH, NMX_F_SUB_N, NMX_F_DIR, NMX_F_TREE_N,
+  NMX_F_WINDOW_IDX, NMX_F_DA_T, NMX_F_WF_N, NMX_F_TURNING, NMX_F_TREE_DIV, NMX_F_SUB_DIV,
+  NMX_F_HMC_K, NMX_F_HMC_N, NMX_F_LAST_NSTEPS, NMX_F_LAST_DIV, NMX_F_MAXDEPTH_CUR,
+  /* per-chain float scalars */
+  NMX_F_STEP_SIZE, NMX_F_E0, NMX_F_PE, NMX_F_ENERGY, NMX_F_TREE_W, NMX_F_TREE_ACC,
+  NMX_F_SUB_W, NMX_F_SUB_ACC, NMX_F_PE_SUB, NMX_F_E_SUB, NMX_F_DA_XT, NMX_F_DA_XAVG,
+  NMX_F_DA_GAVG, NMX_F_DA_PROX, NMX_F_MEAN_ACC, NMX_F_LAST_ACC, NMX_F_STEP_EFF, NMX_F_PE_EVAL,
+  /* per-chain vectors [D][ldc] */
+  NMX_F_Z, NMX_F_ZGRAD, NMX_F_ZL, NMX_F_RL, NMX_F_GL, NMX_F_ZR, NMX_F_RR, NMX_F_GR,
+  NMX_F_ZSUB, NMX_F_GSUB, NMX_F_RSUM, NMX_F_RSUM_SUB, NMX_F_INV_MASS, NMX_F_MASS_SQRT,
+  NMX_F_WF_MEAN, NMX_F_WF_M2, NMX_F_Z_EVAL, NMX_F_G_EVAL,
+  /* checkpoints [max_depth][D][ldc] */
+  NMX_F_CKPT_R, NMX_F_CKPT_RSUM,
+  /* device counters int32[16]: [0] chains DONE, [1] chains NEEDINIT, [2..] reserved */
+  NMX_F_COUNTERS,
+  /* sync_chains: int32[iter_capacity] #chains that finished transition iter_begin + i */
+  NMX_F_FINISHED,
+  NMX_NUM_FIELDS
+};
+
+/* Collected per-sample scalar fields, layout fields[slot][NMX_NUM_COLLECT][ldc] float. */
+enum nmx_collect {
+  NMX_C_POTENTIAL_ENERGY = 0, NMX_C_ENERGY, NMX_C_ACCEPT_PROB, NMX_C_MEAN_ACCEPT_PROB,
+  NMX_C_STEP_SIZE, NMX_C_NUM_STEPS, NMX_C_DIVERGING, NMX_C_ITER, NMX_NUM_COLLECT
+};
+
+typedef struct nmx_nuts_config {
+  int32_t algo;                  /* nmx_algo */
+  int32_t num_chains;            /* chains on this device (C) */
+  int32_t dim;                   /* flattened latent size (D) */
+  int32_t max_depth_alloc;       /* checkpoint rows allocated (>= both depths below) */
+  int32_t max_tree_depth_warmup; /* hmc.py:299-303 (d1, d2) */
+  int32_t max_tree_depth;
+  int32_t num_warmup;            /* adaptation steps, hmc.py:297 */
+  int32_t iter_end;              /* a chain is DONE after this many transitions */
+  int32_t iter_begin;            /* first transition index of this run (sync counters) */
+  int32_t iter_capacity;         /* rows of NMX_F_FINISHED (>= iter_end - iter_begin) */
+  int32_t adapt_step_size;       /* hmc_util.py:518-707 flags */
+  int32_t adapt_mass_matrix;
+  int32_t regularize_mass_matrix;
+  int32_t dense_mass;            /* must be 0 (diag) in this version */
+  int32_t sync_chains;           /* 1: reference vmap lockstep per transition */
+  float target_accept_prob;
+  float max_delta_energy;        /* hmc.py:188 */
+  float trajectory_length;       /* HMC; <= 0 means None */
+  int32_t num_steps;             /* HMC fixed steps; 0 means None */
+  int32_t num_windows;           /* build_adaptation_schedule(num_warmup), hmc_util.py:387 */
+  int32_t window_end[NMX_MAX_WINDOWS];
+  uint64_t seed;                 /* Philox key */
+  int64_t chain_offset;          /* global id of chain 0 on this device */
+  int32_t collect_start;         /* fori_collect start_idx (util.py:330) */
+  int32_t collect_thinning;
+  int32_t collection_size;       /* slots in samples/fields; 0 disables collection */
+  int32_t ldc;                   /* filled by the library (round_up(C, 64)) */
+} nmx_nuts_config;
+
+/* Arena size/offsets for (C, D, max_depth_alloc, iter_capacity). */
+size_t nmx_nuts_arena_bytes(int num_chains, int dim, int max_depth_alloc, int iter_capacity);
+int nmx_nuts_field_info(int num_chains, int dim, int max_depth_alloc, int iter_capacity,
+                        int field, size_t* offset, size_t* nbytes);
+
+/* Reset adaptation + scalar state: warmup_adapter init_fn (hmc_util.py:546-594) with
+ * step_size and an optional diag inverse mass matrix [D] (NULL = ones).  Sets every chain
+ * to NMX_PH_NEEDINIT, iteration 0. */
+int nmx_nuts_reset(const nmx_nuts_config* cfg, void* arena, float step_size,
+                   const float* inverse_mass_diag, void* stream);
+/* init_to_uniform draw for chains in NEEDINIT (numpyro/infer/initialization.py:95-129,
+ * find_valid_initial_params attempt loop infer/util.py:386-388): z_eval ~ U(-radius, radius),
+ * phase -> INITEVAL. */
+int nmx_nuts_init_draw(const nmx_nuts_config* cfg, void* arena, int attempt, float radius,
+                       void* stream);
+/* User init params z [D][ldc] for every chain: z_eval = z, phase -> INITEVAL. */
+int nmx_nuts_init_from(const nmx_nuts_config* cfg, void* arena, const float* z, void* stream);
+/* Validity check after the potential ran (infer/util.py:437-444): finite U and grad ->
+ * state (z, grad, U) stored, phase START; otherwise NEEDINIT.  counters[1] = #NEEDINIT. */
+int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void* stream);
+/* Set every non-DONE chain with a stored state to START and extend iter_end; used when a
+ * run continues from post_warmup_state / last_state (mcmc.py:664-670). */
+int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream);
+/* One lockstep step of the per-chain NUTS/HMC state machine (sample_kernel hmc.py:459-530
+ * with build_tree hmc_util.py:1088-1180 unrolled into leaves): consumes the potential at
+ * z_eval for LEAF chains, advances trees / transitions / adaptation / collection, and
+ * writes the next z_eval.  samples: [collection_size][D][ldc] (constrained via transform,
+ * int8 [D]: 0 identity, 1 exp); fields: [collection_size][NMX_NUM_COLLECT][ldc]. */
+int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                  const int8_t* transform, void* stream);
+
+/* ======================================================================================
+ * Fused potential-energy + gradient kernels.  Each replaces, for one model,
+ * jax.value_and_grad(potential_fn) (numpyro/infer/hmc_util.py:242-252) over
+ * potential_energy (numpyro/infer/util.py:302-327).  They evaluate every chain whose
+ * phase >= NMX_PH_LEAF and write pe_eval[c] = U(z_c), g_eval[d][c] = dU/dz_d.
+ * ====================================================================================== */
+typedef struct nmx_eval_batch {
+  const float* z;          /* [D][ldc] positions (arena NMX_F_Z_EVAL) */
+  float* grad;             /* [D][ldc] (arena NMX_F_G_EVAL) */
+  float* pe;               /* [ldc]    (arena NMX_F_PE_EVAL) */
+  const int32_t* phase;    /* [ldc]    (arena NMX_F_PHASE); NULL = evaluate every chain */
+  int32_t num_chains;
+  int32_t ldc;
+} nmx_eval_batch;
+
+/* Unnormalized diagonal Gaussian, U = 0.5 sum((z-mu)^2 * prec): the test target of
+ * test/infer/test_mcmc.py:28-72. */
+int nmx_pe_diag_normal(const float* mu, const float* prec, int dim, const nmx_eval_batch* ev,
+                       void* stream);
+/* Eight schools, centred (README.md:47-55), z = (mu, log tau, theta[J]). */
+int nmx_pe_eight_schools(const float* y, const float* sigma, int J, const nmx_eval_batch* ev,
+                         void* stream);
+
+/* Logistic regression (examples/covtype.py:66-71): coefs ~ N(0,1)^D,
+ * obs ~ BernoulliLogits(X @ coefs).  X is first packed (row tiles with the label in a pad
+ * column); U and dU are computed by two f32 MFMA GEMMs per 32-row tile
+ * (X.Z and X^T.(sigmoid(X.Z) - y)) with the logits never leaving registers, per-split
+ * partial slabs, then a fixed-order reduction. */
+size_t nmx_logreg_packed_bytes(int64_t n_rows, int dim);
+int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, int dim, void* packed,
+                    void* stream);
+size_t nmx_logreg_workspace_bytes(int64_t n_rows, int dim, int num_chains);
+int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, const nmx_eval_batch* ev,
+                       void* workspace, void* stream);
+/* Number of row splits the kernel uses for n_rows (depends on n_rows only, so results
+ * do not depend on how many chains or GPUs share the work). */
+int nmx_logreg_num_splits(int64_t n_rows);
 
 /* ---- self tests (no reference counterpart; used by tests and smoke()) ---- */
 /* Philox4x32-10 on device: ctr_key is n x {c0,c1,c2,c3,k0,k1}, out is n x 4 words. */

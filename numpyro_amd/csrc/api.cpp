@@ -24,3 +24,11 @@ int nmx_check_launch(const char* what) {
 extern "C" int nmx_version(void) { return NMX_VERSION; }
 
 extern "C" const char* nmx_last_error(void) { return g_last_error; }
+
+extern "C" size_t nmx_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(nmx_nuts_config);
+    case 1: return sizeof(nmx_eval_batch);
+    default: return 0;
+  }
+}

@@ -1,0 +1,797 @@
+// Vectorized-chain NUTS / HMC as a per-chain state machine on the GPU.
+//
+// The reference builds a NUTS tree with nested lax.while_loops under vmap
+// (numpyro/infer/hmc_util.py:984-1180); under vmap every chain runs until the slowest
+// chain of the batch is done ("lockstep").  Here a tree is unrolled into
+// leaves: one nmx_nuts_step launch consumes one potential evaluation per LEAF chain and
+// advances that chain's tree, transition, adaptation and collection, then writes the next
+// position to evaluate.  A chain whose transition ends starts its next transition in the
+// same launch (sync_chains=0), so the potential kernel always has a full batch; the
+// per-chain computation, and with it every output, is identical to the lockstep
+// schedule (sync_chains=1) because all randomness is keyed per chain (nmx_common.h).
+//
+// Layout: chain-major SoA.  Block = 64 chains x TPC waves; wave w handles coordinates
+// d = w, w+TPC, ... of its 64 chains and dot products are reduced across the TPC waves
+// through LDS in a fixed order (deterministic).
+#include <math.h>
+#include <string.h>
+
+#include "nmx_api_internal.h"
+#include "nmx_common.h"
+
+namespace {
+
+constexpr int MAXD = NMX_MAX_TREE_DEPTH;
+constexpr int NRED = 2 * MAXD + 2;
+constexpr size_t ALIGN = 256;
+
+inline size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+inline int ldc_of(int C) { return (C + 63) / 64 * 64; }
+
+constexpr int NUM_INT_SCALARS = NMX_F_MAXDEPTH_CUR - NMX_F_PHASE + 1;
+constexpr int NUM_FLOAT_SCALARS = NMX_F_PE_EVAL - NMX_F_STEP_SIZE + 1;
+constexpr int NUM_VECTORS = NMX_F_G_EVAL - NMX_F_Z + 1;
+
+size_t field_bytes(int field, int ldc, int D, int MD, int iter_cap) {
+  if (field <= NMX_F_MAXDEPTH_CUR) return (size_t)ldc * 4;
+  if (field <= NMX_F_PE_EVAL) return (size_t)ldc * 4;
+  if (field <= NMX_F_G_EVAL) return (size_t)D * ldc * 4;
+  if (field <= NMX_F_CKPT_RSUM) return (size_t)MD * D * ldc * 4;
+  if (field == NMX_F_COUNTERS) return 16 * 4;
+  if (field == NMX_F_FINISHED) return (size_t)(iter_cap > 0 ? iter_cap : 1) * 4;
+  return 0;
+}
+
+size_t field_offset(int field, int ldc, int D, int MD, int iter_cap) {
+  size_t off = 0;
+  for (int f = 0; f < field; ++f) off += align_up(field_bytes(f, ldc, D, MD, iter_cap));
+  return off;
+}
+
+// Device view of the arena.
+struct Arena {
+  int32_t* is[NUM_INT_SCALARS];
+  float* fs[NUM_FLOAT_SCALARS];
+  float* v[NUM_VECTORS];
+  float* ckr;
+  float* ckrs;
+  int32_t* counters;
+  int32_t* finished;
+};
+
+#define AI(f) a.is[(f) - NMX_F_PHASE]
+#define AF(f) a.fs[(f) - NMX_F_STEP_SIZE]
+#define AV(f) a.v[(f) - NMX_F_Z]
+
+Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
+  Arena a;
+  char* b = (char*)base;
+  for (int f = NMX_F_PHASE; f <= NMX_F_MAXDEPTH_CUR; ++f)
+    a.is[f - NMX_F_PHASE] = (int32_t*)(b + field_offset(f, ldc, D, MD, iter_cap));
+  for (int f = NMX_F_STEP_SIZE; f <= NMX_F_PE_EVAL; ++f)
+    a.fs[f - NMX_F_STEP_SIZE] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
+  for (int f = NMX_F_Z; f <= NMX_F_G_EVAL; ++f)
+    a.v[f - NMX_F_Z] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
+  a.ckr = (float*)(b + field_offset(NMX_F_CKPT_R, ldc, D, MD, iter_cap));
+  a.ckrs = (float*)(b + field_offset(NMX_F_CKPT_RSUM, ldc, D, MD, iter_cap));
+  a.counters = (int32_t*)(b + field_offset(NMX_F_COUNTERS, ldc, D, MD, iter_cap));
+  a.finished = (int32_t*)(b + field_offset(NMX_F_FINISHED, ldc, D, MD, iter_cap));
+  return a;
+}
+
+struct StepArgs {
+  Arena a;
+  nmx_nuts_config cfg;
+  float* samples;
+  float* fields;
+  const int8_t* transform;
+};
+
+// Fixed-order sum of N per-thread partials over the TPC waves of a block (all waves get
+// the total).  Must be reached by every thread of the block.
+template <int TPC, int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], float* lds) {
+  if constexpr (TPC > 1) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < N; ++i) lds[(i * TPC + wv) * 64 + lane] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float s = 0.0f;
+#pragma unroll
+      for (int w = 0; w < TPC; ++w) s += lds[(i * TPC + w) * 64 + lane];
+      v[i] = s;
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ float transform_value(int8_t code, float z) {
+  return code == 1 ? expf(z) : z;
+}
+
+// ---------------------------------------------------------------------------------------
+// The step kernel.
+// ---------------------------------------------------------------------------------------
+template <int TPC>
+__global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
+  __shared__ float lds[TPC > 1 ? NRED * TPC * 64 : 1];
+  const nmx_nuts_config& cfg = A.cfg;
+  Arena& a = A.a;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int ldc = cfg.ldc;
+  const int D = cfg.dim;
+  const bool valid = c < cfg.num_chains;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+
+  int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  if (ph == NMX_PH_WAIT) {
+    const int slot_w = AI(NMX_F_ITER)[c] - 1 - cfg.iter_begin;
+    const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
+                        ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : cfg.num_chains;
+    if (fin >= cfg.num_chains) ph = NMX_PH_START;
+  }
+
+  float* const INVM = AV(NMX_F_INV_MASS);
+  const bool leaf = ph == NMX_PH_LEAF;
+  const int dirR = leaf ? AI(NMX_F_DIR)[c] : 0;
+  const float seff = valid ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
+  float* ZF = dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
+  float* RF = dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  float* GF = dirR ? AV(NMX_F_GR) : AV(NMX_F_GL);
+  float* const ZE = AV(NMX_F_Z_EVAL);
+  float* const GE = AV(NMX_F_G_EVAL);
+
+  // ---------------- L1: finish the pending leapfrog (hmc_util.py:306-308) + kinetic energy
+  float red[NRED];
+#pragma unroll
+  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
+  {
+    const float es = dirR ? seff : -seff;
+    const float half = 0.5f * es;
+    if (leaf) {
+      for (int d = wv; d < D; d += TPC) {
+        const size_t idx = (size_t)d * ldc + c;
+        const float g = GE[idx];
+        const float r = RF[idx] - half * g;
+        RF[idx] = r;
+        ZF[idx] = ZE[idx];
+        GF[idx] = g;
+        red[0] += (INVM[idx] * r) * r;
+      }
+    }
+  }
+  block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
+
+  // leaf scalars (_build_basetree, hmc_util.py:851-894)
+  float pe_new = 0.f, E_new = 0.f, dE = 0.f, w_new = 0.f, acc_new = 0.f;
+  bool div_new = false;
+  if (leaf) {
+    const float ke = 0.5f * red[0];
+    pe_new = AF(NMX_F_PE_EVAL)[c];
+    E_new = pe_new + ke;
+    dE = E_new - AF(NMX_F_E0)[c];
+    if (isnan(dE)) dE = INFINITY;
+    w_new = -dE;
+    div_new = dE > cfg.max_delta_energy;
+    acc_new = fminf(expf(-dE), 1.0f);
+  }
+
+  // next-action flags
+  bool prep_leaf = false;     // continue integrating from the same frontier
+  bool new_doubling = false;  // pick a new direction, then prep_leaf
+  bool iter_done = false;     // transition finished
+  float it_accept = 0.f;
+  int it_nsteps = 0;
+  bool it_div = false;
+
+  // ---------------- NUTS leaf bookkeeping (_iterative_build_subtree body, hmc_util.py:999-1061)
+  const int k = (leaf && is_nuts) ? AI(NMX_F_SUB_N)[c] : 0;
+  const int j = (leaf && is_nuts) ? AI(NMX_F_DEPTH)[c] : 0;
+  bool take_leaf = false;
+  int imin = 1, imax = 0;
+  if (leaf && is_nuts) {
+    float sub_w = AF(NMX_F_SUB_W)[c];
+    float sub_acc = AF(NMX_F_SUB_ACC)[c];
+    if (k == 0) {  // new_tree = new_leaf (:1019-1021)
+      take_leaf = true;
+      sub_w = w_new;
+      sub_acc = acc_new;
+    } else {  // _combine_tree(..., biased_transition=False) (:767-848, :749-753)
+      const float p = nmx_sigmoid(w_new - sub_w);
+      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_LEAF, j, k).x);
+      take_leaf = u < p;
+      sub_w = nmx_logaddexp(sub_w, w_new);
+      sub_acc = sub_acc + acc_new;
+    }
+    AF(NMX_F_SUB_W)[c] = sub_w;
+    AF(NMX_F_SUB_ACC)[c] = sub_acc;
+    AI(NMX_F_SUB_DIV)[c] = div_new;
+    AI(NMX_F_SUB_N)[c] = k + 1;
+    if (take_leaf) {
+      AF(NMX_F_PE_SUB)[c] = pe_new;
+      AF(NMX_F_E_SUB)[c] = E_new;
+    }
+    nmx_leaf_idx_to_ckpt_idxs(k, imin, imax);  // :1036
+  }
+
+  // ---------------- L2: subtree r_sum, proposal copy, checkpoints, turning partial dots
+#pragma unroll
+  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
+  if (leaf && is_nuts) {
+    float* const RS = AV(NMX_F_RSUM_SUB);
+    float* const RST = AV(NMX_F_RSUM);
+    float* const ZS = AV(NMX_F_ZSUB);
+    float* const GS = AV(NMX_F_GSUB);
+    float* const RL = AV(NMX_F_RL);
+    float* const RR = AV(NMX_F_RR);
+    const bool even = (k & 1) == 0;
+    const size_t ck_stride = (size_t)D * ldc;
+    for (int d = wv; d < D; d += TPC) {
+      const size_t idx = (size_t)d * ldc + c;
+      const float r = RF[idx];
+      const float im = INVM[idx];
+      const float rs = (k == 0) ? r : RS[idx] + r;
+      RS[idx] = rs;
+      if (take_leaf) {
+        ZS[idx] = ZF[idx];
+        GS[idx] = GF[idx];
+      }
+      if (even) {  // checkpoint update (:1040-1047)
+        a.ckr[imax * ck_stride + idx] = r;
+        a.ckrs[imax * ck_stride + idx] = rs;
+      }
+      // _is_iterative_turning (:961-981): all checkpoints in [imin, imax]; the reference
+      // stops at the first turning one, the OR below is the same predicate.
+#pragma unroll
+      for (int i = 0; i < MAXD; ++i) {
+        if (i >= imin && i <= imax) {
+          const float rl = a.ckr[i * ck_stride + idx];
+          const float rsub = (rs - a.ckrs[i * ck_stride + idx]) + rl;
+          const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
+          red[2 * i] += (im * rl) * rss;
+          red[2 * i + 1] += (im * r) * rss;
+        }
+      }
+      // tentative whole-tree turning check with the tree's outer momenta (:795-799)
+      const float rst = RST[idx] + rs;
+      const float rlv = dirR ? RL[idx] : r;
+      const float rrv = dirR ? r : RR[idx];
+      const float rss2 = rst - (rlv + rrv) / 2.0f;
+      red[2 * MAXD] += (im * rlv) * rss2;
+      red[2 * MAXD + 1] += (im * rrv) * rss2;
+    }
+  }
+  block_sum<TPC, NRED>(red, lds);
+
+  bool done_sub = false, take_biased = false;
+  if (leaf && is_nuts) {
+    bool turning_sub = false;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i)
+      if (i >= imin && i <= imax) turning_sub |= (red[2 * i] <= 0.0f) | (red[2 * i + 1] <= 0.0f);
+    const int sub_n = k + 1;
+    done_sub = (sub_n >= (1 << j)) || turning_sub || div_new;  // loop exit (:992-997)
+    if (done_sub) {
+      // _double_tree -> _combine_tree(..., biased_transition=True) (:936-938, :756-764)
+      const float sub_w = AF(NMX_F_SUB_W)[c];
+      const float tree_w = AF(NMX_F_TREE_W)[c];
+      const bool turning_tree =
+          turning_sub || (red[2 * MAXD] <= 0.0f) || (red[2 * MAXD + 1] <= 0.0f);
+      float pb = expf(sub_w - tree_w);
+      pb = isnan(pb) ? pb : fminf(pb, 1.0f);  // jnp.clip keeps NaN
+      if (turning_sub || div_new) pb = 0.0f;
+      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_BIASED, j, 0).x);
+      take_biased = u < pb;
+      if (take_biased) {
+        AF(NMX_F_PE)[c] = AF(NMX_F_PE_SUB)[c];
+        AF(NMX_F_ENERGY)[c] = AF(NMX_F_E_SUB)[c];
+      }
+      const int depth = j + 1;
+      const int tree_n = AI(NMX_F_TREE_N)[c] + sub_n;
+      const float tree_acc = AF(NMX_F_TREE_ACC)[c] + AF(NMX_F_SUB_ACC)[c];
+      AI(NMX_F_DEPTH)[c] = depth;
+      AF(NMX_F_TREE_W)[c] = nmx_logaddexp(tree_w, sub_w);
+      AI(NMX_F_TREE_DIV)[c] = div_new;
+      AF(NMX_F_TREE_ACC)[c] = tree_acc;
+      AI(NMX_F_TREE_N)[c] = tree_n;
+      AI(NMX_F_TURNING)[c] = turning_tree;
+      // build_tree loop condition (:1153-1157)
+      if (depth >= AI(NMX_F_MAXDEPTH_CUR)[c] || turning_tree || div_new) {
+        iter_done = true;
+        it_accept = tree_acc / (float)tree_n;  // _nuts_next :441
+        it_nsteps = tree_n;
+        it_div = div_new;
+      } else {
+        new_doubling = true;
+      }
+    } else {
+      prep_leaf = true;
+    }
+  }
+
+  // ---------------- HMC leaf bookkeeping (_hmc_next, hmc.py:364-414)
+  bool hmc_accept = false;
+  if (leaf && !is_nuts) {
+    const int kk = AI(NMX_F_HMC_K)[c] + 1;
+    AI(NMX_F_HMC_K)[c] = kk;
+    const int n = AI(NMX_F_HMC_N)[c];
+    if (kk < n) {
+      prep_leaf = true;
+    } else {
+      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_ACCEPT, 0, 0).x);
+      hmc_accept = u < acc_new;
+      if (hmc_accept) {
+        AF(NMX_F_PE)[c] = pe_new;
+        AF(NMX_F_ENERGY)[c] = E_new;
+      } else {
+        AF(NMX_F_ENERGY)[c] = AF(NMX_F_E0)[c];
+      }
+      iter_done = true;
+      it_accept = acc_new;
+      it_nsteps = n;
+      it_div = div_new;
+    }
+  }
+
+  // ---------------- transition end: adaptation scalars (warmup_adapter update_fn,
+  // hmc_util.py:637-705), mean accept prob (hmc.py:509-513), collection slot.
+  bool wf_update = false, finalize = false;
+  int wf_n = 0, slot = -1;
+  float new_step = 0.f;
+  bool start_iter = ph == NMX_PH_START;
+  if (iter_done) {
+    const int t = AI(NMX_F_ITER)[c];
+    new_step = AF(NMX_F_STEP_SIZE)[c];
+    if (t < cfg.num_warmup) {
+      if (cfg.adapt_step_size) {  // dual_averaging update_fn (:103-126)
+        int da_t = AI(NMX_F_DA_T)[c] + 1;
+        const float g = cfg.target_accept_prob - it_accept;
+        const float tt0 = (float)(da_t + 10);
+        float g_avg = (1.0f - 1.0f / tt0) * AF(NMX_F_DA_GAVG)[c] + g / tt0;
+        const float x_t = AF(NMX_F_DA_PROX)[c] - sqrtf((float)da_t) / 0.05f * g_avg;
+        const float weight_t = powf((float)da_t, -0.75f);
+        const float x_avg = (1.0f - weight_t) * AF(NMX_F_DA_XAVG)[c] + weight_t * x_t;
+        AI(NMX_F_DA_T)[c] = da_t;
+        AF(NMX_F_DA_GAVG)[c] = g_avg;
+        AF(NMX_F_DA_XT)[c] = x_t;
+        AF(NMX_F_DA_XAVG)[c] = x_avg;
+        new_step = (t == cfg.num_warmup - 1) ? expf(x_avg) : expf(x_t);  // :662-666
+        new_step = fminf(fmaxf(new_step, 1.17549435e-38f), 3.40282347e+38f);  // :670-672
+      }
+      const int widx = AI(NMX_F_WINDOW_IDX)[c];
+      const bool middle = (0 < widx) && (widx < cfg.num_windows - 1);
+      wf_update = cfg.adapt_mass_matrix && middle;
+      if (wf_update) wf_n = AI(NMX_F_WF_N)[c] + 1;
+      const bool at_end = t == cfg.window_end[widx];
+      AI(NMX_F_WINDOW_IDX)[c] = widx + (at_end ? 1 : 0);
+      finalize = at_end && middle;  // _update_at_window_end (:596-635)
+      if (finalize && cfg.adapt_step_size) {
+        AF(NMX_F_DA_PROX)[c] = logf(10.0f) + logf(new_step);
+        AF(NMX_F_DA_XT)[c] = 0.0f;
+        AF(NMX_F_DA_XAVG)[c] = 0.0f;
+        AF(NMX_F_DA_GAVG)[c] = 0.0f;
+        AI(NMX_F_DA_T)[c] = 0;
+      }
+      AF(NMX_F_STEP_SIZE)[c] = new_step;
+      AI(NMX_F_WF_N)[c] = (finalize && cfg.adapt_mass_matrix) ? 0 : (wf_update ? wf_n : AI(NMX_F_WF_N)[c]);
+    }
+    const int itr = t + 1;
+    const int nn = t < cfg.num_warmup ? itr : itr - cfg.num_warmup;
+    const float mean_acc = AF(NMX_F_MEAN_ACC)[c];
+    const float mean_new = mean_acc + (it_accept - mean_acc) / (float)nn;
+    AF(NMX_F_MEAN_ACC)[c] = mean_new;
+    AF(NMX_F_LAST_ACC)[c] = it_accept;
+    AI(NMX_F_LAST_NSTEPS)[c] = it_nsteps;
+    AI(NMX_F_LAST_DIV)[c] = it_div;
+    AI(NMX_F_ITER)[c] = itr;
+    // fori_collect slot (numpyro/util.py:330-346): idx = (i - start) // thinning, last write wins
+    if (cfg.collection_size > 0 && t >= cfg.collect_start) {
+      const int off = t - cfg.collect_start;
+      if (off % cfg.collect_thinning == cfg.collect_thinning - 1) {
+        const int s = off / cfg.collect_thinning;
+        if (s < cfg.collection_size) slot = s;
+      }
+    }
+    if (slot >= 0) {
+      float* F = A.fields + (size_t)slot * NMX_NUM_COLLECT * ldc;
+      F[NMX_C_POTENTIAL_ENERGY * ldc + c] = AF(NMX_F_PE)[c];
+      F[NMX_C_ENERGY * ldc + c] = AF(NMX_F_ENERGY)[c];
+      F[NMX_C_ACCEPT_PROB * ldc + c] = it_accept;
+      F[NMX_C_MEAN_ACCEPT_PROB * ldc + c] = mean_new;
+      F[NMX_C_STEP_SIZE * ldc + c] = AF(NMX_F_STEP_SIZE)[c];
+      F[NMX_C_NUM_STEPS * ldc + c] = (float)it_nsteps;
+      F[NMX_C_DIVERGING * ldc + c] = it_div ? 1.0f : 0.0f;
+      F[NMX_C_ITER * ldc + c] = (float)itr;
+    }
+    if (itr >= cfg.iter_end) {
+      AI(NMX_F_PHASE)[c] = NMX_PH_DONE;
+      if (wv == 0) atomicAdd(&a.counters[0], 1);
+    } else if (cfg.sync_chains) {
+      AI(NMX_F_PHASE)[c] = NMX_PH_WAIT;
+      const int fs = t - cfg.iter_begin;
+      if (wv == 0 && fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
+    } else {
+      start_iter = true;
+    }
+  }
+
+  // ---------------- L3/L4: tree r_sum + biased proposal copy; HMC accept copy;
+  //                  Welford update / window finalize; sample collection.
+  const bool l3 = done_sub || hmc_accept || iter_done;
+  if (l3) {
+    float* const ZP = AV(NMX_F_Z);
+    float* const GP = AV(NMX_F_ZGRAD);
+    float* const RST = AV(NMX_F_RSUM);
+    float* const RS = AV(NMX_F_RSUM_SUB);
+    float* const ZS = AV(NMX_F_ZSUB);
+    float* const GS = AV(NMX_F_GSUB);
+    float* const WM = AV(NMX_F_WF_MEAN);
+    float* const W2 = AV(NMX_F_WF_M2);
+    float* const MS = AV(NMX_F_MASS_SQRT);
+    float* const samp = slot >= 0 ? A.samples + (size_t)slot * D * ldc : nullptr;
+    const float wfn = (float)wf_n;
+    for (int d = wv; d < D; d += TPC) {
+      const size_t idx = (size_t)d * ldc + c;
+      if (done_sub) RST[idx] = RST[idx] + RS[idx];
+      if (take_biased) {
+        ZP[idx] = ZS[idx];
+        GP[idx] = GS[idx];
+      }
+      if (hmc_accept) {
+        ZP[idx] = AV(NMX_F_ZR)[idx];
+        GP[idx] = AV(NMX_F_GR)[idx];
+      }
+      if (iter_done) {
+        const float z = ZP[idx];
+        if (wf_update) {  // welford_covariance update_fn, diagonal (:172-196)
+          const float mean = WM[idx];
+          const float delta_pre = z - mean;
+          const float mean_new = mean + delta_pre / wfn;
+          const float delta_post = z - mean_new;
+          WM[idx] = mean_new;
+          W2[idx] = W2[idx] + delta_pre * delta_post;
+        }
+        if (finalize && cfg.adapt_mass_matrix) {  // final_fn (:198-237)
+          float cov = W2[idx] / (float)(wf_n - 1);
+          if (cfg.regularize_mass_matrix) {
+            const float scaled = ((float)wf_n / (float)(wf_n + 5)) * cov;
+            const float shrink = 1e-3f * (5.0f / (float)(wf_n + 5));
+            cov = scaled + shrink;
+          }
+          INVM[idx] = cov;
+          MS[idx] = 1.0f / sqrtf(cov);
+          WM[idx] = 0.0f;
+          W2[idx] = 0.0f;
+        }
+        if (samp) samp[idx] = transform_value(A.transform[d], z);
+      }
+    }
+  }
+
+  // ---------------- new transition: momentum, tree init (sample_kernel hmc.py:471-481,
+  // build_tree :1127-1151), first direction; new doubling direction (:1160-1162).
+  int new_dir = dirR;
+  float step_eff = seff;
+  if (start_iter) {
+    const int it = AI(NMX_F_ITER)[c];
+    const float step = AF(NMX_F_STEP_SIZE)[c];
+    if (is_nuts) {
+      step_eff = step;
+      AI(NMX_F_MAXDEPTH_CUR)[c] =
+          it < cfg.num_warmup ? cfg.max_tree_depth_warmup : cfg.max_tree_depth;  // hmc.py:488-490
+      new_dir = nmx_u01(nmx_rng(seed, gch, it, NMX_EV_DIRECTION, 0, 0).x) < 0.5f;
+    } else {
+      int n;
+      if (cfg.num_steps > 0) n = cfg.num_steps;
+      else n = (int)ceilf(cfg.trajectory_length / step);  // _get_num_steps hmc.py:85-89
+      n = n < 1 ? 1 : n;
+      step_eff = cfg.trajectory_length > 0.0f ? cfg.trajectory_length / (float)n : step;
+      AI(NMX_F_HMC_N)[c] = n;
+      AI(NMX_F_HMC_K)[c] = 0;
+      new_dir = 1;
+    }
+    AF(NMX_F_STEP_EFF)[c] = step_eff;
+    AI(NMX_F_DEPTH)[c] = 0;
+    AI(NMX_F_SUB_N)[c] = 0;
+    AI(NMX_F_TREE_N)[c] = 0;
+    AI(NMX_F_TURNING)[c] = 0;
+    AI(NMX_F_TREE_DIV)[c] = 0;
+    AF(NMX_F_TREE_W)[c] = 0.0f;
+    AF(NMX_F_TREE_ACC)[c] = 0.0f;
+    AI(NMX_F_DIR)[c] = new_dir;
+    AI(NMX_F_PHASE)[c] = NMX_PH_LEAF;
+  } else if (new_doubling) {
+    const int depth = AI(NMX_F_DEPTH)[c];
+    new_dir = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_DIRECTION, depth, 0).x) < 0.5f;
+    AI(NMX_F_DIR)[c] = new_dir;
+    AI(NMX_F_SUB_N)[c] = 0;
+    prep_leaf = true;
+  }
+
+  // ---------------- L5: momentum draw + tree init; L6: half momentum step and the next
+  // position z_eval (velocity_verlet update_fn first half, hmc_util.py:297-301).
+#pragma unroll
+  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
+  if (start_iter || prep_leaf) {
+    float* const ZFn = new_dir ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
+    float* const RFn = new_dir ? AV(NMX_F_RR) : AV(NMX_F_RL);
+    float* const GFn = new_dir ? AV(NMX_F_GR) : AV(NMX_F_GL);
+    float* const ZO = new_dir ? AV(NMX_F_ZL) : AV(NMX_F_ZR);
+    float* const RO = new_dir ? AV(NMX_F_RL) : AV(NMX_F_RR);
+    float* const GO = new_dir ? AV(NMX_F_GL) : AV(NMX_F_GR);
+    const float es = new_dir ? step_eff : -step_eff;
+    const float half = 0.5f * es;
+    if (start_iter) {
+      float* const ZP = AV(NMX_F_Z);
+      float* const GP = AV(NMX_F_ZGRAD);
+      float* const MS = AV(NMX_F_MASS_SQRT);
+      float* const RST = AV(NMX_F_RSUM);
+      const uint32_t it = (uint32_t)AI(NMX_F_ITER)[c];
+      // blocks of 4 coordinates share one Philox call (momentum_generator hmc.py:92-110)
+      for (int blk = wv; 4 * blk < D; blk += TPC) {
+        const nmx_u4 x = nmx_rng(seed, gch, it, NMX_EV_MOMENTUM, blk, 0);
+        float n[4];
+        nmx_box_muller(x.x, x.y, n[0], n[1]);
+        nmx_box_muller(x.z, x.w, n[2], n[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * blk + q;
+          if (d < D) {
+            const size_t idx = (size_t)d * ldc + c;
+            const float r = MS[idx] * n[q];
+            const float z = ZP[idx];
+            const float g = GP[idx];
+            const float im = INVM[idx];
+            red[0] += (im * r) * r;
+            RST[idx] = r;
+            ZO[idx] = z;
+            GO[idx] = g;
+            RO[idx] = r;
+            ZFn[idx] = z;
+            GFn[idx] = g;
+            const float rh = r - half * g;
+            RFn[idx] = rh;
+            ZE[idx] = z + es * (im * rh);
+          }
+        }
+      }
+    } else {
+      for (int d = wv; d < D; d += TPC) {
+        const size_t idx = (size_t)d * ldc + c;
+        const float rh = RFn[idx] - half * GFn[idx];
+        RFn[idx] = rh;
+        ZE[idx] = ZFn[idx] + es * (INVM[idx] * rh);
+      }
+      AI(NMX_F_PHASE)[c] = NMX_PH_LEAF;
+    }
+  }
+  block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
+  if (start_iter) {
+    const float E0 = AF(NMX_F_PE)[c] + 0.5f * red[0];  // build_tree :1130
+    AF(NMX_F_E0)[c] = E0;
+    AF(NMX_F_ENERGY)[c] = E0;  // proposal energy of the initial tree (:1137)
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Reset / init kernels
+// ---------------------------------------------------------------------------------------
+__global__ void k_nuts_reset(Arena a, nmx_nuts_config cfg, float step_size, const float* imm) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ldc = cfg.ldc;
+  if (c < ldc) {
+    const bool valid = c < cfg.num_chains;
+    for (int f = 0; f < NUM_INT_SCALARS; ++f) a.is[f][c] = 0;
+    for (int f = 0; f < NUM_FLOAT_SCALARS; ++f) a.fs[f][c] = 0.0f;
+    AI(NMX_F_PHASE)[c] = valid ? NMX_PH_NEEDINIT : NMX_PH_DONE;
+    AF(NMX_F_STEP_SIZE)[c] = step_size;
+    AF(NMX_F_STEP_EFF)[c] = step_size;
+    AF(NMX_F_DA_PROX)[c] = logf(10.0f * step_size);  // warmup_adapter init_fn :576
+    for (int d = 0; d < cfg.dim; ++d) {
+      const size_t idx = (size_t)d * ldc + c;
+      const float im = imm ? imm[d] : 1.0f;
+      AV(NMX_F_INV_MASS)[idx] = im;
+      // _initialize_mass_matrix diag branch (:507-512): sqrt_inv = sqrt(imm), sqrt = 1/that
+      AV(NMX_F_MASS_SQRT)[idx] = imm ? 1.0f / sqrtf(im) : 1.0f;
+      AV(NMX_F_WF_MEAN)[idx] = 0.0f;
+      AV(NMX_F_WF_M2)[idx] = 0.0f;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 16) a.counters[threadIdx.x] = 0;
+  for (int i = c; i < cfg.iter_capacity; i += gridDim.x * blockDim.x) a.finished[i] = 0;
+}
+
+__global__ void k_nuts_init_draw(Arena a, nmx_nuts_config cfg, int attempt, float radius) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cfg.num_chains) return;
+  if (AI(NMX_F_PHASE)[c] != NMX_PH_NEEDINIT) return;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const int ldc = cfg.ldc;
+  for (int blk = 0; 4 * blk < cfg.dim; ++blk) {
+    const nmx_u4 x = nmx_rng(cfg.seed, gch, 0, NMX_EV_INIT, blk, (uint32_t)attempt);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = 4 * blk + q;
+      if (d < cfg.dim) AV(NMX_F_Z_EVAL)[(size_t)d * ldc + c] = (2.0f * radius) * nmx_u01(w[q]) - radius;
+    }
+  }
+  AI(NMX_F_PHASE)[c] = NMX_PH_INITEVAL;
+}
+
+__global__ void k_nuts_init_from(Arena a, nmx_nuts_config cfg, const float* z) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cfg.num_chains) return;
+  const int ldc = cfg.ldc;
+  for (int d = 0; d < cfg.dim; ++d) AV(NMX_F_Z_EVAL)[(size_t)d * ldc + c] = z[(size_t)d * ldc + c];
+  AI(NMX_F_PHASE)[c] = NMX_PH_INITEVAL;
+}
+
+__global__ void k_nuts_init_check(Arena a, nmx_nuts_config cfg) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cfg.num_chains) return;
+  const int ph = AI(NMX_F_PHASE)[c];
+  if (ph == NMX_PH_INITEVAL) {
+    const int ldc = cfg.ldc;
+    const float pe = AF(NMX_F_PE_EVAL)[c];
+    bool ok = isfinite(pe);
+    for (int d = 0; d < cfg.dim; ++d) ok = ok && isfinite(AV(NMX_F_G_EVAL)[(size_t)d * ldc + c]);
+    if (ok) {
+      for (int d = 0; d < cfg.dim; ++d) {
+        const size_t idx = (size_t)d * ldc + c;
+        AV(NMX_F_Z)[idx] = AV(NMX_F_Z_EVAL)[idx];
+        AV(NMX_F_ZGRAD)[idx] = AV(NMX_F_G_EVAL)[idx];
+      }
+      AF(NMX_F_PE)[c] = pe;
+      AF(NMX_F_ENERGY)[c] = pe;
+      AI(NMX_F_PHASE)[c] = NMX_PH_START;
+    } else {
+      AI(NMX_F_PHASE)[c] = NMX_PH_NEEDINIT;
+      atomicAdd(&a.counters[1], 1);
+    }
+  } else if (ph == NMX_PH_NEEDINIT) {
+    atomicAdd(&a.counters[1], 1);
+  }
+}
+
+__global__ void k_nuts_resume(Arena a, nmx_nuts_config cfg) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 16) a.counters[threadIdx.x] = 0;
+  for (int i = c; i < cfg.iter_capacity; i += gridDim.x * blockDim.x) a.finished[i] = 0;
+  if (c >= cfg.num_chains) return;
+  const int ph = AI(NMX_F_PHASE)[c];
+  if (ph == NMX_PH_DONE || ph == NMX_PH_WAIT || ph == NMX_PH_START) AI(NMX_F_PHASE)[c] = NMX_PH_START;
+}
+
+int validate(const nmx_nuts_config* cfg) {
+  if (!cfg) return nmx_fail(NMX_ERR_INVALID, "config is NULL");
+  if (cfg->num_chains <= 0 || cfg->dim <= 0) return nmx_fail(NMX_ERR_INVALID, "num_chains and dim must be positive");
+  if (cfg->algo != NMX_ALGO_NUTS && cfg->algo != NMX_ALGO_HMC)
+    return nmx_fail(NMX_ERR_INVALID, "algo must be NUTS(0) or HMC(1)");
+  if (cfg->dense_mass) return nmx_fail(NMX_ERR_UNSUPPORTED, "dense_mass is not supported by this engine build");
+  const int md = cfg->max_tree_depth > cfg->max_tree_depth_warmup ? cfg->max_tree_depth : cfg->max_tree_depth_warmup;
+  if (cfg->algo == NMX_ALGO_NUTS) {
+    if (cfg->max_tree_depth < 1 || cfg->max_tree_depth_warmup < 1)
+      return nmx_fail(NMX_ERR_INVALID, "max_tree_depth must be >= 1");
+    if (md > NMX_MAX_TREE_DEPTH || md > cfg->max_depth_alloc)
+      return nmx_fail(NMX_ERR_INVALID, "max_tree_depth %d exceeds allocation (%d, limit %d)", md,
+                      cfg->max_depth_alloc, NMX_MAX_TREE_DEPTH);
+  }
+  if (cfg->num_windows < 1 || cfg->num_windows > NMX_MAX_WINDOWS)
+    return nmx_fail(NMX_ERR_INVALID, "num_windows out of range");
+  if (cfg->collect_thinning < 1) return nmx_fail(NMX_ERR_INVALID, "collect_thinning must be >= 1");
+  if (cfg->sync_chains && cfg->iter_capacity < cfg->iter_end - cfg->iter_begin)
+    return nmx_fail(NMX_ERR_INVALID, "sync_chains needs iter_capacity >= iter_end - iter_begin");
+  if (cfg->algo == NMX_ALGO_HMC && cfg->num_steps <= 0 && !(cfg->trajectory_length > 0.0f))
+    return nmx_fail(NMX_ERR_INVALID, "HMC needs num_steps or trajectory_length");
+  if (cfg->ldc != ldc_of(cfg->num_chains))
+    return nmx_fail(NMX_ERR_INVALID, "cfg.ldc must be round_up(num_chains, 64) = %d", ldc_of(cfg->num_chains));
+  return NMX_OK;
+}
+
+Arena arena_of(const nmx_nuts_config* cfg, void* base) {
+  return make_arena(base, cfg->ldc, cfg->dim, cfg->max_depth_alloc, cfg->iter_capacity);
+}
+
+int tpc_for_dim(int D) {
+  if (D <= 64) return 1;
+  if (D <= 1024) return 4;
+  return 16;
+}
+
+}  // namespace
+
+extern "C" size_t nmx_nuts_arena_bytes(int num_chains, int dim, int max_depth_alloc, int iter_capacity) {
+  const int ldc = ldc_of(num_chains);
+  return field_offset(NMX_NUM_FIELDS, ldc, dim, max_depth_alloc, iter_capacity);
+}
+
+extern "C" int nmx_nuts_field_info(int num_chains, int dim, int max_depth_alloc, int iter_capacity,
+                                   int field, size_t* offset, size_t* nbytes) {
+  if (field < 0 || field >= NMX_NUM_FIELDS) return nmx_fail(NMX_ERR_INVALID, "bad field %d", field);
+  const int ldc = ldc_of(num_chains);
+  if (offset) *offset = field_offset(field, ldc, dim, max_depth_alloc, iter_capacity);
+  if (nbytes) *nbytes = field_bytes(field, ldc, dim, max_depth_alloc, iter_capacity);
+  return NMX_OK;
+}
+
+extern "C" int nmx_nuts_reset(const nmx_nuts_config* cfg, void* arena, float step_size,
+                              const float* inverse_mass_diag, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
+  Arena a = arena_of(cfg, arena);
+  const int grid = (cfg->ldc + 63) / 64;
+  hipLaunchKernelGGL(k_nuts_reset, dim3(grid), dim3(64), 0, (hipStream_t)stream, a, *cfg,
+                     step_size, inverse_mass_diag);
+  return nmx_check_launch("k_nuts_reset");
+}
+
+extern "C" int nmx_nuts_init_draw(const nmx_nuts_config* cfg, void* arena, int attempt, float radius,
+                                  void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  hipLaunchKernelGGL(k_nuts_init_draw, dim3((cfg->num_chains + 63) / 64), dim3(64), 0,
+                     (hipStream_t)stream, a, *cfg, attempt, radius);
+  return nmx_check_launch("k_nuts_init_draw");
+}
+
+extern "C" int nmx_nuts_init_from(const nmx_nuts_config* cfg, void* arena, const float* z, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!z) return nmx_fail(NMX_ERR_INVALID, "z is NULL");
+  Arena a = arena_of(cfg, arena);
+  hipLaunchKernelGGL(k_nuts_init_from, dim3((cfg->num_chains + 63) / 64), dim3(64), 0,
+                     (hipStream_t)stream, a, *cfg, z);
+  return nmx_check_launch("k_nuts_init_from");
+}
+
+extern "C" int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream);
+  hipLaunchKernelGGL(k_nuts_init_check, dim3((cfg->num_chains + 63) / 64), dim3(64), 0,
+                     (hipStream_t)stream, a, *cfg);
+  return nmx_check_launch("k_nuts_init_check");
+}
+
+extern "C" int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  hipLaunchKernelGGL(k_nuts_resume, dim3((cfg->ldc + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     a, *cfg);
+  return nmx_check_launch("k_nuts_resume");
+}
+
+extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                             const int8_t* transform, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
+  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+    return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
+  StepArgs args;
+  args.a = arena_of(cfg, arena);
+  args.cfg = *cfg;
+  args.samples = samples;
+  args.fields = fields;
+  args.transform = transform;
+  const int grid = cfg->ldc / 64;
+  hipStream_t s = (hipStream_t)stream;
+  switch (tpc_for_dim(cfg->dim)) {
+    case 1: hipLaunchKernelGGL(k_nuts_step<1>, dim3(grid), dim3(64), 0, s, args); break;
+    case 4: hipLaunchKernelGGL(k_nuts_step<4>, dim3(grid), dim3(256), 0, s, args); break;
+    default: hipLaunchKernelGGL(k_nuts_step<16>, dim3(grid), dim3(1024), 0, s, args); break;
+  }
+  return nmx_check_launch("k_nuts_step");
+}

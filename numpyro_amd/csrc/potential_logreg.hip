@@ -1,0 +1,270 @@
+// Logistic-regression potential + gradient for thousands of chains (examples/covtype.py:66-71).
+//
+//   U(b)  = sum_n [max(l_n,0) + log1p(exp(-|l_n|)) - y_n l_n] + sum_d [b_d^2/2 + log(2pi)/2]
+//   dU/db = X^T (sigmoid(l) - y) + b,      l = X b          
+//
+// For a 32-row tile and 32 chains a wave computes L = X.Z with v_mfma_f32_32x32x2_f32
+// (exact f32 fma chains), applies the Bernoulli epilogue to the accumulator registers in
+// place, and feeds those same registers as the B operand of G += X^T.R: the 32x32 result
+// holds chains on the lane and rows in the registers, and the 32x32x2 B operand wants
+// exactly (row pair, chain) on (lane half, lane) -- no shuffle, no LDS round trip, and the
+// N x C logit matrix never exists in memory.
+//
+// Packed X (nmx_logreg_pack): 64-row tiles, each row K+1 floats (K = round_up(D, 2)):
+// x_0..x_{D-1}, zero pad up to K, then the label y.  The odd row stride K+1 makes the
+// GEMM1 operand read (32 lanes = 32 rows, same column) bank-conflict free and puts the
+// label next to its row.  A tile is one contiguous block, copied to LDS with 16-byte loads.
+//
+// Work split: grid = chain groups (128 chains = 4 waves) x S row splits.  S depends on
+// n_rows only, and each split sums its rows in a fixed order, so a chain's U and dU do
+// not depend on how many chains share the launch (GPU-count invariance).  Per-split
+// partials go to slabs reduced in fixed order by k_logreg_finalize.  Workgroups of the
+// same split are placed on one XCD (blockIdx % 8) so the chain groups share X tiles in L2.
+#include <math.h>
+
+#include "nmx_api_internal.h"
+#include "nmx_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BR = 64;       // rows per LDS stage
+constexpr int NW = 4;        // waves per workgroup
+constexpr int CPB = NW * 32; // chains per workgroup
+constexpr int MAX_S = 128;   // row splits
+constexpr int LDS_SLACK = 64;
+
+inline int k_of(int D) { return (D + 1) / 2 * 2; }
+inline int xs_of(int D) { return k_of(D) + 1; }
+inline int64_t ntiles_of(int64_t n) { return (n + BR - 1) / BR; }
+
+int num_splits(int64_t n_rows) {
+  int64_t t = ntiles_of(n_rows);
+  int64_t s = t / 16;
+  s = s / 8 * 8;
+  if (s < 8) s = 8;
+  if (s > MAX_S) s = MAX_S;
+  return (int)s;
+}
+
+__global__ void k_logreg_pack(const float* X, const float* y, int64_t n, int D, int XS, int64_t npad,
+                              float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = npad * XS;
+  if (i >= total) return;
+  const int64_t row = i / XS;
+  const int k = (int)(i - row * XS);
+  float v = 0.0f;
+  if (row < n) {
+    if (k < D) v = X[row * D + k];
+    else if (k == XS - 1) v = y[row];
+  }
+  out[i] = v;
+}
+
+// KS = K/2 MFMA k-steps.  EXACT: the dim's KS equals the template (compile-time strides);
+// otherwise KS is an upper bound and the packed stride comes at run time.
+template <int KS, bool EXACT>
+__global__ __launch_bounds__(NW * 64) void k_logreg_tiles(const float* __restrict__ Xp, int64_t n_rows,
+                                                          int ntiles, int D, int S, int Gc,
+                                                          nmx_eval_batch ev, float* __restrict__ gpart,
+                                                          double* __restrict__ pepart) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int ks = EXACT ? KS : (D + 1) / 2;
+  const int XS = EXACT ? 2 * KS + 1 : 2 * ks + 1;
+  const int b = blockIdx.x;
+  const int xcd = b & 7;
+  const int q = b >> 3;
+  const int cg = q % Gc;
+  const int split = (q / Gc) * 8 + xcd;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int c = cg * CPB + w * 32 + l31;
+  const bool cin = c < ldc;
+  const bool act = c < ev.num_chains && (ev.phase == nullptr || ev.phase[c] >= NMX_PH_LEAF);
+  const bool wave_active = __any(act);
+  if (!__syncthreads_or(wave_active)) return;
+
+  if (tid < LDS_SLACK) xs[BR * XS + tid] = 0.0f;
+
+  const int per = (ntiles + S - 1) / S;
+  const int t0 = split * per;
+  const int t1 = min(t0 + per, ntiles);
+
+  // B operand of GEMM1 for this wave's 32 chains: Z[k = 2s + h][chain]
+  float zb[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    zb[s] = (k < D && cin) ? ev.z[(size_t)k * ldc + c] : 0.0f;
+  }
+  f32x16 g0, g1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    g0[r] = 0.0f;
+    g1[r] = 0.0f;
+  }
+  double pe = 0.0;
+  const bool two_blocks = D > 32;
+
+  for (int t = t0; t < t1; ++t) {
+    __syncthreads();
+    {
+      const float4* src = reinterpret_cast<const float4*>(Xp + (size_t)t * BR * XS);
+      float4* dst = reinterpret_cast<float4*>(xs);
+      const int NCH = BR * XS / 4;
+      for (int i = tid; i < NCH; i += NW * 64) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (!wave_active) continue;
+#pragma unroll 1
+    for (int sub = 0; sub < BR / 32; ++sub) {
+      const float* xt = xs + sub * 32 * XS;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        if (EXACT || s < ks)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[s], acc, 0, 0, 0);
+      // Bernoulli-logits epilogue in place: acc[r] <- sigmoid(l) - y (masked past n_rows)
+      const int64_t rowbase = (int64_t)t * BR + sub * 32;
+      float pes = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float y = xt[rr * XS + (XS - 1)];
+        const float lg = acc[r];
+        const bool ok = rowbase + rr < n_rows;
+        const float e = __expf(-fabsf(lg));
+        const float onepe = 1.0f + e;
+        const float bce = fmaxf(lg, 0.0f) + __logf(onepe) - lg * y;  // util.py:295-298
+        const float inv = __builtin_amdgcn_rcpf(onepe);
+        const float sig = lg >= 0.0f ? inv : e * inv;
+        pes += ok ? bce : 0.0f;
+        acc[r] = ok ? sig - y : 0.0f;
+      }
+      pe += (double)pes;
+      // G += X^T R: A[d][row] from LDS, B = the epilogue registers
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], acc[r], g0, 0, 0, 0);
+        if (two_blocks)
+          g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], acc[r], g1, 0, 0, 0);
+      }
+    }
+  }
+
+  if (wave_active && cin) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (d < D) gpart[((size_t)split * D + d) * ldc + c] = g0[r];
+      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + c] = g1[r];
+    }
+  }
+  pe += __shfl_xor(pe, 32);
+  if (wave_active && cin && h == 0) pepart[(size_t)split * ldc + c] = pe;
+}
+
+__global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
+                                  int D, nmx_eval_batch ev) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int d = blockIdx.y;
+  if (c >= ev.num_chains) return;
+  if (ev.phase && ev.phase[c] < NMX_PH_LEAF) return;
+  const int ldc = ev.ldc;
+  if (d < D) {
+    float s = 0.0f;
+    for (int sp = 0; sp < S; ++sp) s += gpart[((size_t)sp * D + d) * ldc + c];
+    const size_t idx = (size_t)d * ldc + c;
+    ev.grad[idx] = s + ev.z[idx];
+  } else {
+    double s = 0.0;
+    for (int sp = 0; sp < S; ++sp) s += pepart[(size_t)sp * ldc + c];
+    double zz = 0.0;
+    for (int k = 0; k < D; ++k) {
+      const double z = ev.z[(size_t)k * ldc + c];
+      zz += z * z;
+    }
+    ev.pe[c] = (float)(s + 0.5 * zz + 0.9189385332046727 * D);
+  }
+}
+
+int check_ev(const nmx_eval_batch* ev) {
+  if (!ev || !ev->z || !ev->grad || !ev->pe) return nmx_fail(NMX_ERR_INVALID, "eval batch has NULL pointers");
+  if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
+    return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
+  return NMX_OK;
+}
+
+template <int KS, bool EXACT>
+void launch_tiles(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
+                  double* pepart, hipStream_t s) {
+  const int ntiles = (int)ntiles_of(n_rows);
+  const int S = num_splits(n_rows);
+  const int Gc = (ev->ldc + CPB - 1) / CPB;
+  const size_t lds = (size_t)(BR * xs_of(D) + LDS_SLACK) * sizeof(float);
+  hipLaunchKernelGGL((k_logreg_tiles<KS, EXACT>), dim3(Gc * S), dim3(NW * 64), lds, s, Xp, n_rows, ntiles, D,
+                     S, Gc, *ev, gpart, pepart);
+}
+
+}  // namespace
+
+extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return num_splits(n_rows); }
+
+extern "C" size_t nmx_logreg_packed_bytes(int64_t n_rows, int dim) {
+  if (n_rows <= 0 || dim <= 0) return 0;
+  return (size_t)(ntiles_of(n_rows) * BR) * xs_of(dim) * sizeof(float);
+}
+
+extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, int dim, void* packed,
+                               void* stream) {
+  if (!X || !y || !packed) return nmx_fail(NMX_ERR_INVALID, "logreg_pack: NULL pointer");
+  if (n_rows <= 0 || dim <= 0 || dim > 64)
+    return nmx_fail(NMX_ERR_INVALID, "logreg_pack: need n_rows > 0 and 0 < dim <= 64 (got %lld, %d)",
+                    (long long)n_rows, dim);
+  const int XS = xs_of(dim);
+  const int64_t npad = ntiles_of(n_rows) * BR;
+  const int64_t total = npad * XS;
+  hipLaunchKernelGGL(k_logreg_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     X, y, n_rows, dim, XS, npad, (float*)packed);
+  return nmx_check_launch("k_logreg_pack");
+}
+
+extern "C" size_t nmx_logreg_workspace_bytes(int64_t n_rows, int dim, int num_chains) {
+  const size_t ldc = (size_t)(num_chains + 63) / 64 * 64;
+  const size_t S = num_splits(n_rows);
+  const size_t g = S * dim * ldc * sizeof(float);
+  const size_t p = S * ldc * sizeof(double);
+  return (g + 255) / 256 * 256 + p;
+}
+
+extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, const nmx_eval_batch* ev,
+                                  void* workspace, void* stream) {
+  if (int st = check_ev(ev)) return st;
+  if (!packed || !workspace) return nmx_fail(NMX_ERR_INVALID, "logreg_pe_grad: NULL packed/workspace");
+  if (n_rows <= 0 || dim <= 0 || dim > 64)
+    return nmx_fail(NMX_ERR_INVALID, "logreg_pe_grad: need 0 < dim <= 64 (got %d)", dim);
+  hipStream_t s = (hipStream_t)stream;
+  const int S = num_splits(n_rows);
+  const size_t gbytes = (size_t)S * dim * ev->ldc * sizeof(float);
+  float* gpart = (float*)workspace;
+  double* pepart = (double*)((char*)workspace + (gbytes + 255) / 256 * 256);
+  const float* Xp = (const float*)packed;
+  const int KS = k_of(dim) / 2;
+  if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
+  else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS <= 16) launch_tiles<16, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else launch_tiles<32, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  if (int st = nmx_check_launch("k_logreg_tiles")) return st;
+  hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S, dim, *ev);
+  return nmx_check_launch("k_logreg_finalize");
+}

@@ -1,0 +1,264 @@
+"""Host driver of the device NUTS/HMC state machine (csrc/nuts.hip).
+
+All chain state lives in one device arena (a torch uint8 tensor) laid out by the library;
+this module owns the arena, the collection buffers and the launch loop
+
+    nuts_step -> [potential -> nuts_step] * n      (until every chain is DONE)
+
+and never touches chain state on the host.  It corresponds to the reference's
+``fori_collect`` loop over ``sample_kernel`` (numpyro/util.py:277-407,
+numpyro/infer/hmc.py:459-530) with ``progress_bar=False``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import native
+from .native import NutsConfig, EvalBatch, check, lib, ptr, stream_ptr
+
+INIT_ATTEMPTS = 100  # find_valid_initial_params (numpyro/infer/util.py:386-388)
+
+
+def build_adaptation_schedule(num_steps):
+    """Stan windows, numpyro/infer/hmc_util.py:387-436 (host-side; sent to the device)."""
+    schedule = []
+    if num_steps < 20:
+        schedule.append((0, num_steps - 1))
+        return schedule
+    start_buffer, end_buffer, init_window = 75, 50, 25
+    if start_buffer + end_buffer + init_window > num_steps:
+        start_buffer = int(0.15 * num_steps)
+        end_buffer = int(0.1 * num_steps)
+        init_window = num_steps - start_buffer - end_buffer
+    schedule.append((0, start_buffer - 1))
+    end_window_start = num_steps - end_buffer
+    next_size, next_start = init_window, start_buffer
+    while next_start < end_window_start:
+        cur_start, cur_size = next_start, next_size
+        if 3 * cur_size <= end_window_start - cur_start:
+            next_size = 2 * cur_size
+        else:
+            cur_size = end_window_start - cur_start
+        next_start = cur_start + cur_size
+        schedule.append((cur_start, next_start - 1))
+    schedule.append((end_window_start, num_steps - 1))
+    return schedule
+
+
+@dataclass
+class SamplerOptions:
+    algo: int = native.ALGO_NUTS
+    step_size: float = 1.0
+    adapt_step_size: bool = True
+    adapt_mass_matrix: bool = True
+    dense_mass: bool = False
+    target_accept_prob: float = 0.8
+    max_tree_depth: tuple = (10, 10)
+    trajectory_length: float | None = 2 * math.pi
+    num_steps: int | None = None
+    regularize_mass_matrix: bool = True
+    max_delta_energy: float = 1000.0
+    inverse_mass_matrix: object = None  # diag [D] or None
+
+
+class Engine:
+    """Chains of one device: arena + potential + launch loop."""
+
+    def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
+                 chain_offset: int = 0, sync_chains: bool = False):
+        if opts.dense_mass:
+            raise NotImplementedError("dense_mass=True is not supported by this engine build")
+        self.potential = potential
+        self.C = int(num_chains)
+        self.D = int(potential.dim)
+        self.opts = opts
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ldc = (self.C + 63) // 64 * 64
+        self.md = max(opts.max_tree_depth) if opts.algo == native.ALGO_NUTS else 1
+        if self.md > native.MAX_TREE_DEPTH:
+            raise ValueError(f"max_tree_depth {self.md} > {native.MAX_TREE_DEPTH}")
+        self.chain_offset = int(chain_offset)
+        self.sync_chains = bool(sync_chains)
+        self.iter_capacity = 1
+        self.arena = None
+        self._views = {}
+        self.iteration = 0  # transitions completed by every chain
+        self.num_warmup = 0
+        self.cfg = NutsConfig()
+        self.potential.bind(self.C, self.ldc, self.device)
+
+    # ------------------------------------------------------------------ arena
+    def _alloc(self, iter_capacity: int):
+        self.iter_capacity = max(1, int(iter_capacity))
+        nbytes = lib().nmx_nuts_arena_bytes(self.C, self.D, self.md, self.iter_capacity)
+        self.arena = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        self._views = {}
+        self.eval_batch = EvalBatch(ptr(self.view("z_eval")), ptr(self.view("g_eval")),
+                                    ptr(self.view("pe_eval")), ptr(self.view("phase")),
+                                    self.C, self.ldc)
+
+    def view(self, name: str):
+        """torch view of an arena field: scalars [ldc], vectors [D, ldc], ckpts [md, D, ldc]."""
+        if name in self._views:
+            return self._views[name]
+        off, nb = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().nmx_nuts_field_info(self.C, self.D, self.md, self.iter_capacity,
+                                        native.FIELD_ID[name], ctypes.byref(off), ctypes.byref(nb)))
+        raw = self.arena[off.value:off.value + nb.value]
+        t = raw.view(torch.int32 if name in native.INT_FIELDS else torch.float32)
+        if name in native.VECTOR_FIELDS:
+            t = t.view(self.D, self.ldc)
+        elif name in native.CKPT_FIELDS:
+            t = t.view(self.md, self.D, self.ldc)
+        self._views[name] = t
+        return t
+
+    # ------------------------------------------------------------------ config
+    def _fill_cfg(self, iter_begin, iter_end, num_warmup, seed, collect_start, thinning, collection_size):
+        o, c = self.opts, self.cfg
+        c.algo = o.algo
+        c.num_chains = self.C
+        c.dim = self.D
+        c.max_depth_alloc = self.md
+        d1, d2 = o.max_tree_depth
+        c.max_tree_depth_warmup = int(d1)
+        c.max_tree_depth = int(d2)
+        c.num_warmup = int(num_warmup)
+        c.iter_begin = int(iter_begin)
+        c.iter_end = int(iter_end)
+        c.iter_capacity = self.iter_capacity
+        c.adapt_step_size = int(bool(o.adapt_step_size))
+        c.adapt_mass_matrix = int(bool(o.adapt_mass_matrix))
+        c.regularize_mass_matrix = int(bool(o.regularize_mass_matrix))
+        c.dense_mass = 0
+        c.sync_chains = int(self.sync_chains)
+        c.target_accept_prob = float(o.target_accept_prob)
+        c.max_delta_energy = float(o.max_delta_energy)
+        c.trajectory_length = float(o.trajectory_length) if o.trajectory_length is not None else -1.0
+        c.num_steps = int(o.num_steps) if o.num_steps is not None else 0
+        sched = build_adaptation_schedule(int(num_warmup)) if num_warmup > 0 else [(0, -1)]
+        if len(sched) > native.MAX_WINDOWS:
+            raise ValueError("too many adaptation windows")
+        c.num_windows = len(sched)
+        for i in range(native.MAX_WINDOWS):
+            c.window_end[i] = sched[i][1] if i < len(sched) else -1
+        c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        c.chain_offset = self.chain_offset
+        c.collect_start = int(collect_start)
+        c.collect_thinning = int(thinning)
+        c.collection_size = int(collection_size)
+        c.ldc = self.ldc
+
+    # ------------------------------------------------------------------ phases
+    def initialize(self, seed: int, num_warmup: int, init_params=None, radius: float = 2.0,
+                   stream=None):
+        """Reset adaptation state and find a valid initial point for every chain
+        (HMC.init -> initialize_model / find_valid_initial_params + init_kernel)."""
+        s = stream_ptr(stream)
+        self.num_warmup = int(num_warmup)
+        self._alloc(self.iter_capacity)
+        self._fill_cfg(0, 0, num_warmup, seed, 0, 1, 0)
+        imm = self.opts.inverse_mass_matrix
+        imm_t = None
+        if imm is not None:
+            imm_t = torch.as_tensor(imm, dtype=torch.float32, device=self.device).reshape(-1)
+            if imm_t.numel() != self.D:
+                raise ValueError("inverse_mass_matrix must be a diagonal of size D")
+        check(lib().nmx_nuts_reset(ctypes.byref(self.cfg), ptr(self.arena), float(self.opts.step_size),
+                                   ptr(imm_t), s), "nmx_nuts_reset")
+        if init_params is not None:
+            z = torch.as_tensor(init_params, dtype=torch.float32, device=self.device)
+            z = z.reshape(self.C, self.D)
+            zt = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device)
+            zt[:, :self.C] = z.t()
+            check(lib().nmx_nuts_init_from(ctypes.byref(self.cfg), ptr(self.arena), ptr(zt), s))
+            self.potential.evaluate(self.eval_batch, s)
+            check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
+            bad = int(self.view("counters")[1].item())
+            if bad:
+                raise RuntimeError(f"Cannot find valid initial parameters: {bad} chains have "
+                                   "non-finite potential energy or gradient at init_params.")
+        else:
+            for attempt in range(INIT_ATTEMPTS):
+                check(lib().nmx_nuts_init_draw(ctypes.byref(self.cfg), ptr(self.arena), attempt,
+                                               float(radius), s))
+                self.potential.evaluate(self.eval_batch, s)
+                check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
+                if int(self.view("counters")[1].item()) == 0:
+                    break
+            else:
+                raise RuntimeError("Cannot find valid initial parameters. Please check your model "
+                                   "again.")  # infer/util.py:795-797
+        self.iteration = 0
+
+    def run(self, num_iters: int, seed: int, collect_begin: int = 0, collection_size: int | None = None,
+            thinning: int = 1, poll_every: int = 16, stream=None, max_launches: int | None = None):
+        """Advance every chain by `num_iters` transitions.  Transitions with relative index
+        i >= start_idx (fori_collect semantics) are collected into the returned buffers.
+        Returns (samples [S, D, ldc], fields [S, NC, ldc], launches)."""
+        s = stream_ptr(stream)
+        num_iters = int(num_iters)
+        lower = int(collect_begin)
+        if collection_size is None:
+            collection_size = (num_iters - lower) // thinning
+        start_idx = lower + (num_iters - lower) % thinning  # util.py:330
+        it0 = self.iteration
+        if self.sync_chains and num_iters > self.iter_capacity:
+            self._grow_finished(num_iters)
+        self._fill_cfg(it0, it0 + num_iters, self.num_warmup, seed, it0 + start_idx, thinning,
+                       collection_size)
+        S = max(int(collection_size), 0)
+        samples = torch.empty((max(S, 1), self.D, self.ldc), dtype=torch.float32, device=self.device)
+        fields = torch.zeros((max(S, 1), len(native.COLLECT), self.ldc), dtype=torch.float32,
+                             device=self.device)
+        cfgp = ctypes.byref(self.cfg)
+        arena = ptr(self.arena)
+        tr = self.potential.transform_codes()
+        check(lib().nmx_nuts_resume(cfgp, arena, s), "nmx_nuts_resume")
+        done = self.view("counters")[0:1]
+        host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        ev = torch.cuda.Event()
+        pending = False
+        launches = 0
+        step = lib().nmx_nuts_step
+        sp, fp, tp = ptr(samples), ptr(fields), ptr(tr)
+        check(step(cfgp, arena, sp, fp, tp, s), "nmx_nuts_step")
+        evaluate = self.potential.evaluate
+        evb = self.eval_batch
+        while True:
+            for _ in range(poll_every):
+                evaluate(evb, s)
+                check(step(cfgp, arena, sp, fp, tp, s), "nmx_nuts_step")
+            launches += poll_every
+            if pending:
+                ev.synchronize()
+                if int(host[0]) >= self.C:
+                    break
+            host.copy_(done, non_blocking=True)
+            ev.record()
+            pending = True
+            if max_launches is not None and launches >= max_launches:
+                raise RuntimeError(f"chains did not finish within {max_launches} leapfrog launches")
+        self.iteration = it0 + num_iters
+        return samples[:S], fields[:S], launches
+
+    def _grow_finished(self, n):
+        # re-layout the arena with a larger sync-counter table, keeping all chain state
+        old = self.arena
+        old_views = {k: self.view(k).clone() for k in native.FIELDS if k != "finished"}
+        self._alloc(n)
+        for k, v in old_views.items():
+            self.view(k).copy_(v)
+        del old
+
+    # ------------------------------------------------------------------ accessors
+    def chain_state(self, name):
+        """Per-chain view without padding: scalars [C], vectors [C, D]."""
+        v = self.view(name)
+        if v.dim() == 1:
+            return v[:self.C]
+        return v[:, :self.C].t()

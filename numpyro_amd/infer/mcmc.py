@@ -1,0 +1,236 @@
+"""``MCMC`` driver with numpyro's API (numpyro/infer/mcmc.py:224-800).
+
+``run`` / ``warmup`` / ``get_samples`` / ``get_extra_fields`` / ``print_summary`` /
+``post_warmup_state`` / ``last_state`` keep their reference meaning.  All chains of a
+process live on one GPU and run as one vectorized batch on the device state machine; a
+chain's trajectory is a function of (key, global chain id) only, so ``chain_method``
+"parallel", "sequential" and "vectorized" give the same per-chain results (the reference
+guarantees the same up to its stream, test/infer/test_mcmc.py:553-592).  Under
+``torch.distributed`` each rank owns a contiguous shard of the chains
+(``numpyro_amd.parallel``-free: see ``shard_chains``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import diagnostics, native
+from ..random import key_to_seed
+from .hmc import HMCAdaptState, HMCState
+
+_FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
+
+
+def shard_chains(num_chains, rank, world_size):
+    """Contiguous chain shard [lo, hi) of `rank`."""
+    per = num_chains // world_size
+    rem = num_chains % world_size
+    lo = rank * per + min(rank, rem)
+    hi = lo + per + (1 if rank < rem else 0)
+    return lo, hi
+
+
+class MCMC:
+    def __init__(self, sampler, *, num_warmup, num_samples, num_chains=1, thinning=1,
+                 postprocess_fn=None, chain_method="parallel", progress_bar=True,
+                 jit_model_args=False, device=None, sync_chains=False, chain_offset=None,
+                 poll_every=16):
+        self.sampler = sampler
+        self._sample_field = sampler.sample_field
+        self._default_fields = sampler.default_fields
+        self.num_warmup = int(num_warmup)
+        self.num_samples = int(num_samples)
+        self.num_chains = int(num_chains)
+        if not isinstance(thinning, int) or thinning < 1:
+            raise ValueError("thinning must be a positive integer")
+        self.thinning = thinning
+        if postprocess_fn is not None:
+            raise NotImplementedError("postprocess_fn: samples are constrained on the device")
+        if not callable(chain_method) and chain_method not in ("parallel", "vectorized", "sequential"):
+            raise ValueError('Only supporting the following methods to draw chains: "sequential", '
+                             '"parallel", or "vectorized"')
+        self.chain_method = chain_method
+        self.progress_bar = progress_bar
+        self.device = device
+        self.sync_chains = sync_chains
+        self.poll_every = int(poll_every)
+        # chain shard of this process
+        if chain_offset is not None:
+            self.chain_lo, self.chain_hi = int(chain_offset), int(chain_offset) + self.num_chains
+            self.local_chains = self.num_chains
+        elif torch.distributed.is_available() and torch.distributed.is_initialized():
+            r, w = torch.distributed.get_rank(), torch.distributed.get_world_size()
+            self.chain_lo, self.chain_hi = shard_chains(self.num_chains, r, w)
+            self.local_chains = self.chain_hi - self.chain_lo
+        else:
+            self.chain_lo, self.chain_hi, self.local_chains = 0, self.num_chains, self.num_chains
+        self._engine = None
+        self._engine_key = None
+        self._warmup_state = None
+        self._last_state = None
+        self._samples = None
+        self._fields = None
+        self._collected = ()
+        self.last_run_stats = {}
+
+    # ------------------------------------------------------------------ engine
+    def _get_engine(self, args, kwargs):
+        key = (id(self.sampler), tuple(id(a) for a in args), tuple(sorted((k, id(v)) for k, v in kwargs.items())))
+        if self._engine is None or self._engine_key != key:
+            self._engine = self.sampler.make_engine(self.local_chains, args, kwargs, device=self.device,
+                                                    chain_offset=self.chain_lo, sync_chains=self.sync_chains)
+            self._engine_key = key
+        return self._engine
+
+    # ------------------------------------------------------------------ state
+    @property
+    def post_warmup_state(self):
+        return self._warmup_state
+
+    @post_warmup_state.setter
+    def post_warmup_state(self, state):
+        self._warmup_state = state
+
+    @property
+    def last_state(self):
+        return self._last_state
+
+    def _snapshot(self, eng, seed):
+        C = eng.C
+        z_flat = eng.chain_state("z").clone()
+        pot = eng.potential
+        z = pot.unflatten(z_flat) if len(pot.sites) else z_flat
+        adapt = HMCAdaptState(
+            eng.chain_state("step_size").clone(), eng.chain_state("inv_mass").clone(),
+            eng.chain_state("mass_sqrt").clone(), 1.0 / eng.chain_state("mass_sqrt").clone(),
+            (eng.chain_state("da_xt").clone(), eng.chain_state("da_xavg").clone(),
+             eng.chain_state("da_gavg").clone(), eng.chain_state("da_t").clone(),
+             eng.chain_state("da_prox").clone()),
+            (eng.chain_state("wf_mean").clone(), eng.chain_state("wf_m2").clone(),
+             eng.chain_state("wf_n").clone()),
+            eng.chain_state("window_idx").clone(), seed)
+        st = HMCState(
+            eng.chain_state("iter").clone(), z, eng.chain_state("zgrad").clone(),
+            eng.chain_state("pe").clone(), eng.chain_state("energy").clone(), None,
+            eng.opts.trajectory_length, eng.chain_state("last_nsteps").clone(),
+            eng.chain_state("last_acc").clone(), eng.chain_state("mean_acc").clone(),
+            eng.chain_state("last_div").clone().bool(), adapt, seed)
+        st._arena = eng.arena.clone()
+        st._iteration = eng.iteration
+        st._num_warmup = eng.num_warmup
+        st._engine = eng
+        assert C == st.i.shape[0]
+        return st
+
+    def _restore(self, eng, state):
+        if getattr(state, "_engine", None) is not eng:
+            raise ValueError("post_warmup_state belongs to a different model/data binding")
+        eng.arena.copy_(state._arena)
+        eng.iteration = state._iteration
+        eng.num_warmup = state._num_warmup
+
+    # ------------------------------------------------------------------ run
+    def warmup(self, rng_key, *args, extra_fields=(), collect_warmup=False, init_params=None, **kwargs):
+        self._warmup_state = None
+        self._run(rng_key, args, kwargs, extra_fields, init_params, n_iter=self.num_warmup,
+                  lower=0 if collect_warmup else self.num_warmup)
+        self._warmup_state = self._last_state
+
+    def run(self, rng_key, *args, extra_fields=(), init_params=None, **kwargs):
+        if self._warmup_state is not None:
+            self._run(rng_key, args, kwargs, extra_fields, None, n_iter=self.num_samples, lower=0,
+                      resume=self._warmup_state)
+        else:
+            self._run(rng_key, args, kwargs, extra_fields, init_params,
+                      n_iter=self.num_warmup + self.num_samples, lower=self.num_warmup)
+
+    def _run(self, rng_key, args, kwargs, extra_fields, init_params, n_iter, lower, resume=None):
+        assert isinstance(extra_fields, (tuple, list))
+        collect = []
+        for f in (self._sample_field,) + tuple(self._default_fields) + tuple(extra_fields):
+            f = _FIELD_ALIASES.get(f, f)
+            if f == self._sample_field or f in native.COLLECT:
+                if f not in collect:
+                    collect.append(f)
+            elif f.startswith("~"):
+                continue
+            else:
+                raise ValueError(f"extra field {f!r} is not collected by the device engine; "
+                                 f"available: {native.COLLECT}")
+        self._collected = tuple(collect)
+        seed = key_to_seed(rng_key)
+        eng = self._get_engine(args, kwargs)
+        dev = eng.device
+        with torch.cuda.device(dev):
+            if resume is not None:
+                self._restore(eng, resume)
+            else:
+                ip = None
+                if init_params is not None:
+                    ip = init_params
+                    if isinstance(ip, dict):
+                        ip = eng.potential.flatten(ip)
+                    ip = torch.as_tensor(ip, dtype=torch.float32)
+                    if ip.dim() == 1:
+                        ip = ip[None, :].expand(eng.C, -1)
+                    if ip.shape[0] == self.num_chains and self.local_chains != self.num_chains:
+                        ip = ip[self.chain_lo:self.chain_hi]
+                    if ip.shape[0] != eng.C:
+                        raise ValueError("`init_params` must have the same leading dimension as `num_chains`.")
+                eng.initialize(seed, self.num_warmup, init_params=ip, radius=self.sampler.init_radius())
+            start = torch.cuda.Event(enable_timing=True)
+            end = torch.cuda.Event(enable_timing=True)
+            start.record()
+            samples, fields, launches = eng.run(n_iter, seed, collect_begin=lower, thinning=self.thinning,
+                                                poll_every=self.poll_every)
+            end.record()
+            end.synchronize()
+            self.last_run_stats = {"launches": launches, "device_ms": start.elapsed_time(end),
+                                   "iterations": n_iter}
+        self._samples, self._fields = samples, fields
+        self._last_state = self._snapshot(eng, seed)
+
+    # ------------------------------------------------------------------ results
+    def _site_arrays(self, group_by_chain):
+        eng = self._engine
+        S = self._samples.shape[0]
+        flat = self._samples[:, :, :eng.C].permute(2, 0, 1)  # [C, S, D]
+        out = eng.potential.unflatten(flat)
+        if not group_by_chain:
+            out = {k: v.reshape(eng.C * S, *v.shape[2:]) for k, v in out.items()}
+        return out
+
+    def get_samples(self, group_by_chain=False):
+        return self._site_arrays(group_by_chain)
+
+    def get_extra_fields(self, group_by_chain=False):
+        eng = self._engine
+        out = {}
+        for f in self._collected:
+            if f == self._sample_field:
+                continue
+            v = self._fields[:, native.COLLECT.index(f), :eng.C].t()  # [C, S]
+            if f == "num_steps" or f == "i":
+                v = v.round().to(torch.int32)
+            elif f == "diverging":
+                v = v > 0.5
+            if not group_by_chain:
+                v = v.reshape(-1)
+            out["adapt_state.step_size" if f == "step_size" else f] = v
+        return out
+
+    def print_summary(self, prob=0.9, exclude_deterministic=True):
+        sites = {k: v.detach().cpu().numpy() for k, v in self._site_arrays(True).items()}
+        diagnostics.print_summary(sites, prob=prob)
+        ef = self.get_extra_fields()
+        if "diverging" in ef:
+            print("Number of divergences: {}".format(int(ef["diverging"].sum())))
+
+    def transfer_states_to_host(self):
+        self._samples = self._samples.cpu()
+        self._fields = self._fields.cpu()
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_engine"] = None
+        return state

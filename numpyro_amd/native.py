@@ -27,12 +27,85 @@ c_float = ctypes.c_float
 c_double = ctypes.c_double
 c_vp = ctypes.c_void_p
 
+MAX_WINDOWS = 32  # NMX_MAX_WINDOWS
+MAX_TREE_DEPTH = 12  # NMX_MAX_TREE_DEPTH
+
+ALGO_NUTS, ALGO_HMC = 0, 1
+PH_DONE, PH_WAIT, PH_START, PH_LEAF, PH_INITEVAL, PH_NEEDINIT = range(6)
+
+# enum nmx_field (order matters)
+FIELDS = [
+    "phase", "iter", "depth", "sub_n", "dir", "tree_n", "window_idx", "da_t", "wf_n", "turning",
+    "tree_div", "sub_div", "hmc_k", "hmc_n", "last_nsteps", "last_div", "maxdepth_cur",
+    "step_size", "e0", "pe", "energy", "tree_w", "tree_acc", "sub_w", "sub_acc", "pe_sub", "e_sub",
+    "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "pe_eval",
+    "z", "zgrad", "zl", "rl", "gl", "zr", "rr", "gr", "zsub", "gsub", "rsum", "rsum_sub",
+    "inv_mass", "mass_sqrt", "wf_mean", "wf_m2", "z_eval", "g_eval",
+    "ckpt_r", "ckpt_rsum", "counters", "finished",
+]
+FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
+INT_FIELDS = set(FIELDS[:FIELDS.index("step_size")]) | {"counters", "finished"}
+VECTOR_FIELDS = set(FIELDS[FIELDS.index("z"):FIELDS.index("ckpt_r")])
+CKPT_FIELDS = {"ckpt_r", "ckpt_rsum"}
+
+# enum nmx_collect
+COLLECT = ["potential_energy", "energy", "accept_prob", "mean_accept_prob", "step_size",
+           "num_steps", "diverging", "i"]
+
+
+class NutsConfig(ctypes.Structure):
+    """Mirror of nmx_nuts_config (include/numpyro_amd.h)."""
+
+    _fields_ = [
+        ("algo", ctypes.c_int32), ("num_chains", ctypes.c_int32), ("dim", ctypes.c_int32),
+        ("max_depth_alloc", ctypes.c_int32), ("max_tree_depth_warmup", ctypes.c_int32),
+        ("max_tree_depth", ctypes.c_int32), ("num_warmup", ctypes.c_int32),
+        ("iter_end", ctypes.c_int32), ("iter_begin", ctypes.c_int32),
+        ("iter_capacity", ctypes.c_int32), ("adapt_step_size", ctypes.c_int32),
+        ("adapt_mass_matrix", ctypes.c_int32), ("regularize_mass_matrix", ctypes.c_int32),
+        ("dense_mass", ctypes.c_int32), ("sync_chains", ctypes.c_int32),
+        ("target_accept_prob", ctypes.c_float), ("max_delta_energy", ctypes.c_float),
+        ("trajectory_length", ctypes.c_float), ("num_steps", ctypes.c_int32),
+        ("num_windows", ctypes.c_int32), ("window_end", ctypes.c_int32 * MAX_WINDOWS),
+        ("seed", ctypes.c_uint64), ("chain_offset", ctypes.c_int64),
+        ("collect_start", ctypes.c_int32), ("collect_thinning", ctypes.c_int32),
+        ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32),
+    ]
+
+
+class EvalBatch(ctypes.Structure):
+    """Mirror of nmx_eval_batch."""
+
+    _fields_ = [("z", c_vp), ("grad", c_vp), ("pe", c_vp), ("phase", c_vp),
+                ("num_chains", ctypes.c_int32), ("ldc", ctypes.c_int32)]
+
+
+_P = ctypes.POINTER
+_cfgp = _P(NutsConfig)
+_evp = _P(EvalBatch)
+
 # name -> (restype, argtypes); kept in sync with include/numpyro_amd.h (tests check it).
 SIGNATURES: dict[str, tuple] = {
     "nmx_version": (c_int, []),
     "nmx_last_error": (ctypes.c_char_p, []),
+    "nmx_struct_size": (c_size, [c_int]),
     "nmx_selftest_philox": (c_int, [c_vp, c_vp, c_int, c_vp]),
     "nmx_selftest_mfma": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
+    "nmx_nuts_arena_bytes": (c_size, [c_int, c_int, c_int, c_int]),
+    "nmx_nuts_field_info": (c_int, [c_int, c_int, c_int, c_int, c_int, _P(c_size), _P(c_size)]),
+    "nmx_nuts_reset": (c_int, [_cfgp, c_vp, c_float, c_vp, c_vp]),
+    "nmx_nuts_init_draw": (c_int, [_cfgp, c_vp, c_int, c_float, c_vp]),
+    "nmx_nuts_init_from": (c_int, [_cfgp, c_vp, c_vp, c_vp]),
+    "nmx_nuts_init_check": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_nuts_resume": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_nuts_step": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nmx_pe_diag_normal": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
+    "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
+    "nmx_logreg_packed_bytes": (c_size, [c_i64, c_int]),
+    "nmx_logreg_pack": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
+    "nmx_logreg_workspace_bytes": (c_size, [c_i64, c_int, c_int]),
+    "nmx_logreg_pe_grad": (c_int, [c_vp, c_i64, c_int, _evp, c_vp, c_vp]),
+    "nmx_logreg_num_splits": (c_int, [c_i64]),
 }
 
 

@@ -1,0 +1,179 @@
+"""Fused potentials: the model side of the hot path.
+
+The reference turns a model into ``potential_fn(z)`` by tracing its effect handlers
+(numpyro/infer/util.py:546-611) and differentiates it with ``jax.value_and_grad``
+(numpyro/infer/hmc_util.py:242-252).  Here each supported model is a hand-written HIP
+kernel computing U and dU/dz for all chains at once; this module binds a model's data
+to its kernel and describes its sample sites (names, shapes, support transforms) in the
+order of ``ravel_pytree`` over the sorted site dict, so samples come back keyed by site
+exactly like ``MCMC.get_samples()``.
+
+``FusedModel`` objects play the role of the reference's model functions:
+``NUTS(logistic_regression)`` then ``mcmc.run(key, features, labels)`` binds the data.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import native
+from .native import check, lib, ptr
+
+REAL, POSITIVE = 0, 1  # transform codes: identity, ExpTransform (transforms.py:537-577)
+
+
+class Potential:
+    """Base class.  Subclasses set ``sites`` = [(name, shape, transform)] and ``dim``."""
+
+    sites: list = []
+    dim: int = 0
+
+    def bind(self, num_chains: int, ldc: int, device) -> None:
+        self.num_chains, self.ldc, self.device = num_chains, ldc, torch.device(device)
+        self._codes = None
+        self._bind(num_chains, ldc, self.device)
+
+    def _bind(self, num_chains, ldc, device):
+        pass
+
+    def evaluate(self, eval_batch: native.EvalBatch, stream: int) -> None:
+        raise NotImplementedError
+
+    def transform_codes(self):
+        if self._codes is None:
+            codes = []
+            for _, shape, tr in self.sites:
+                codes += [tr] * int(np.prod(shape, dtype=np.int64))
+            assert len(codes) == self.dim
+            self._codes = torch.tensor(codes, dtype=torch.int8, device=self.device)
+        return self._codes
+
+    def unflatten(self, flat):
+        """[..., D] -> {site: [..., *shape]} (ravel_pytree order)."""
+        out, o = {}, 0
+        for name, shape, _ in self.sites:
+            n = int(np.prod(shape, dtype=np.int64))
+            out[name] = flat[..., o:o + n].reshape(*flat.shape[:-1], *shape)
+            o += n
+        return out
+
+    def flatten(self, params: dict):
+        """{site: [C, *shape]} unconstrained -> [C, D]."""
+        parts = []
+        for name, shape, _ in self.sites:
+            v = torch.as_tensor(params[name], dtype=torch.float32)
+            parts.append(v.reshape(v.shape[0], -1))
+        return torch.cat(parts, dim=1)
+
+
+def _dev(x, device, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x, dtype=dtype).to(device).contiguous()
+
+
+class DiagNormal(Potential):
+    """U = 0.5 sum((z - mu)^2 / sd^2): test target of test/infer/test_mcmc.py:28-72."""
+
+    def __init__(self, mu, sd, name="x"):
+        self.mu_h = np.asarray(mu, np.float32).reshape(-1)
+        self.sd_h = np.broadcast_to(np.asarray(sd, np.float32), self.mu_h.shape).copy()
+        self.dim = self.mu_h.size
+        self.sites = [(name, (self.dim,), REAL)]
+
+    def _bind(self, C, ldc, device):
+        self.mu = _dev(self.mu_h, device)
+        self.prec = _dev(1.0 / self.sd_h.astype(np.float64) ** 2, device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_diag_normal(ptr(self.mu), ptr(self.prec), self.dim, ctypes.byref(ev), stream),
+              "nmx_pe_diag_normal")
+
+
+class EightSchools(Potential):
+    """README.md:47-55: mu ~ N(0,5), tau ~ HalfCauchy(5), theta ~ N(mu, tau), y ~ N(theta, sigma)."""
+
+    def __init__(self, J, sigma, y):
+        self.J = int(J)
+        self.sigma_h = np.asarray(sigma, np.float32)
+        self.y_h = np.asarray(y, np.float32)
+        self.dim = 2 + self.J
+        self.sites = [("mu", (), REAL), ("tau", (), POSITIVE), ("theta", (self.J,), REAL)]
+
+    def _bind(self, C, ldc, device):
+        self.y = _dev(self.y_h, device)
+        self.sigma = _dev(self.sigma_h, device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_eight_schools(ptr(self.y), ptr(self.sigma), self.J, ctypes.byref(ev), stream),
+              "nmx_pe_eight_schools")
+
+
+class LogisticRegression(Potential):
+    """examples/covtype.py:66-71 (coefs ~ N(0, 1)^D, obs ~ Bernoulli(logits=X @ coefs))."""
+
+    def __init__(self, data, labels):
+        self.X_in, self.y_in = data, labels
+        shape = tuple(data.shape)
+        self.N, self.dim = int(shape[0]), int(shape[1])
+        if self.dim > 64:
+            raise ValueError("the fused logistic-regression kernel supports up to 64 features")
+        self.sites = [("coefs", (self.dim,), REAL)]
+        self.packed = None
+
+    def _bind(self, C, ldc, device):
+        if self.packed is None or self.packed.device != device:
+            X = _dev(self.X_in, device)
+            y = _dev(self.y_in, device)
+            nb = lib().nmx_logreg_packed_bytes(self.N, self.dim)
+            self.packed = torch.empty(nb // 4, dtype=torch.float32, device=device)
+            with torch.cuda.device(device):
+                check(lib().nmx_logreg_pack(ptr(X), ptr(y), self.N, self.dim, ptr(self.packed),
+                                            native.stream_ptr()), "nmx_logreg_pack")
+            del X, y
+        wb = lib().nmx_logreg_workspace_bytes(self.N, self.dim, C)
+        self.workspace = torch.empty(wb, dtype=torch.uint8, device=device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_logreg_pe_grad(ptr(self.packed), self.N, self.dim, ctypes.byref(ev),
+                                       ptr(self.workspace), stream), "nmx_logreg_pe_grad")
+
+    def flops_per_eval(self, num_chains):
+        """Algorithmic FLOPs of one evaluation (two GEMMs): 4 N D C."""
+        return 4.0 * self.N * self.dim * num_chains
+
+
+# ------------------------------------------------------------------------------------------
+# Model functions (the reference's examples) -> fused potentials.
+# ------------------------------------------------------------------------------------------
+class FusedModel:
+    """A model callable whose potential is a fused kernel.  ``builder(*args, **kwargs)``
+    returns a bound-data Potential (the analogue of initialize_model's potential_fn_gen)."""
+
+    def __init__(self, name, builder, doc=""):
+        self.__name__ = name
+        self.builder = builder
+        self.__doc__ = doc
+
+    def potential(self, *args, **kwargs) -> Potential:
+        return self.builder(*args, **kwargs)
+
+    def __call__(self, *args, **kwargs):
+        raise TypeError(f"{self.__name__} is a fused model: pass it to NUTS/HMC, do not call it")
+
+    def __repr__(self):
+        return f"FusedModel({self.__name__})"
+
+
+logistic_regression = FusedModel(
+    "logistic_regression", lambda data, labels, subsample_size=None: LogisticRegression(data, labels),
+    "examples/covtype.py:66-71 model(data, labels)")
+
+eight_schools = FusedModel(
+    "eight_schools", lambda J, sigma, y=None: EightSchools(J, sigma, y),
+    "README.md:47-55 eight_schools(J, sigma, y)")
+
+diag_normal = FusedModel("diag_normal", lambda mu, sd: DiagNormal(mu, sd))
+
+LOG_2PI = math.log(2 * math.pi)

@@ -1,0 +1,190 @@
+"""Device NUTS/HMC engine vs the NumPy oracle (oracle/hmc_ref.py) on identical Philox
+streams, plus schedule-invariance and statistical checks.
+
+Parity bar: the oracle restates numpyro's sample kernel in float32 with the same event
+keys, so per-chain trajectories coincide until an fp32 rounding difference (transcendental
+ulps, dot-product order) flips a discrete decision; tests require the large majority of
+chains to reproduce the oracle's num_steps sequence exactly and their draws to 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from numpyro_amd import datasets, native
+from numpyro_amd import potentials as P
+from numpyro_amd.infer import HMC, MCMC, NUTS
+from oracle import hmc_ref as H
+from oracle import philox
+from oracle import potentials as OP
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS", **kw):
+    o = H.NUTSOracle(lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)
+                                     for v in pe_grad(z)),
+                     dim, num_warmup, algo=algo, **kw)
+    z0 = philox.init_uniform(seed, chain, 0, dim)
+    s = o.init(z0, seed, chain)
+    out = []
+    for _ in range(num_iters):
+        s = o.sample(s)
+        out.append(s)
+    return out
+
+
+def _run_engine(model_args, model, num_chains, num_warmup, num_samples, seed, kernel_cls=NUTS,
+                sync=False, chain_offset=None, **kw):
+    kernel = kernel_cls(model, **kw)
+    mcmc = MCMC(kernel, num_warmup=num_warmup, num_samples=num_samples, num_chains=num_chains,
+                chain_method="vectorized", progress_bar=False, sync_chains=sync,
+                chain_offset=chain_offset)
+    if num_warmup > 0:
+        mcmc.warmup(seed, *model_args, collect_warmup=True,
+                    extra_fields=("num_steps", "accept_prob", "potential_energy", "adapt_state.step_size"))
+        warm = mcmc.get_samples(group_by_chain=True), mcmc.get_extra_fields(group_by_chain=True)
+    else:
+        warm = ({}, {"num_steps": torch.zeros(num_chains, 0, dtype=torch.int32)})
+    mcmc.run(seed, *model_args,
+             extra_fields=("num_steps", "accept_prob", "potential_energy", "adapt_state.step_size"))
+    return mcmc, warm
+
+
+def _dev_paths(mcmc, warm):
+    ws, wf = warm
+    ef = mcmc.get_extra_fields(True)
+    sm = mcmc.get_samples(True)
+    ns = np.concatenate([wf["num_steps"].cpu().numpy(), ef["num_steps"].cpu().numpy()], axis=1)
+    flat = {k: np.concatenate([ws[k].cpu().numpy(), sm[k].cpu().numpy()], axis=1) if k in ws
+            else sm[k].cpu().numpy() for k in sm}
+    return ns, flat
+
+
+@pytest.mark.parametrize("algo", ["NUTS", "HMC"])
+def test_engine_matches_oracle_eight_schools(device, algo):
+    """Adaptive run: the centred 8-schools posterior is a funnel, where fp32 rounding
+    differences grow along trajectories (chaotic dynamics), so exact agreement is required
+    over the first transitions only; later agreement is statistical (other tests)."""
+    seed, C, W, S, T0 = 1234, 32, 30, 10, 4
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    kcls = NUTS if algo == "NUTS" else HMC
+    kw = {} if algo == "NUTS" else {"trajectory_length": 1.0}
+    mcmc, warm = _run_engine(args, P.eight_schools, C, W, S, seed, kernel_cls=kcls, **kw)
+    ns_dev, site = _dev_paths(mcmc, warm)
+    ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
+    match = 0
+    for c in range(C):
+        states = _oracle_chain(ref.pe_grad, 10, seed, c, W, T0, algo=algo, **kw)
+        ns = np.array([s.num_steps for s in states])
+        assert ns[0] == ns_dev[c, 0], (c, ns, ns_dev[c, :T0])
+        if np.array_equal(ns, ns_dev[c, :T0]):
+            match += 1
+            mu = np.array([s.z[0] for s in states])
+            th = np.stack([s.z[2:] for s in states])
+            np.testing.assert_allclose(site["mu"][c, :T0], mu, rtol=2e-3, atol=2e-3)
+            np.testing.assert_allclose(site["theta"][c, :T0], th, rtol=2e-3, atol=2e-3)
+    assert match >= int(0.9 * C), f"only {match}/{C} chains reproduced the oracle path"
+
+
+@pytest.mark.parametrize("algo", ["NUTS", "HMC"])
+def test_engine_matches_oracle_fixed_step(device, algo):
+    """No adaptation, fixed step size: every transition is a deterministic function of
+    the Philox stream; device and oracle must take the same discrete path."""
+    seed, C, T = 77, 64, 3
+    rs = np.random.RandomState(0)
+    X = rs.randn(300, 4).astype(np.float32)
+    y = (rs.rand(300) < 1 / (1 + np.exp(-X @ np.array([1.0, -0.5, 0.3, 0.0])))).astype(np.float32)
+    kcls = NUTS if algo == "NUTS" else HMC
+    kw = dict(step_size=0.02, adapt_step_size=False, adapt_mass_matrix=False)
+    if algo == "HMC":
+        kw["trajectory_length"] = 0.3
+    mcmc, warm = _run_engine((X, y), P.logistic_regression, C, 0, T, seed, kernel_cls=kcls, **kw)
+    ns_dev, site = _dev_paths(mcmc, warm)
+    ref = OP.LogisticRegression(X, y, dtype=np.float32)
+    match = 0
+    for c in range(C):
+        states = _oracle_chain(ref.pe_grad, 4, seed, c, 0, T, algo=algo, **kw)
+        ns = np.array([s.num_steps for s in states])
+        if np.array_equal(ns, ns_dev[c]):
+            match += 1
+            z = np.stack([s.z for s in states])
+            np.testing.assert_allclose(site["coefs"][c], z, rtol=1e-3, atol=1e-4)
+    assert match >= int(0.95 * C), f"only {match}/{C} chains reproduced the oracle path"
+
+
+def test_sync_and_async_schedules_are_bitwise_identical(device):
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    a, _ = _run_engine(args, P.eight_schools, 64, 50, 30, 99, sync=False)
+    b, _ = _run_engine(args, P.eight_schools, 64, 50, 30, 99, sync=True)
+    for k in ("mu", "tau", "theta"):
+        np.testing.assert_array_equal(a.get_samples()[k].cpu().numpy(), b.get_samples()[k].cpu().numpy())
+    np.testing.assert_array_equal(a.get_extra_fields()["num_steps"].cpu().numpy(),
+                                  b.get_extra_fields()["num_steps"].cpu().numpy())
+    # the sync schedule wastes leapfrogs waiting for the slowest chain
+    assert b.last_run_stats["launches"] >= a.last_run_stats["launches"]
+
+
+def test_chain_sharding_is_bitwise_invariant(device):
+    """Chains keyed by global id: two shards reproduce the full run exactly."""
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    full, _ = _run_engine(args, P.eight_schools, 96, 40, 20, 5)
+    lo, _ = _run_engine(args, P.eight_schools, 40, 40, 20, 5, chain_offset=0)
+    hi, _ = _run_engine(args, P.eight_schools, 56, 40, 20, 5, chain_offset=40)
+    f = full.get_samples(True)["theta"].cpu().numpy()
+    np.testing.assert_array_equal(f[:40], lo.get_samples(True)["theta"].cpu().numpy())
+    np.testing.assert_array_equal(f[40:], hi.get_samples(True)["theta"].cpu().numpy())
+
+
+@pytest.mark.parametrize("kernel_cls,dense", [(NUTS, False), (HMC, False)])
+def test_unnormalized_normal(device, kernel_cls, dense):
+    """test/infer/test_mcmc.py:28-72: mean/std of a Gaussian target, rtol 0.07."""
+    true_mean, true_std = 1.0, 2.0
+    pot = P.DiagNormal([true_mean], [true_std])
+    kw = {"trajectory_length": 8.0} if kernel_cls is HMC else {}
+    kernel = kernel_cls(potential_fn=pot, **kw)
+    mcmc = MCMC(kernel, num_warmup=500, num_samples=2000, num_chains=32, progress_bar=False)
+    mcmc.run(0, init_params=torch.zeros(32, 1))
+    x = mcmc.get_samples()["x"].cpu().numpy().ravel()
+    np.testing.assert_allclose(x.mean(), true_mean, rtol=0.07)
+    np.testing.assert_allclose(x.std(), true_std, rtol=0.07)
+
+
+def test_eight_schools_posterior(device):
+    """README.md:75-91 table (statistical): mu ~ 4.1 +- 3.2 and tau ~ 4 (wide tolerance)."""
+    kernel = NUTS(P.eight_schools)
+    mcmc = MCMC(kernel, num_warmup=500, num_samples=1000, num_chains=256, chain_method="vectorized")
+    mcmc.run(0, 8, datasets.EIGHT_SCHOOLS_SIGMA, y=datasets.EIGHT_SCHOOLS_Y,
+             extra_fields=("potential_energy",))
+    s = mcmc.get_samples()
+    mu = s["mu"].cpu().numpy()
+    assert abs(mu.mean() - 4.4) < 0.6
+    assert 2.8 < mu.std() < 3.8
+    assert 2.5 < s["tau"].cpu().numpy().mean() < 4.5
+    pe = mcmc.get_extra_fields()["potential_energy"].cpu().numpy()
+    assert -58 < np.mean(-pe) < -50  # "Expected log joint density: -54.55"
+
+
+def test_logistic_regression_recovers_coefs(device):
+    """test/infer/test_mcmc.py:104-168 analogue: N=3000, dim 3, coefs atol 0.4."""
+    rs = np.random.RandomState(0)
+    true = np.array([1.0, 2.0, 3.0], np.float32)
+    X = rs.randn(3000, 3).astype(np.float32)
+    y = (rs.rand(3000) < 1 / (1 + np.exp(-X @ true))).astype(np.float32)
+    mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=300, num_samples=300, num_chains=64)
+    mcmc.run(2, X, y)
+    m = mcmc.get_samples()["coefs"].cpu().numpy().mean(0)
+    np.testing.assert_allclose(m, true, atol=0.4)
+
+
+def test_resume_from_post_warmup_state(device):
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    mcmc = MCMC(NUTS(P.eight_schools), num_warmup=100, num_samples=50, num_chains=32)
+    mcmc.warmup(3, *args)
+    st = mcmc.post_warmup_state
+    assert int(st.i[0]) == 100
+    mcmc.run(4, *args)
+    first = mcmc.get_samples()["mu"].cpu().numpy()
+    assert first.shape == (32 * 50,)
+    mcmc.run(4, *args)  # post_warmup_state still set -> same samples again
+    np.testing.assert_array_equal(first, mcmc.get_samples()["mu"].cpu().numpy())
+    assert int(mcmc.last_state.i[0]) == 150

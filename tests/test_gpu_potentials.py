@@ -1,0 +1,127 @@
+"""Fused potential kernels vs the oracle (oracle/potentials.py), on the GPU through the C-ABI.
+
+Tolerances (fp32 kernels vs float64 oracle): pe relative 2e-5 (logreg sums up to 1e5 rows),
+grad |g - g_ref| <= 1e-4 * (|g_ref| + sum_n |x_n|) -- the f32 MFMA k-ordered fma chains
+carry ~1e-7 relative error per term (cdna_hip_programming.md §3 'FP32-input MFMA').
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from numpyro_amd import datasets
+from oracle import potentials as OP
+
+pytestmark = pytest.mark.gpu
+
+
+def _eval(pot, Z, device, phase=None):
+    import torch
+
+    from numpyro_amd import native
+
+    C, D = Z.shape
+    ldc = (C + 63) // 64 * 64
+    pot.bind(C, ldc, device)
+    z = torch.zeros(D, ldc, device=device)
+    z[:, :C] = torch.from_numpy(Z.T.astype(np.float32)).to(device)
+    g = torch.full((D, ldc), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    ph = None
+    if phase is not None:
+        ph = torch.zeros(ldc, dtype=torch.int32, device=device)
+        ph[:C] = torch.from_numpy(phase.astype(np.int32)).to(device)
+    ev = native.EvalBatch(native.ptr(z), native.ptr(g), native.ptr(pe), native.ptr(ph), C, ldc)
+    pot.evaluate(ev, native.stream_ptr())
+    torch.cuda.synchronize()
+    return pe[:C].cpu().numpy().astype(np.float64), g[:, :C].cpu().numpy().T.astype(np.float64)
+
+
+@pytest.mark.parametrize("N,D,C", [(1000, 55, 200), (517, 5, 64), (3000, 33, 130), (64, 2, 1),
+                                   (20000, 55, 256)])
+def test_logreg_matches_oracle(device, N, D, C):
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(N + D)
+    X = rs.randn(N, D).astype(np.float32)
+    y = (rs.rand(N) < 0.4).astype(np.float32)
+    Z = (rs.randn(C, D) * 0.3).astype(np.float32)
+    pe, g = _eval(LogisticRegression(X, y), Z, device)
+    ref = OP.LogisticRegression(X.astype(np.float64), y.astype(np.float64))
+    pe_r, g_r = ref.pe_grad_batch(Z.astype(np.float64))
+    np.testing.assert_allclose(pe, pe_r, rtol=2e-5, atol=1e-3)
+    scale = np.abs(g_r) + np.abs(X).sum(0)[None, :]
+    assert np.all(np.abs(g - g_r) <= 1e-4 * scale), np.max(np.abs(g - g_r) / scale)
+
+
+def test_logreg_covtype_shape_at_scale(device):
+    """Full covtype row count (581012 x 55), 128 chains: size-independent checks plus a
+    float64 reference on the same synthetic data."""
+    from numpyro_amd.potentials import LogisticRegression
+
+    X, y = datasets.covtype_synthetic(seed=0)
+    rs = np.random.RandomState(5)
+    Z = (datasets.COVTYPE_REF_COEFS[None, :] + 0.01 * rs.randn(128, 55)).astype(np.float32)
+    pe, g = _eval(LogisticRegression(X, y), Z, device)
+    ref = OP.LogisticRegression(X, y)
+    pe_r, g_r = ref.pe_grad_batch(Z.astype(np.float64))
+    np.testing.assert_allclose(pe, pe_r, rtol=2e-6)
+    scale = np.abs(g_r) + np.abs(X).sum(0)[None, :]
+    assert np.all(np.abs(g - g_r) <= 2e-5 * scale)
+
+
+def test_logreg_skips_inactive_chains(device):
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(3)
+    X = rs.randn(700, 7).astype(np.float32)
+    y = (rs.rand(700) < 0.5).astype(np.float32)
+    Z = rs.randn(300, 7).astype(np.float32)
+    phase = np.full(300, 3)
+    phase[:150] = 0  # first 150 chains inactive (whole chain groups skipped)
+    pe, g = _eval(LogisticRegression(X, y), Z, device, phase=phase)
+    pe_r, g_r = OP.LogisticRegression(X, y).pe_grad_batch(Z)
+    assert np.all(np.isnan(pe[:128]))  # a fully inactive workgroup writes nothing
+    np.testing.assert_allclose(pe[150:], pe_r[150:], rtol=2e-5)
+    np.testing.assert_allclose(g[150:], g_r[150:], rtol=1e-3, atol=1e-2)
+
+
+def test_logreg_split_invariance(device):
+    """A chain's U/dU must not depend on how many chains share the launch (bitwise)."""
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(4)
+    X = rs.randn(5000, 55).astype(np.float32)
+    y = (rs.rand(5000) < 0.5).astype(np.float32)
+    Z = rs.randn(300, 55).astype(np.float32) * 0.1
+    pe_a, g_a = _eval(LogisticRegression(X, y), Z, device)
+    pe_b, g_b = _eval(LogisticRegression(X, y), Z[200:260], device)
+    np.testing.assert_array_equal(pe_a[200:260], pe_b)
+    np.testing.assert_array_equal(g_a[200:260], g_b)
+
+
+def test_eight_schools_matches_oracle(device):
+    from numpyro_amd.potentials import EightSchools
+
+    rs = np.random.RandomState(0)
+    Z = rs.uniform(-2, 2, (100, 10)).astype(np.float32)
+    pe, g = _eval(EightSchools(8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y), Z, device)
+    ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
+    for c in range(100):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c], pr, rtol=1e-5, atol=1e-4)
+        np.testing.assert_allclose(g[c], gr, rtol=1e-4, atol=1e-4)
+
+
+def test_diag_normal(device):
+    from numpyro_amd.potentials import DiagNormal
+
+    mu = np.array([1.0, -2.0, 0.5], np.float32)
+    sd = np.array([0.5, 2.0, 1.0], np.float32)
+    Z = np.random.RandomState(0).randn(70, 3).astype(np.float32)
+    pe, g = _eval(DiagNormal(mu, sd), Z, device)
+    ref = OP.IsoNormal(mu, sd)
+    for c in range(70):
+        pr, gr = ref.pe_grad(Z[c])
+        np.testing.assert_allclose(pe[c], pr, rtol=1e-5)
+        np.testing.assert_allclose(g[c], gr, rtol=1e-5, atol=1e-6)

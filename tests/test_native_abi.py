@@ -27,6 +27,27 @@ def test_library_exports_header_symbols():
     assert lib.nmx_version() >= 1
 
 
+def test_struct_layouts_match():
+    import ctypes
+
+    from numpyro_amd import native
+
+    assert native.lib().nmx_struct_size(0) == ctypes.sizeof(native.NutsConfig)
+    assert native.lib().nmx_struct_size(1) == ctypes.sizeof(native.EvalBatch)
+
+
+def test_field_enum_matches_header():
+    from numpyro_amd import native
+
+    src = open(os.path.join(ROOT, "include", "numpyro_amd.h")).read()
+    body = src[src.index("enum nmx_field"):]
+    body = body[:body.index("};")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = [n.strip().split("=")[0].strip() for n in body.split("{", 1)[1].split(",")]
+    names = [n for n in names if n and n != "NMX_NUM_FIELDS"]
+    assert [n[len("NMX_F_"):].lower() for n in names] == native.FIELDS
+
+
 def test_invalid_argument_reports_error():
     from numpyro_amd import native
 
