@@ -27,8 +27,8 @@ MI355X_HBM_PEAK_GBS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5, help="timed sampling transitions")
-    p.add_argument("--warmup", type=int, default=5, help="untimed warmup/adaptation transitions")
+    p.add_argument("--steps", type=int, default=10, help="timed sampling transitions")
+    p.add_argument("--warmup", type=int, default=30, help="untimed warmup/adaptation transitions")
     p.add_argument("--chains", type=int, default=4096, help="total chains over all GPUs")
     p.add_argument("--rows", type=int, default=581012)
     p.add_argument("--seed", type=int, default=0)

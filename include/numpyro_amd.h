@@ -76,7 +76,10 @@ enum nmx_field {
   NMX_F_WF_MEAN, NMX_F_WF_M2, NMX_F_Z_EVAL, NMX_F_G_EVAL,
   /* checkpoints [max_depth][D][ldc] */
   NMX_F_CKPT_R, NMX_F_CKPT_RSUM,
-  /* device counters int32[16]: [0] chains DONE, [1] chains NEEDINIT, [2..] reserved */
+  /* compacted list of LEAF chains for the next potential launch, int32 [2][ldc] by parity */
+  NMX_F_ACTIVE_IDX,
+  /* device counters int32[16]: [0] chains DONE, [1] chains NEEDINIT, [2],[3] active-list
+   * lengths for parity 0/1, [4..] reserved */
   NMX_F_COUNTERS,
   /* sync_chains: int32[iter_capacity] #chains that finished transition iter_begin + i */
   NMX_F_FINISHED,
@@ -116,7 +119,9 @@ typedef struct nmx_nuts_config {
   int32_t collect_start;         /* fori_collect start_idx (util.py:330) */
   int32_t collect_thinning;
   int32_t collection_size;       /* slots in samples/fields; 0 disables collection */
-  int32_t ldc;                   /* filled by the library (round_up(C, 64)) */
+  int32_t ldc;                   /* round_up(C, 64) */
+  int32_t parity;                /* launch parity: nmx_nuts_step appends LEAF chains to
+                                    active list [parity] (and clears [parity ^ 1]) */
 } nmx_nuts_config;
 
 /* Arena size/offsets for (C, D, max_depth_alloc, iter_capacity). */
@@ -161,6 +166,10 @@ typedef struct nmx_eval_batch {
   float* grad;             /* [D][ldc] (arena NMX_F_G_EVAL) */
   float* pe;               /* [ldc]    (arena NMX_F_PE_EVAL) */
   const int32_t* phase;    /* [ldc]    (arena NMX_F_PHASE); NULL = evaluate every chain */
+  const int32_t* active_idx;   /* optional compacted chain list (arena NMX_F_ACTIVE_IDX);
+                                  when set, only chains active_idx[0 .. *active_count) are
+                                  evaluated and `phase` is ignored */
+  const int32_t* active_count;
   int32_t num_chains;
   int32_t ldc;
 } nmx_eval_batch;

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/numpyro_amd.h"
+
 #define NMX_HD __host__ __device__ __forceinline__
 
 // RNG event tags (high byte of counter word 2).
@@ -94,4 +96,12 @@ __device__ __forceinline__ float nmx_logaddexp(float a, float b) {
 __device__ __forceinline__ float nmx_sigmoid(float x) {
   // jax.scipy.special.expit
   return 1.0f / (1.0f + expf(-x));
+}
+
+// Chain evaluated at batch position `pos` of a potential launch, or -1.
+__device__ __forceinline__ int nmx_eval_chain(const nmx_eval_batch& ev, int pos) {
+  if (ev.active_idx) return pos < *ev.active_count ? ev.active_idx[pos] : -1;
+  if (pos >= ev.num_chains) return -1;
+  if (ev.phase && ev.phase[pos] < NMX_PH_LEAF) return -1;
+  return pos;
 }

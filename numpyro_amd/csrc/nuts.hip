@@ -37,6 +37,7 @@ size_t field_bytes(int field, int ldc, int D, int MD, int iter_cap) {
   if (field <= NMX_F_PE_EVAL) return (size_t)ldc * 4;
   if (field <= NMX_F_G_EVAL) return (size_t)D * ldc * 4;
   if (field <= NMX_F_CKPT_RSUM) return (size_t)MD * D * ldc * 4;
+  if (field == NMX_F_ACTIVE_IDX) return (size_t)2 * ldc * 4;
   if (field == NMX_F_COUNTERS) return 16 * 4;
   if (field == NMX_F_FINISHED) return (size_t)(iter_cap > 0 ? iter_cap : 1) * 4;
   return 0;
@@ -55,6 +56,7 @@ struct Arena {
   float* v[NUM_VECTORS];
   float* ckr;
   float* ckrs;
+  int32_t* active_idx;
   int32_t* counters;
   int32_t* finished;
 };
@@ -74,6 +76,7 @@ Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
     a.v[f - NMX_F_Z] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
   a.ckr = (float*)(b + field_offset(NMX_F_CKPT_R, ldc, D, MD, iter_cap));
   a.ckrs = (float*)(b + field_offset(NMX_F_CKPT_RSUM, ldc, D, MD, iter_cap));
+  a.active_idx = (int32_t*)(b + field_offset(NMX_F_ACTIVE_IDX, ldc, D, MD, iter_cap));
   a.counters = (int32_t*)(b + field_offset(NMX_F_COUNTERS, ldc, D, MD, iter_cap));
   a.finished = (int32_t*)(b + field_offset(NMX_F_FINISHED, ldc, D, MD, iter_cap));
   return a;
@@ -113,12 +116,98 @@ __device__ __forceinline__ float transform_value(int8_t code, float z) {
 
 // ---------------------------------------------------------------------------------------
 // The step kernel.
+//
+// Per-chain scalar state is loaded into registers by every wave of the block before the
+// first barrier, updated identically by all waves (decisions only depend on block-reduced
+// sums and the chain's own registers) and written back by wave 0 only, so no wave can
+// observe another wave's partial update.  Vector work is split by coordinate across waves.
 // ---------------------------------------------------------------------------------------
+struct ChainScalars {
+  int phase, it, depth, sub_n, dir, tree_n, widx, da_t, wf_n, turning, tree_div, sub_div;
+  int hmc_k, hmc_n, last_nsteps, last_div, maxdepth;
+  float step, E0, pe, energy, tree_w, tree_acc, sub_w, sub_acc, pe_sub, e_sub;
+  float da_xt, da_xavg, da_gavg, da_prox, mean_acc, last_acc, step_eff;
+};
+
+__device__ __forceinline__ void load_scalars(const Arena& a, int c, ChainScalars& s) {
+  s.phase = AI(NMX_F_PHASE)[c];
+  s.it = AI(NMX_F_ITER)[c];
+  s.depth = AI(NMX_F_DEPTH)[c];
+  s.sub_n = AI(NMX_F_SUB_N)[c];
+  s.dir = AI(NMX_F_DIR)[c];
+  s.tree_n = AI(NMX_F_TREE_N)[c];
+  s.widx = AI(NMX_F_WINDOW_IDX)[c];
+  s.da_t = AI(NMX_F_DA_T)[c];
+  s.wf_n = AI(NMX_F_WF_N)[c];
+  s.turning = AI(NMX_F_TURNING)[c];
+  s.tree_div = AI(NMX_F_TREE_DIV)[c];
+  s.sub_div = AI(NMX_F_SUB_DIV)[c];
+  s.hmc_k = AI(NMX_F_HMC_K)[c];
+  s.hmc_n = AI(NMX_F_HMC_N)[c];
+  s.last_nsteps = AI(NMX_F_LAST_NSTEPS)[c];
+  s.last_div = AI(NMX_F_LAST_DIV)[c];
+  s.maxdepth = AI(NMX_F_MAXDEPTH_CUR)[c];
+  s.step = AF(NMX_F_STEP_SIZE)[c];
+  s.E0 = AF(NMX_F_E0)[c];
+  s.pe = AF(NMX_F_PE)[c];
+  s.energy = AF(NMX_F_ENERGY)[c];
+  s.tree_w = AF(NMX_F_TREE_W)[c];
+  s.tree_acc = AF(NMX_F_TREE_ACC)[c];
+  s.sub_w = AF(NMX_F_SUB_W)[c];
+  s.sub_acc = AF(NMX_F_SUB_ACC)[c];
+  s.pe_sub = AF(NMX_F_PE_SUB)[c];
+  s.e_sub = AF(NMX_F_E_SUB)[c];
+  s.da_xt = AF(NMX_F_DA_XT)[c];
+  s.da_xavg = AF(NMX_F_DA_XAVG)[c];
+  s.da_gavg = AF(NMX_F_DA_GAVG)[c];
+  s.da_prox = AF(NMX_F_DA_PROX)[c];
+  s.mean_acc = AF(NMX_F_MEAN_ACC)[c];
+  s.last_acc = AF(NMX_F_LAST_ACC)[c];
+  s.step_eff = AF(NMX_F_STEP_EFF)[c];
+}
+
+__device__ __forceinline__ void store_scalars(const Arena& a, int c, const ChainScalars& s) {
+  AI(NMX_F_PHASE)[c] = s.phase;
+  AI(NMX_F_ITER)[c] = s.it;
+  AI(NMX_F_DEPTH)[c] = s.depth;
+  AI(NMX_F_SUB_N)[c] = s.sub_n;
+  AI(NMX_F_DIR)[c] = s.dir;
+  AI(NMX_F_TREE_N)[c] = s.tree_n;
+  AI(NMX_F_WINDOW_IDX)[c] = s.widx;
+  AI(NMX_F_DA_T)[c] = s.da_t;
+  AI(NMX_F_WF_N)[c] = s.wf_n;
+  AI(NMX_F_TURNING)[c] = s.turning;
+  AI(NMX_F_TREE_DIV)[c] = s.tree_div;
+  AI(NMX_F_SUB_DIV)[c] = s.sub_div;
+  AI(NMX_F_HMC_K)[c] = s.hmc_k;
+  AI(NMX_F_HMC_N)[c] = s.hmc_n;
+  AI(NMX_F_LAST_NSTEPS)[c] = s.last_nsteps;
+  AI(NMX_F_LAST_DIV)[c] = s.last_div;
+  AI(NMX_F_MAXDEPTH_CUR)[c] = s.maxdepth;
+  AF(NMX_F_STEP_SIZE)[c] = s.step;
+  AF(NMX_F_E0)[c] = s.E0;
+  AF(NMX_F_PE)[c] = s.pe;
+  AF(NMX_F_ENERGY)[c] = s.energy;
+  AF(NMX_F_TREE_W)[c] = s.tree_w;
+  AF(NMX_F_TREE_ACC)[c] = s.tree_acc;
+  AF(NMX_F_SUB_W)[c] = s.sub_w;
+  AF(NMX_F_SUB_ACC)[c] = s.sub_acc;
+  AF(NMX_F_PE_SUB)[c] = s.pe_sub;
+  AF(NMX_F_E_SUB)[c] = s.e_sub;
+  AF(NMX_F_DA_XT)[c] = s.da_xt;
+  AF(NMX_F_DA_XAVG)[c] = s.da_xavg;
+  AF(NMX_F_DA_GAVG)[c] = s.da_gavg;
+  AF(NMX_F_DA_PROX)[c] = s.da_prox;
+  AF(NMX_F_MEAN_ACC)[c] = s.mean_acc;
+  AF(NMX_F_LAST_ACC)[c] = s.last_acc;
+  AF(NMX_F_STEP_EFF)[c] = s.step_eff;
+}
+
 template <int TPC>
 __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   __shared__ float lds[TPC > 1 ? NRED * TPC * 64 : 1];
   const nmx_nuts_config& cfg = A.cfg;
-  Arena& a = A.a;
+  const Arena& a = A.a;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -129,9 +218,17 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   const uint64_t seed = cfg.seed;
 
-  int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  // active list [parity ^ 1] was consumed by the previous potential launch; clear it for
+  // the next step (which appends to it).  List [parity] was cleared by the previous step.
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+
+  ChainScalars S;
+  if (valid) load_scalars(a, c, S);
+  else S.phase = NMX_PH_DONE;
+  const int ph_in = S.phase;
+  int ph = ph_in;
   if (ph == NMX_PH_WAIT) {
-    const int slot_w = AI(NMX_F_ITER)[c] - 1 - cfg.iter_begin;
+    const int slot_w = S.it - 1 - cfg.iter_begin;
     const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
                         ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                         : cfg.num_chains;
@@ -140,13 +237,14 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
 
   float* const INVM = AV(NMX_F_INV_MASS);
   const bool leaf = ph == NMX_PH_LEAF;
-  const int dirR = leaf ? AI(NMX_F_DIR)[c] : 0;
-  const float seff = valid ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
+  const int dirR = leaf ? S.dir : 0;
+  const float seff = valid ? S.step_eff : 0.0f;
   float* ZF = dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
   float* RF = dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
   float* GF = dirR ? AV(NMX_F_GR) : AV(NMX_F_GL);
   float* const ZE = AV(NMX_F_Z_EVAL);
   float* const GE = AV(NMX_F_G_EVAL);
+  const float pe_eval = leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
 
   // ---------------- L1: finish the pending leapfrog (hmc_util.py:306-308) + kinetic energy
   float red[NRED];
@@ -170,20 +268,18 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
 
   // leaf scalars (_build_basetree, hmc_util.py:851-894)
-  float pe_new = 0.f, E_new = 0.f, dE = 0.f, w_new = 0.f, acc_new = 0.f;
+  float E_new = 0.f, dE = 0.f, w_new = 0.f, acc_new = 0.f;
   bool div_new = false;
   if (leaf) {
     const float ke = 0.5f * red[0];
-    pe_new = AF(NMX_F_PE_EVAL)[c];
-    E_new = pe_new + ke;
-    dE = E_new - AF(NMX_F_E0)[c];
+    E_new = pe_eval + ke;
+    dE = E_new - S.E0;
     if (isnan(dE)) dE = INFINITY;
     w_new = -dE;
     div_new = dE > cfg.max_delta_energy;
     acc_new = fminf(expf(-dE), 1.0f);
   }
 
-  // next-action flags
   bool prep_leaf = false;     // continue integrating from the same frontier
   bool new_doubling = false;  // pick a new direction, then prep_leaf
   bool iter_done = false;     // transition finished
@@ -192,31 +288,27 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   bool it_div = false;
 
   // ---------------- NUTS leaf bookkeeping (_iterative_build_subtree body, hmc_util.py:999-1061)
-  const int k = (leaf && is_nuts) ? AI(NMX_F_SUB_N)[c] : 0;
-  const int j = (leaf && is_nuts) ? AI(NMX_F_DEPTH)[c] : 0;
+  const int k = (leaf && is_nuts) ? S.sub_n : 0;
+  const int j = (leaf && is_nuts) ? S.depth : 0;
   bool take_leaf = false;
   int imin = 1, imax = 0;
   if (leaf && is_nuts) {
-    float sub_w = AF(NMX_F_SUB_W)[c];
-    float sub_acc = AF(NMX_F_SUB_ACC)[c];
     if (k == 0) {  // new_tree = new_leaf (:1019-1021)
       take_leaf = true;
-      sub_w = w_new;
-      sub_acc = acc_new;
+      S.sub_w = w_new;
+      S.sub_acc = acc_new;
     } else {  // _combine_tree(..., biased_transition=False) (:767-848, :749-753)
-      const float p = nmx_sigmoid(w_new - sub_w);
-      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_LEAF, j, k).x);
+      const float p = nmx_sigmoid(w_new - S.sub_w);
+      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_LEAF, j, k).x);
       take_leaf = u < p;
-      sub_w = nmx_logaddexp(sub_w, w_new);
-      sub_acc = sub_acc + acc_new;
+      S.sub_w = nmx_logaddexp(S.sub_w, w_new);
+      S.sub_acc = S.sub_acc + acc_new;
     }
-    AF(NMX_F_SUB_W)[c] = sub_w;
-    AF(NMX_F_SUB_ACC)[c] = sub_acc;
-    AI(NMX_F_SUB_DIV)[c] = div_new;
-    AI(NMX_F_SUB_N)[c] = k + 1;
+    S.sub_div = div_new;
+    S.sub_n = k + 1;
     if (take_leaf) {
-      AF(NMX_F_PE_SUB)[c] = pe_new;
-      AF(NMX_F_E_SUB)[c] = E_new;
+      S.pe_sub = pe_eval;
+      S.e_sub = E_new;
     }
     nmx_leaf_idx_to_ckpt_idxs(k, imin, imax);  // :1036
   }
@@ -276,37 +368,31 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
       if (i >= imin && i <= imax) turning_sub |= (red[2 * i] <= 0.0f) | (red[2 * i + 1] <= 0.0f);
-    const int sub_n = k + 1;
-    done_sub = (sub_n >= (1 << j)) || turning_sub || div_new;  // loop exit (:992-997)
+    done_sub = (S.sub_n >= (1 << j)) || turning_sub || div_new;  // loop exit (:992-997)
     if (done_sub) {
       // _double_tree -> _combine_tree(..., biased_transition=True) (:936-938, :756-764)
-      const float sub_w = AF(NMX_F_SUB_W)[c];
-      const float tree_w = AF(NMX_F_TREE_W)[c];
       const bool turning_tree =
           turning_sub || (red[2 * MAXD] <= 0.0f) || (red[2 * MAXD + 1] <= 0.0f);
-      float pb = expf(sub_w - tree_w);
+      float pb = expf(S.sub_w - S.tree_w);
       pb = isnan(pb) ? pb : fminf(pb, 1.0f);  // jnp.clip keeps NaN
       if (turning_sub || div_new) pb = 0.0f;
-      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_BIASED, j, 0).x);
+      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_BIASED, j, 0).x);
       take_biased = u < pb;
       if (take_biased) {
-        AF(NMX_F_PE)[c] = AF(NMX_F_PE_SUB)[c];
-        AF(NMX_F_ENERGY)[c] = AF(NMX_F_E_SUB)[c];
+        S.pe = S.pe_sub;
+        S.energy = S.e_sub;
       }
-      const int depth = j + 1;
-      const int tree_n = AI(NMX_F_TREE_N)[c] + sub_n;
-      const float tree_acc = AF(NMX_F_TREE_ACC)[c] + AF(NMX_F_SUB_ACC)[c];
-      AI(NMX_F_DEPTH)[c] = depth;
-      AF(NMX_F_TREE_W)[c] = nmx_logaddexp(tree_w, sub_w);
-      AI(NMX_F_TREE_DIV)[c] = div_new;
-      AF(NMX_F_TREE_ACC)[c] = tree_acc;
-      AI(NMX_F_TREE_N)[c] = tree_n;
-      AI(NMX_F_TURNING)[c] = turning_tree;
+      S.depth = j + 1;
+      S.tree_w = nmx_logaddexp(S.tree_w, S.sub_w);
+      S.tree_div = div_new;
+      S.tree_acc = S.tree_acc + S.sub_acc;
+      S.tree_n = S.tree_n + S.sub_n;
+      S.turning = turning_tree;
       // build_tree loop condition (:1153-1157)
-      if (depth >= AI(NMX_F_MAXDEPTH_CUR)[c] || turning_tree || div_new) {
+      if (S.depth >= S.maxdepth || turning_tree || div_new) {
         iter_done = true;
-        it_accept = tree_acc / (float)tree_n;  // _nuts_next :441
-        it_nsteps = tree_n;
+        it_accept = S.tree_acc / (float)S.tree_n;  // _nuts_next :441
+        it_nsteps = S.tree_n;
         it_div = div_new;
       } else {
         new_doubling = true;
@@ -319,23 +405,21 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   // ---------------- HMC leaf bookkeeping (_hmc_next, hmc.py:364-414)
   bool hmc_accept = false;
   if (leaf && !is_nuts) {
-    const int kk = AI(NMX_F_HMC_K)[c] + 1;
-    AI(NMX_F_HMC_K)[c] = kk;
-    const int n = AI(NMX_F_HMC_N)[c];
-    if (kk < n) {
+    S.hmc_k = S.hmc_k + 1;
+    if (S.hmc_k < S.hmc_n) {
       prep_leaf = true;
     } else {
-      const float u = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_ACCEPT, 0, 0).x);
+      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_ACCEPT, 0, 0).x);
       hmc_accept = u < acc_new;
       if (hmc_accept) {
-        AF(NMX_F_PE)[c] = pe_new;
-        AF(NMX_F_ENERGY)[c] = E_new;
+        S.pe = pe_eval;
+        S.energy = E_new;
       } else {
-        AF(NMX_F_ENERGY)[c] = AF(NMX_F_E0)[c];
+        S.energy = S.E0;
       }
       iter_done = true;
       it_accept = acc_new;
-      it_nsteps = n;
+      it_nsteps = S.hmc_n;
       it_div = div_new;
     }
   }
@@ -343,54 +427,49 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   // ---------------- transition end: adaptation scalars (warmup_adapter update_fn,
   // hmc_util.py:637-705), mean accept prob (hmc.py:509-513), collection slot.
   bool wf_update = false, finalize = false;
-  int wf_n = 0, slot = -1;
-  float new_step = 0.f;
+  int slot = -1;
   bool start_iter = ph == NMX_PH_START;
+  bool fin_done = false, fin_wait = false;
+  int fin_t = 0;
   if (iter_done) {
-    const int t = AI(NMX_F_ITER)[c];
-    new_step = AF(NMX_F_STEP_SIZE)[c];
+    const int t = S.it;
+    fin_t = t;
     if (t < cfg.num_warmup) {
+      float new_step = S.step;
       if (cfg.adapt_step_size) {  // dual_averaging update_fn (:103-126)
-        int da_t = AI(NMX_F_DA_T)[c] + 1;
+        S.da_t = S.da_t + 1;
         const float g = cfg.target_accept_prob - it_accept;
-        const float tt0 = (float)(da_t + 10);
-        float g_avg = (1.0f - 1.0f / tt0) * AF(NMX_F_DA_GAVG)[c] + g / tt0;
-        const float x_t = AF(NMX_F_DA_PROX)[c] - sqrtf((float)da_t) / 0.05f * g_avg;
-        const float weight_t = powf((float)da_t, -0.75f);
-        const float x_avg = (1.0f - weight_t) * AF(NMX_F_DA_XAVG)[c] + weight_t * x_t;
-        AI(NMX_F_DA_T)[c] = da_t;
-        AF(NMX_F_DA_GAVG)[c] = g_avg;
-        AF(NMX_F_DA_XT)[c] = x_t;
-        AF(NMX_F_DA_XAVG)[c] = x_avg;
-        new_step = (t == cfg.num_warmup - 1) ? expf(x_avg) : expf(x_t);  // :662-666
+        const float tt0 = (float)(S.da_t + 10);
+        S.da_gavg = (1.0f - 1.0f / tt0) * S.da_gavg + g / tt0;
+        S.da_xt = S.da_prox - sqrtf((float)S.da_t) / 0.05f * S.da_gavg;
+        const float weight_t = powf((float)S.da_t, -0.75f);
+        S.da_xavg = (1.0f - weight_t) * S.da_xavg + weight_t * S.da_xt;
+        new_step = (t == cfg.num_warmup - 1) ? expf(S.da_xavg) : expf(S.da_xt);  // :662-666
         new_step = fminf(fmaxf(new_step, 1.17549435e-38f), 3.40282347e+38f);  // :670-672
       }
-      const int widx = AI(NMX_F_WINDOW_IDX)[c];
+      const int widx = S.widx;
       const bool middle = (0 < widx) && (widx < cfg.num_windows - 1);
       wf_update = cfg.adapt_mass_matrix && middle;
-      if (wf_update) wf_n = AI(NMX_F_WF_N)[c] + 1;
+      if (wf_update) S.wf_n = S.wf_n + 1;
       const bool at_end = t == cfg.window_end[widx];
-      AI(NMX_F_WINDOW_IDX)[c] = widx + (at_end ? 1 : 0);
+      S.widx = widx + (at_end ? 1 : 0);
       finalize = at_end && middle;  // _update_at_window_end (:596-635)
       if (finalize && cfg.adapt_step_size) {
-        AF(NMX_F_DA_PROX)[c] = logf(10.0f) + logf(new_step);
-        AF(NMX_F_DA_XT)[c] = 0.0f;
-        AF(NMX_F_DA_XAVG)[c] = 0.0f;
-        AF(NMX_F_DA_GAVG)[c] = 0.0f;
-        AI(NMX_F_DA_T)[c] = 0;
+        S.da_prox = logf(10.0f) + logf(new_step);
+        S.da_xt = 0.0f;
+        S.da_xavg = 0.0f;
+        S.da_gavg = 0.0f;
+        S.da_t = 0;
       }
-      AF(NMX_F_STEP_SIZE)[c] = new_step;
-      AI(NMX_F_WF_N)[c] = (finalize && cfg.adapt_mass_matrix) ? 0 : (wf_update ? wf_n : AI(NMX_F_WF_N)[c]);
+      S.step = new_step;
     }
     const int itr = t + 1;
     const int nn = t < cfg.num_warmup ? itr : itr - cfg.num_warmup;
-    const float mean_acc = AF(NMX_F_MEAN_ACC)[c];
-    const float mean_new = mean_acc + (it_accept - mean_acc) / (float)nn;
-    AF(NMX_F_MEAN_ACC)[c] = mean_new;
-    AF(NMX_F_LAST_ACC)[c] = it_accept;
-    AI(NMX_F_LAST_NSTEPS)[c] = it_nsteps;
-    AI(NMX_F_LAST_DIV)[c] = it_div;
-    AI(NMX_F_ITER)[c] = itr;
+    S.mean_acc = S.mean_acc + (it_accept - S.mean_acc) / (float)nn;
+    S.last_acc = it_accept;
+    S.last_nsteps = it_nsteps;
+    S.last_div = it_div;
+    S.it = itr;
     // fori_collect slot (numpyro/util.py:330-346): idx = (i - start) // thinning, last write wins
     if (cfg.collection_size > 0 && t >= cfg.collect_start) {
       const int off = t - cfg.collect_start;
@@ -399,24 +478,23 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
         if (s < cfg.collection_size) slot = s;
       }
     }
-    if (slot >= 0) {
+    if (slot >= 0 && wv == 0) {
       float* F = A.fields + (size_t)slot * NMX_NUM_COLLECT * ldc;
-      F[NMX_C_POTENTIAL_ENERGY * ldc + c] = AF(NMX_F_PE)[c];
-      F[NMX_C_ENERGY * ldc + c] = AF(NMX_F_ENERGY)[c];
+      F[NMX_C_POTENTIAL_ENERGY * ldc + c] = S.pe;
+      F[NMX_C_ENERGY * ldc + c] = S.energy;
       F[NMX_C_ACCEPT_PROB * ldc + c] = it_accept;
-      F[NMX_C_MEAN_ACCEPT_PROB * ldc + c] = mean_new;
-      F[NMX_C_STEP_SIZE * ldc + c] = AF(NMX_F_STEP_SIZE)[c];
+      F[NMX_C_MEAN_ACCEPT_PROB * ldc + c] = S.mean_acc;
+      F[NMX_C_STEP_SIZE * ldc + c] = S.step;
       F[NMX_C_NUM_STEPS * ldc + c] = (float)it_nsteps;
       F[NMX_C_DIVERGING * ldc + c] = it_div ? 1.0f : 0.0f;
       F[NMX_C_ITER * ldc + c] = (float)itr;
     }
     if (itr >= cfg.iter_end) {
-      AI(NMX_F_PHASE)[c] = NMX_PH_DONE;
-      if (wv == 0) atomicAdd(&a.counters[0], 1);
+      S.phase = NMX_PH_DONE;
+      fin_done = true;
     } else if (cfg.sync_chains) {
-      AI(NMX_F_PHASE)[c] = NMX_PH_WAIT;
-      const int fs = t - cfg.iter_begin;
-      if (wv == 0 && fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
+      S.phase = NMX_PH_WAIT;
+      fin_wait = true;
     } else {
       start_iter = true;
     }
@@ -436,6 +514,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
     float* const W2 = AV(NMX_F_WF_M2);
     float* const MS = AV(NMX_F_MASS_SQRT);
     float* const samp = slot >= 0 ? A.samples + (size_t)slot * D * ldc : nullptr;
+    const int wf_n = S.wf_n;
     const float wfn = (float)wf_n;
     for (int d = wv; d < D; d += TPC) {
       const size_t idx = (size_t)d * ldc + c;
@@ -474,44 +553,39 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       }
     }
   }
+  if (finalize && cfg.adapt_mass_matrix) S.wf_n = 0;
 
   // ---------------- new transition: momentum, tree init (sample_kernel hmc.py:471-481,
   // build_tree :1127-1151), first direction; new doubling direction (:1160-1162).
   int new_dir = dirR;
-  float step_eff = seff;
   if (start_iter) {
-    const int it = AI(NMX_F_ITER)[c];
-    const float step = AF(NMX_F_STEP_SIZE)[c];
     if (is_nuts) {
-      step_eff = step;
-      AI(NMX_F_MAXDEPTH_CUR)[c] =
-          it < cfg.num_warmup ? cfg.max_tree_depth_warmup : cfg.max_tree_depth;  // hmc.py:488-490
-      new_dir = nmx_u01(nmx_rng(seed, gch, it, NMX_EV_DIRECTION, 0, 0).x) < 0.5f;
+      S.step_eff = S.step;
+      S.maxdepth = S.it < cfg.num_warmup ? cfg.max_tree_depth_warmup : cfg.max_tree_depth;  // hmc.py:488-490
+      new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, 0, 0).x) < 0.5f;
     } else {
       int n;
       if (cfg.num_steps > 0) n = cfg.num_steps;
-      else n = (int)ceilf(cfg.trajectory_length / step);  // _get_num_steps hmc.py:85-89
+      else n = (int)ceilf(cfg.trajectory_length / S.step);  // _get_num_steps hmc.py:85-89
       n = n < 1 ? 1 : n;
-      step_eff = cfg.trajectory_length > 0.0f ? cfg.trajectory_length / (float)n : step;
-      AI(NMX_F_HMC_N)[c] = n;
-      AI(NMX_F_HMC_K)[c] = 0;
+      S.step_eff = cfg.trajectory_length > 0.0f ? cfg.trajectory_length / (float)n : S.step;
+      S.hmc_n = n;
+      S.hmc_k = 0;
       new_dir = 1;
     }
-    AF(NMX_F_STEP_EFF)[c] = step_eff;
-    AI(NMX_F_DEPTH)[c] = 0;
-    AI(NMX_F_SUB_N)[c] = 0;
-    AI(NMX_F_TREE_N)[c] = 0;
-    AI(NMX_F_TURNING)[c] = 0;
-    AI(NMX_F_TREE_DIV)[c] = 0;
-    AF(NMX_F_TREE_W)[c] = 0.0f;
-    AF(NMX_F_TREE_ACC)[c] = 0.0f;
-    AI(NMX_F_DIR)[c] = new_dir;
-    AI(NMX_F_PHASE)[c] = NMX_PH_LEAF;
+    S.depth = 0;
+    S.sub_n = 0;
+    S.tree_n = 0;
+    S.turning = 0;
+    S.tree_div = 0;
+    S.tree_w = 0.0f;
+    S.tree_acc = 0.0f;
+    S.dir = new_dir;
+    S.phase = NMX_PH_LEAF;
   } else if (new_doubling) {
-    const int depth = AI(NMX_F_DEPTH)[c];
-    new_dir = nmx_u01(nmx_rng(seed, gch, AI(NMX_F_ITER)[c], NMX_EV_DIRECTION, depth, 0).x) < 0.5f;
-    AI(NMX_F_DIR)[c] = new_dir;
-    AI(NMX_F_SUB_N)[c] = 0;
+    new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, S.depth, 0).x) < 0.5f;
+    S.dir = new_dir;
+    S.sub_n = 0;
     prep_leaf = true;
   }
 
@@ -519,6 +593,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
   // position z_eval (velocity_verlet update_fn first half, hmc_util.py:297-301).
 #pragma unroll
   for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
+  const float step_eff = S.step_eff;
   if (start_iter || prep_leaf) {
     float* const ZFn = new_dir ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
     float* const RFn = new_dir ? AV(NMX_F_RR) : AV(NMX_F_RL);
@@ -533,7 +608,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       float* const GP = AV(NMX_F_ZGRAD);
       float* const MS = AV(NMX_F_MASS_SQRT);
       float* const RST = AV(NMX_F_RSUM);
-      const uint32_t it = (uint32_t)AI(NMX_F_ITER)[c];
+      const uint32_t it = (uint32_t)S.it;
       // blocks of 4 coordinates share one Philox call (momentum_generator hmc.py:92-110)
       for (int blk = wv; 4 * blk < D; blk += TPC) {
         const nmx_u4 x = nmx_rng(seed, gch, it, NMX_EV_MOMENTUM, blk, 0);
@@ -569,14 +644,40 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
         RFn[idx] = rh;
         ZE[idx] = ZFn[idx] + es * (INVM[idx] * rh);
       }
-      AI(NMX_F_PHASE)[c] = NMX_PH_LEAF;
+      S.phase = NMX_PH_LEAF;
     }
   }
   block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
   if (start_iter) {
-    const float E0 = AF(NMX_F_PE)[c] + 0.5f * red[0];  // build_tree :1130
-    AF(NMX_F_E0)[c] = E0;
-    AF(NMX_F_ENERGY)[c] = E0;  // proposal energy of the initial tree (:1137)
+    S.E0 = S.pe + 0.5f * red[0];  // build_tree :1130
+    S.energy = S.E0;              // proposal energy of the initial tree (:1137)
+  }
+
+  if (wv == 0 && valid) {
+    if (S.phase != ph_in || leaf || start_iter || iter_done) store_scalars(a, c, S);
+    if (fin_done) atomicAdd(&a.counters[0], 1);
+    if (fin_wait) {
+      const int fs = fin_t - cfg.iter_begin;
+      if (fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
+    }
+  }
+  // ---------------- compacted list of chains whose next leaf is pending: the potential
+  // kernels then cost in proportion to the chains still integrating (tail of a run,
+  // chains waiting in sync mode).  List order is arbitrary; a chain's result does not
+  // depend on its position.
+  if (wv == 0) {
+    const bool pend = (start_iter || prep_leaf);
+    const uint64_t m = __ballot(pend);
+    if (m) {
+      int base = 0;
+      if (lane == __builtin_ctzll(m))
+        base = atomicAdd(&a.counters[2 + cfg.parity], __builtin_popcountll(m));
+      base = __shfl(base, __builtin_ctzll(m));
+      if (pend) {
+        const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
+        a.active_idx[(size_t)cfg.parity * ldc + pos] = c;
+      }
+    }
   }
 }
 
@@ -701,8 +802,8 @@ Arena arena_of(const nmx_nuts_config* cfg, void* base) {
 }
 
 int tpc_for_dim(int D) {
-  if (D <= 64) return 1;
-  if (D <= 1024) return 4;
+  if (D < 16) return 1;
+  if (D <= 256) return 8;
   return 16;
 }
 
@@ -788,9 +889,10 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   args.transform = transform;
   const int grid = cfg->ldc / 64;
   hipStream_t s = (hipStream_t)stream;
+  if (cfg->parity != 0 && cfg->parity != 1) return nmx_fail(NMX_ERR_INVALID, "parity must be 0 or 1");
   switch (tpc_for_dim(cfg->dim)) {
     case 1: hipLaunchKernelGGL(k_nuts_step<1>, dim3(grid), dim3(64), 0, s, args); break;
-    case 4: hipLaunchKernelGGL(k_nuts_step<4>, dim3(grid), dim3(256), 0, s, args); break;
+    case 8: hipLaunchKernelGGL(k_nuts_step<8>, dim3(grid), dim3(512), 0, s, args); break;
     default: hipLaunchKernelGGL(k_nuts_step<16>, dim3(grid), dim3(1024), 0, s, args); break;
   }
   return nmx_check_launch("k_nuts_step");

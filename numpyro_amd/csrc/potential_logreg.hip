@@ -21,6 +21,7 @@
 // partials go to slabs reduced in fixed order by k_logreg_finalize.  Workgroups of the
 // same split are placed on one XCD (blockIdx % 8) so the chain groups share X tiles in L2.
 #include <math.h>
+#include <stdlib.h>
 
 #include "nmx_api_internal.h"
 #include "nmx_common.h"
@@ -29,7 +30,8 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BR = 64;       // rows per LDS stage
+constexpr int BR = 64;       // rows per LDS stage of the generic kernel
+constexpr int PACK = 128;    // packed row padding (= stage of the row-lane kernel)
 constexpr int NW = 4;        // waves per workgroup
 constexpr int CPB = NW * 32; // chains per workgroup
 constexpr int MAX_S = 128;   // row splits
@@ -37,10 +39,11 @@ constexpr int LDS_SLACK = 64;
 
 inline int k_of(int D) { return (D + 1) / 2 * 2; }
 inline int xs_of(int D) { return k_of(D) + 1; }
-inline int64_t ntiles_of(int64_t n) { return (n + BR - 1) / BR; }
+inline int64_t npad_of(int64_t n) { return (n + PACK - 1) / PACK * PACK; }
+inline int64_t ntiles_of(int64_t n) { return npad_of(n) / BR; }
 
 int num_splits(int64_t n_rows) {
-  int64_t t = ntiles_of(n_rows);
+  int64_t t = npad_of(n_rows) / PACK;
   int64_t s = t / 16;
   s = s / 8 * 8;
   if (s < 8) s = 8;
@@ -84,9 +87,10 @@ __global__ __launch_bounds__(NW * 64) void k_logreg_tiles(const float* __restric
   const int h = lane >> 5;
   const int l31 = lane & 31;
   const int ldc = ev.ldc;
-  const int c = cg * CPB + w * 32 + l31;
-  const bool cin = c < ldc;
-  const bool act = c < ev.num_chains && (ev.phase == nullptr || ev.phase[c] >= NMX_PH_LEAF);
+  const int pos = cg * CPB + w * 32 + l31;  // batch position (slab column)
+  const bool cin = pos < ldc;
+  const int c = cin ? nmx_eval_chain(ev, pos) : -1;
+  const bool act = c >= 0;
   const bool wave_active = __any(act);
   if (!__syncthreads_or(wave_active)) return;
 
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(NW * 64) void k_logreg_tiles(const float* __restric
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = 2 * s + h;
-    zb[s] = (k < D && cin) ? ev.z[(size_t)k * ldc + c] : 0.0f;
+    zb[s] = (k < D && act) ? ev.z[(size_t)k * ldc + c] : 0.0f;
   }
   f32x16 g0, g1;
 #pragma unroll
@@ -165,29 +169,209 @@ __global__ __launch_bounds__(NW * 64) void k_logreg_tiles(const float* __restric
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (d < D) gpart[((size_t)split * D + d) * ldc + c] = g0[r];
-      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + c] = g1[r];
+      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = g0[r];
+      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = g1[r];
     }
   }
   pe += __shfl_xor(pe, 32);
-  if (wave_active && cin && h == 0) pepart[(size_t)split * ldc + c] = pe;
+  if (wave_active && cin && h == 0) pepart[(size_t)split * ldc + pos] = pe;
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-lane kernel (the production path for covtype, D = 55).
+//
+// Workgroup = 4 waves sharing ONE 32-chain tile; each stage is 128 rows (4 subtiles of 32)
+// filled into LDS by global_load_lds (double-buffered, no VGPR staging), and wave w takes
+// subtile w, so the 4 waves are 4 "row lanes" of the split.  At the end the lanes' partial
+// gradients are combined in a fixed order.  Compared with one wave walking all rows of a
+// split this gives 4x the parallelism per chain, which is what bounds a launch when only a
+// few chains are still integrating (the tail of a run, sync-mode stragglers); the
+// summation order depends on n_rows only, never on how many chains are evaluated.
+// ---------------------------------------------------------------------------------------
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <int KS>
+__device__ __forceinline__ void gemm1(const float* xt, const float (&zb)[KS], int l31, int h, f32x16& acc) {
+  constexpr int XS = 2 * KS + 1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[s], acc, 0, 0, 0);
+}
+
+// acc <- sigmoid(l) - y in place; accumulates sum(max(l,0) - l*y) and sum(log2(1+e^-|l|))
+template <int KS, bool MASK>
+__device__ __forceinline__ void epilogue(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
+                                         float& lin, float& lg2) {
+  constexpr int XS = 2 * KS + 1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float y = xt[rr * XS + (XS - 1)];
+    const float l = acc[r];
+    const float e = __builtin_amdgcn_exp2f(-fabsf(l) * LOG2E);
+    const float ope = 1.0f + e;
+    const float inv = __builtin_amdgcn_rcpf(ope);
+    const float num = l >= 0.0f ? 1.0f : e;
+    float res = num * inv - y;
+    float li = fmaxf(l, 0.0f) - l * y;
+    float lo = __builtin_amdgcn_logf(ope);
+    if (MASK) {
+      const bool ok = rowbase + rr < n_rows;
+      res = ok ? res : 0.0f;
+      li = ok ? li : 0.0f;
+      lo = ok ? lo : 0.0f;
+    }
+    lin += li;
+    lg2 += lo;
+    acc[r] = res;
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void gemm2(const float* xt, const f32x16& res, int l31, int h, f32x16& g0, f32x16& g1) {
+  constexpr int XS = 2 * KS + 1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], res[r], g0, 0, 0, 0);
+    if (KS > 16) g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], res[r], g1, 0, 0, 0);
+  }
+}
+
+constexpr int RL_WAVES = 4;             // row lanes per workgroup
+constexpr int RL_ROWS = 32 * RL_WAVES;  // rows per stage (= PACK)
+static_assert(RL_ROWS == PACK, "row-lane stage must equal the packing granularity");
+
+template <int KS, int NBUF>
+__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes(const float* __restrict__ Xp, int64_t n_rows,
+                                                                      int nstages, int D, int S, int Gt,
+                                                                      nmx_eval_batch ev, float* __restrict__ gpart,
+                                                                      double* __restrict__ pepart) {
+  constexpr int XS = 2 * KS + 1;
+  constexpr int STAGE = RL_ROWS * XS;               // floats per stage
+  constexpr int BUF = (STAGE + LDS_SLACK + 255) / 256 * 256;
+  constexpr int CHUNKS = STAGE / 4;                 // 16-byte pieces
+  constexpr int NINST = (CHUNKS + 63) / 64;         // wave-instructions per stage
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7;
+  const int q = b >> 3;
+  const int ct = q % Gt;
+  const int split = (q / Gt) * 8 + xcd;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int pos = ct * 32 + l31;  // batch position (slab column); same chains in all 4 waves
+  const bool cin = pos < ldc;
+  const int c = cin ? nmx_eval_chain(ev, pos) : -1;
+  const bool act = c >= 0;
+  if (!__any(act)) return;  // identical in all waves of the workgroup
+
+  const int per = (nstages + S - 1) / S;
+  const int t0 = split * per;
+  const int t1 = min(t0 + per, nstages);
+
+  auto stage_in = [&](int t, int buf) {
+    const char* src = reinterpret_cast<const char*>(Xp + (size_t)t * STAGE);
+    float* dst = xs + buf * BUF;
+#pragma unroll
+    for (int i = w; i < NINST; i += RL_WAVES) {
+      const int chunk = i * 64 + lane;
+      if (chunk < CHUNKS)
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + chunk * 16),
+                                         (void __attribute__((address_space(3)))*)(dst + i * 256), 16, 0, 0);
+    }
+  };
+
+  float zb[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    zb[s] = (k < D && act) ? ev.z[(size_t)k * ldc + c] : 0.0f;
+  }
+  f32x16 g0, g1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    g0[r] = 0.0f;
+    g1[r] = 0.0f;
+  }
+  double pe = 0.0;
+  if (NBUF == 2 && t0 < t1) stage_in(t0, 0);
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int buf = NBUF == 2 ? (t - t0) & 1 : 0;
+    if (NBUF == 2) {
+      if (t + 1 < t1) stage_in(t + 1, buf ^ 1);
+    } else {
+      stage_in(t, 0);
+      __syncthreads();
+    }
+    const float* xt = xs + buf * BUF + w * 32 * XS;
+    const int64_t rb = (int64_t)t * RL_ROWS + w * 32;
+    f32x16 a0;
+    float lin = 0.0f, lg2 = 0.0f;
+    gemm1<KS>(xt, zb, l31, h, a0);
+    if (rb + 32 <= n_rows) epilogue<KS, false>(xt, h, rb, n_rows, a0, lin, lg2);
+    else epilogue<KS, true>(xt, h, rb, n_rows, a0, lin, lg2);
+    gemm2<KS>(xt, a0, l31, h, g0, g1);
+    pe += (double)lin + (double)lg2 * (double)LN2;
+    __syncthreads();  // drains this stage's global_load_lds (vmcnt(0)) and frees buf
+  }
+  pe += __shfl_xor(pe, 32);
+
+  // fixed-order combination of the 4 row lanes: lane partials staged through LDS
+  float* red = xs;                                   // [RL_WAVES][32][64] floats
+  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[(w * 32 + r) * 64 + lane] = g0[r];
+    red[(w * 32 + 16 + r) * 64 + lane] = g1[r];
+  }
+  red_pe[w * 64 + lane] = pe;
+  __syncthreads();
+  if (w == 0 && cin) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
+#pragma unroll
+      for (int ww = 1; ww < RL_WAVES; ++ww) {
+        s0 += red[(ww * 32 + r) * 64 + lane];
+        s1 += red[(ww * 32 + 16 + r) * 64 + lane];
+      }
+      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
+      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
+    }
+    if (h == 0) {
+      double sp = red_pe[lane];
+#pragma unroll
+      for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
+      pepart[(size_t)split * ldc + pos] = sp;
+    }
+  }
 }
 
 __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
                                   int D, nmx_eval_batch ev) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int pos = blockIdx.x * blockDim.x + threadIdx.x;
   const int d = blockIdx.y;
-  if (c >= ev.num_chains) return;
-  if (ev.phase && ev.phase[c] < NMX_PH_LEAF) return;
+  const int c = nmx_eval_chain(ev, pos);
+  if (c < 0) return;
   const int ldc = ev.ldc;
   if (d < D) {
     float s = 0.0f;
-    for (int sp = 0; sp < S; ++sp) s += gpart[((size_t)sp * D + d) * ldc + c];
+    for (int sp = 0; sp < S; ++sp) s += gpart[((size_t)sp * D + d) * ldc + pos];
     const size_t idx = (size_t)d * ldc + c;
     ev.grad[idx] = s + ev.z[idx];
   } else {
     double s = 0.0;
-    for (int sp = 0; sp < S; ++sp) s += pepart[(size_t)sp * ldc + c];
+    for (int sp = 0; sp < S; ++sp) s += pepart[(size_t)sp * ldc + pos];
     double zz = 0.0;
     for (int k = 0; k < D; ++k) {
       const double z = ev.z[(size_t)k * ldc + c];
@@ -202,6 +386,26 @@ int check_ev(const nmx_eval_batch* ev) {
   if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
     return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
   return NMX_OK;
+}
+
+// Kernel variant: NMX_LOGREG_VARIANT=0 forces the generic kernel (A/B experiments).
+int variant() {
+  const char* e = getenv("NMX_LOGREG_VARIANT");
+  return e ? atoi(e) : 5;
+}
+
+template <int KS, int NBUF>
+void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
+                     double* pepart, hipStream_t s) {
+  const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
+  const int S = num_splits(n_rows);
+  const int Gt = ev->ldc / 32;
+  constexpr int BUF = (RL_ROWS * (2 * KS + 1) + LDS_SLACK + 255) / 256 * 256;
+  size_t lds = (size_t)NBUF * BUF * sizeof(float);
+  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
+  if (lds < red) lds = red;
+  hipLaunchKernelGGL((k_logreg_rowlanes<KS, NBUF>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages,
+                     D, S, Gt, *ev, gpart, pepart);
 }
 
 template <int KS, bool EXACT>
@@ -221,7 +425,7 @@ extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return num_splits(n_rows)
 
 extern "C" size_t nmx_logreg_packed_bytes(int64_t n_rows, int dim) {
   if (n_rows <= 0 || dim <= 0) return 0;
-  return (size_t)(ntiles_of(n_rows) * BR) * xs_of(dim) * sizeof(float);
+  return (size_t)npad_of(n_rows) * xs_of(dim) * sizeof(float);
 }
 
 extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, int dim, void* packed,
@@ -231,7 +435,7 @@ extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, i
     return nmx_fail(NMX_ERR_INVALID, "logreg_pack: need n_rows > 0 and 0 < dim <= 64 (got %lld, %d)",
                     (long long)n_rows, dim);
   const int XS = xs_of(dim);
-  const int64_t npad = ntiles_of(n_rows) * BR;
+  const int64_t npad = npad_of(n_rows);
   const int64_t total = npad * XS;
   hipLaunchKernelGGL(k_logreg_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      X, y, n_rows, dim, XS, npad, (float*)packed);
@@ -259,7 +463,10 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   double* pepart = (double*)((char*)workspace + (gbytes + 255) / 256 * 256);
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
-  if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
+  const int var = variant();
+  if (KS == 28 && var == 4) launch_rowlanes<28, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
+  else if (KS == 28 && var == 5) launch_rowlanes<28, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 16) launch_tiles<16, false>(Xp, n_rows, dim, ev, gpart, pepart, s);

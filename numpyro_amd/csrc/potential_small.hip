@@ -6,13 +6,9 @@
 
 namespace {
 
-__device__ __forceinline__ bool needs_eval(const nmx_eval_batch& ev, int c) {
-  return c < ev.num_chains && (ev.phase == nullptr || ev.phase[c] >= NMX_PH_LEAF);
-}
-
 __global__ void k_diag_normal(const float* mu, const float* prec, int D, nmx_eval_batch ev) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (!needs_eval(ev, c)) return;
+  const int c = nmx_eval_chain(ev, blockIdx.x * blockDim.x + threadIdx.x);
+  if (c < 0) return;
   float u = 0.0f;
   for (int d = 0; d < D; ++d) {
     const size_t idx = (size_t)d * ev.ldc + c;
@@ -32,8 +28,8 @@ __device__ __forceinline__ float nlpN(float x, float loc, float scale) {
 
 // z = (mu, u = log tau, theta[J]); SURVEY.md Appendix A, C0.
 __global__ void k_eight_schools(const float* y, const float* sigma, int J, nmx_eval_batch ev) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (!needs_eval(ev, c)) return;
+  const int c = nmx_eval_chain(ev, blockIdx.x * blockDim.x + threadIdx.x);
+  if (c < 0) return;
   const int ldc = ev.ldc;
   const float mu = ev.z[c];
   const float u = ev.z[(size_t)ldc + c];

@@ -97,9 +97,15 @@ class Engine:
         nbytes = lib().nmx_nuts_arena_bytes(self.C, self.D, self.md, self.iter_capacity)
         self.arena = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
         self._views = {}
-        self.eval_batch = EvalBatch(ptr(self.view("z_eval")), ptr(self.view("g_eval")),
-                                    ptr(self.view("pe_eval")), ptr(self.view("phase")),
-                                    self.C, self.ldc)
+        z, g, pe, ph = (ptr(self.view(n)) for n in ("z_eval", "g_eval", "pe_eval", "phase"))
+        idx = self.view("active_idx")
+        cnt = self.view("counters")
+        # dense batch (init: every chain with phase >= LEAF) and the two compacted lists
+        self.eval_batch = EvalBatch(z=z, grad=g, pe=pe, phase=ph, active_idx=None, active_count=None,
+                                    num_chains=self.C, ldc=self.ldc)
+        self.eval_lists = [EvalBatch(z=z, grad=g, pe=pe, phase=ph, active_idx=ptr(idx) + 4 * p * self.ldc,
+                                     active_count=ptr(cnt) + 4 * (2 + p), num_chains=self.C, ldc=self.ldc)
+                           for p in (0, 1)]
 
     def view(self, name: str):
         """torch view of an arena field: scalars [ldc], vectors [D, ldc], ckpts [md, D, ldc]."""
@@ -226,12 +232,17 @@ class Engine:
         launches = 0
         step = lib().nmx_nuts_step
         sp, fp, tp = ptr(samples), ptr(fields), ptr(tr)
+        cfg = self.cfg
+        parity = 0
+        cfg.parity = parity
         check(step(cfgp, arena, sp, fp, tp, s), "nmx_nuts_step")
         evaluate = self.potential.evaluate
-        evb = self.eval_batch
+        lists = self.eval_lists
         while True:
             for _ in range(poll_every):
-                evaluate(evb, s)
+                evaluate(lists[parity], s)
+                parity ^= 1
+                cfg.parity = parity
                 check(step(cfgp, arena, sp, fp, tp, s), "nmx_nuts_step")
             launches += poll_every
             if pending:

@@ -41,10 +41,10 @@ FIELDS = [
     "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "pe_eval",
     "z", "zgrad", "zl", "rl", "gl", "zr", "rr", "gr", "zsub", "gsub", "rsum", "rsum_sub",
     "inv_mass", "mass_sqrt", "wf_mean", "wf_m2", "z_eval", "g_eval",
-    "ckpt_r", "ckpt_rsum", "counters", "finished",
+    "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished",
 ]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
-INT_FIELDS = set(FIELDS[:FIELDS.index("step_size")]) | {"counters", "finished"}
+INT_FIELDS = set(FIELDS[:FIELDS.index("step_size")]) | {"counters", "finished", "active_idx"}
 VECTOR_FIELDS = set(FIELDS[FIELDS.index("z"):FIELDS.index("ckpt_r")])
 CKPT_FIELDS = {"ckpt_r", "ckpt_rsum"}
 
@@ -69,7 +69,7 @@ class NutsConfig(ctypes.Structure):
         ("num_windows", ctypes.c_int32), ("window_end", ctypes.c_int32 * MAX_WINDOWS),
         ("seed", ctypes.c_uint64), ("chain_offset", ctypes.c_int64),
         ("collect_start", ctypes.c_int32), ("collect_thinning", ctypes.c_int32),
-        ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32),
+        ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32), ("parity", ctypes.c_int32),
     ]
 
 
@@ -77,6 +77,7 @@ class EvalBatch(ctypes.Structure):
     """Mirror of nmx_eval_batch."""
 
     _fields_ = [("z", c_vp), ("grad", c_vp), ("pe", c_vp), ("phase", c_vp),
+                ("active_idx", c_vp), ("active_count", c_vp),
                 ("num_chains", ctypes.c_int32), ("ldc", ctypes.c_int32)]
 
 

@@ -87,29 +87,70 @@ def test_engine_matches_oracle_eight_schools(device, algo):
 
 
 @pytest.mark.parametrize("algo", ["NUTS", "HMC"])
-def test_engine_matches_oracle_fixed_step(device, algo):
+@pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300)])
+def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     """No adaptation, fixed step size: every transition is a deterministic function of
-    the Philox stream; device and oracle must take the same discrete path."""
+    the Philox stream; device and oracle must take the same discrete path.  dim 40 / 300
+    exercise the multi-wave (8 / 16 waves per 64 chains) step kernel."""
     seed, C, T = 77, 64, 3
-    rs = np.random.RandomState(0)
-    X = rs.randn(300, 4).astype(np.float32)
-    y = (rs.rand(300) < 1 / (1 + np.exp(-X @ np.array([1.0, -0.5, 0.3, 0.0])))).astype(np.float32)
+    rs = np.random.RandomState(dim)
+    if model == "logreg":
+        X = rs.randn(300, dim).astype(np.float32)
+        beta = rs.randn(dim) * 0.5 / np.sqrt(dim)
+        y = (rs.rand(300) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
+        args, fm = (X, y), P.logistic_regression
+        ref = OP.LogisticRegression(X, y, dtype=np.float32)
+        site = "coefs"
+        step = 0.02
+    else:
+        mu = rs.randn(dim).astype(np.float32)
+        sd = (0.5 + rs.rand(dim)).astype(np.float32)
+        args, fm = (mu, sd), P.diag_normal
+        ref = OP.IsoNormal(mu, sd, dtype=np.float32)
+        site = "x"
+        step = 0.05
     kcls = NUTS if algo == "NUTS" else HMC
-    kw = dict(step_size=0.02, adapt_step_size=False, adapt_mass_matrix=False)
+    kw = dict(step_size=step, adapt_step_size=False, adapt_mass_matrix=False)
     if algo == "HMC":
-        kw["trajectory_length"] = 0.3
-    mcmc, warm = _run_engine((X, y), P.logistic_regression, C, 0, T, seed, kernel_cls=kcls, **kw)
-    ns_dev, site = _dev_paths(mcmc, warm)
-    ref = OP.LogisticRegression(X, y, dtype=np.float32)
+        kw["trajectory_length"] = 15 * step
+    mcmc, warm = _run_engine(args, fm, C, 0, T, seed, kernel_cls=kcls, **kw)
+    ns_dev, sites = _dev_paths(mcmc, warm)
     match = 0
     for c in range(C):
-        states = _oracle_chain(ref.pe_grad, 4, seed, c, 0, T, algo=algo, **kw)
+        states = _oracle_chain(ref.pe_grad, dim, seed, c, 0, T, algo=algo, **kw)
         ns = np.array([s.num_steps for s in states])
         if np.array_equal(ns, ns_dev[c]):
             match += 1
             z = np.stack([s.z for s in states])
-            np.testing.assert_allclose(site["coefs"][c], z, rtol=1e-3, atol=1e-4)
+            np.testing.assert_allclose(sites[site][c], z, rtol=1e-3, atol=1e-4)
     assert match >= int(0.95 * C), f"only {match}/{C} chains reproduced the oracle path"
+
+
+def test_num_steps_equals_potential_evaluations(device):
+    """Every leaf consumes exactly one potential evaluation (the compacted list length),
+    summed over the run -- guards the multi-wave step kernel's state handling."""
+    rs = np.random.RandomState(3)
+    X = rs.randn(2000, 55).astype(np.float32)
+    y = (rs.rand(2000) < 0.5).astype(np.float32)
+    mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=20, num_samples=10, num_chains=200)
+    mcmc.warmup(0, X, y)
+    eng = mcmc._engine
+    cnt = eng.view("counters")
+    logged = torch.zeros(100000, dtype=torch.int32, device=eng.device)
+    n = [0]
+    orig = eng.potential.evaluate
+
+    def counting(ev, s):
+        p = 0 if ev is eng.eval_lists[0] else 1
+        logged[n[0]] = cnt[2 + p]
+        n[0] += 1
+        orig(ev, s)
+
+    eng.potential.evaluate = counting
+    mcmc.run(1, X, y, extra_fields=("num_steps",))
+    eng.potential.evaluate = orig
+    evals = int(logged[:n[0]].sum().item())
+    assert evals == int(mcmc.get_extra_fields()["num_steps"].sum().item())
 
 
 def test_sync_and_async_schedules_are_bitwise_identical(device):

@@ -31,7 +31,8 @@ def _eval(pot, Z, device, phase=None):
     if phase is not None:
         ph = torch.zeros(ldc, dtype=torch.int32, device=device)
         ph[:C] = torch.from_numpy(phase.astype(np.int32)).to(device)
-    ev = native.EvalBatch(native.ptr(z), native.ptr(g), native.ptr(pe), native.ptr(ph), C, ldc)
+    ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), phase=native.ptr(ph),
+                          num_chains=C, ldc=ldc)
     pot.evaluate(ev, native.stream_ptr())
     torch.cuda.synchronize()
     return pe[:C].cpu().numpy().astype(np.float64), g[:, :C].cpu().numpy().T.astype(np.float64)
@@ -125,3 +126,44 @@ def test_diag_normal(device):
         pr, gr = ref.pe_grad(Z[c])
         np.testing.assert_allclose(pe[c], pr, rtol=1e-5)
         np.testing.assert_allclose(g[c], gr, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("which", ["logreg", "eight_schools"])
+def test_compacted_active_list_is_bitwise_equal_to_dense(device, which):
+    """Potentials evaluated through the nuts_step's compacted chain list (arbitrary order)
+    give bitwise the dense results for the listed chains and leave the others untouched."""
+    import torch
+
+    from numpyro_amd import native
+    from numpyro_amd.potentials import EightSchools, LogisticRegression
+
+    rs = np.random.RandomState(9)
+    if which == "logreg":
+        X = rs.randn(4000, 55).astype(np.float32)
+        y = (rs.rand(4000) < 0.5).astype(np.float32)
+        pot, D = LogisticRegression(X, y), 55
+    else:
+        pot, D = EightSchools(8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y), 10
+    C = 300
+    Z = (0.1 * rs.randn(C, D)).astype(np.float32)
+    pe_dense, g_dense = _eval(pot, Z, device)
+    ldc = 320
+    pot.bind(C, ldc, device)
+    z = torch.zeros(D, ldc, device=device)
+    z[:, :C] = torch.from_numpy(Z.T.copy()).to(device)
+    g = torch.full((D, ldc), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    chosen = rs.permutation(C)[:77]
+    idx = torch.zeros(ldc, dtype=torch.int32, device=device)
+    idx[:77] = torch.from_numpy(chosen.astype(np.int32)).to(device)
+    cnt = torch.tensor([77], dtype=torch.int32, device=device)
+    ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), active_idx=native.ptr(idx),
+                          active_count=native.ptr(cnt), num_chains=C, ldc=ldc)
+    pot.evaluate(ev, native.stream_ptr())
+    torch.cuda.synchronize()
+    pe_l = pe[:C].cpu().numpy().astype(np.float64)
+    g_l = g[:, :C].cpu().numpy().T.astype(np.float64)
+    np.testing.assert_array_equal(pe_l[chosen], pe_dense[chosen])
+    np.testing.assert_array_equal(g_l[chosen], g_dense[chosen])
+    others = np.setdiff1d(np.arange(C), chosen)
+    assert np.all(np.isnan(pe_l[others]))
