@@ -1,0 +1,154 @@
+// Potentials of wide-latent models whose cost is O(D) per chain: stochastic volatility
+// (examples/stochastic_volatility.py:57-65, D = T + 2) and the centred funnel
+// (examples/funnel.py:44-46, D = dim).  Both are HBM-bound: a block owns 64 chains x 16
+// waves, wave w walks coordinates w, w+16, ... of its 64 chains (256-byte coalesced rows
+// of the chain-major layout) and the per-chain sums are reduced through LDS in a fixed
+// order.  Gradients are hand-derived.
+#include <math.h>
+
+#include "nmx_api_internal.h"
+#include "nmx_common.h"
+
+namespace {
+
+constexpr int WAVES = 16;
+
+// digamma for x > 0: recurrence up to x >= 6, then the asymptotic series.
+__device__ __forceinline__ float nmx_digammaf(float x) {
+  float acc = 0.0f;
+  while (x < 6.0f) {
+    acc -= 1.0f / x;
+    x += 1.0f;
+  }
+  const float inv = 1.0f / x;
+  const float inv2 = inv * inv;
+  const float series =
+      inv2 * (1.0f / 12.0f - inv2 * (1.0f / 120.0f - inv2 * (1.0f / 252.0f - inv2 * (1.0f / 240.0f - inv2 / 132.0f))));
+  return acc + logf(x) - 0.5f * inv - series;
+}
+
+template <int N>
+__device__ __forceinline__ void wave_block_sum(float (&v)[N], float* lds) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) lds[(i * WAVES + wv) * 64 + lane] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) s += lds[(i * WAVES + w) * 64 + lane];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+// z = (a = log nu, s[0..T-1], b = log sigma)
+__global__ __launch_bounds__(64 * WAVES) void k_sv(const float* __restrict__ ret, int T, nmx_eval_batch ev) {
+  __shared__ float lds[4 * WAVES * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int pos = blockIdx.x * 64 + lane;
+  const int c = nmx_eval_chain(ev, pos);
+  const bool act = c >= 0;
+  if (!__syncthreads_or(act)) return;
+  const int ldc = ev.ldc;
+  const float* z = ev.z;
+  float a = 0.f, b = 0.f;
+  if (act) {
+    a = z[c];
+    b = z[(size_t)(T + 1) * ldc + c];
+  }
+  const float nu = expf(a);
+  const float inv_sig2 = expf(-2.0f * b);
+  const float inv_nu = 1.0f / nu;
+  float sums[4] = {0.f, 0.f, 0.f, 0.f};  // sum d^2, sum log1p(q), sum q/(1+q), sum s
+  if (act) {
+    for (int t = wv; t < T; t += WAVES) {
+      const float s = z[(size_t)(1 + t) * ldc + c];
+      const float sp = t > 0 ? z[(size_t)t * ldc + c] : 0.0f;
+      const float sn = t + 1 < T ? z[(size_t)(2 + t) * ldc + c] : 0.0f;
+      const float d = s - sp;
+      const float dn = t + 1 < T ? sn - s : 0.0f;
+      const float r = ret[t];
+      const float q = r * r * expf(-2.0f * s) * inv_nu;
+      const float qq = q / (1.0f + q);
+      sums[0] += d * d;
+      sums[1] += log1pf(q);
+      sums[2] += qq;
+      sums[3] += s;
+      // dU/ds_t = -( -(d_t - d_{t+1})/sigma^2 + (nu+1) q/(1+q) - 1 )
+      ev.grad[(size_t)(1 + t) * ldc + c] = (d - dn) * inv_sig2 - (nu + 1.0f) * qq + 1.0f;
+    }
+  }
+  wave_block_sum<4>(sums, lds);
+  if (act && wv == 0) {
+    const float Tf = (float)T;
+    const float sig = expf(b);
+    const float lg = lgammaf(0.5f * nu) - lgammaf(0.5f * (nu + 1.0f));
+    // log p
+    float lp = 3.912023005428146f - 50.0f * sig + b;                        // Exponential(50) + log|J|
+    lp += -0.5f * sums[0] * inv_sig2 - Tf * b - Tf * 0.9189385332046727f;  // GaussianRandomWalk
+    lp += -2.302585092994046f - 0.1f * nu + a;                              // Exponential(0.1) + log|J|
+    lp += -0.5f * (nu + 1.0f) * sums[1] - sums[3]
+          - Tf * (0.5f * logf(nu) + 0.5723649429247001f + lg);              // StudentT(nu, 0, e^s)
+    ev.pe[c] = -lp;
+    const float dig = nmx_digammaf(0.5f * nu) - nmx_digammaf(0.5f * (nu + 1.0f));
+    const float ga = nu * (-0.1f - 0.5f * sums[1] + 0.5f * (nu + 1.0f) * inv_nu * sums[2]
+                           - 0.5f * Tf * inv_nu - 0.5f * Tf * dig) + 1.0f;
+    const float gb = -50.0f * sig + 1.0f + sums[0] * inv_sig2 - Tf;
+    ev.grad[c] = -ga;
+    ev.grad[(size_t)(T + 1) * ldc + c] = -gb;
+  }
+}
+
+// funnel, centred: z = (x[K], y); U = y^2/18 + log(3 sqrt(2 pi)) + sum_i [x_i^2 e^-y / 2 + y/2 + log(2 pi)/2]
+__global__ __launch_bounds__(64 * WAVES) void k_funnel(int D, nmx_eval_batch ev) {
+  __shared__ float lds[WAVES * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int pos = blockIdx.x * 64 + lane;
+  const int c = nmx_eval_chain(ev, pos);
+  const bool act = c >= 0;
+  if (!__syncthreads_or(act)) return;
+  const int ldc = ev.ldc;
+  const int K = D - 1;
+  const float y = act ? ev.z[(size_t)K * ldc + c] : 0.0f;
+  const float e = expf(-y);
+  float sx[1] = {0.0f};
+  if (act) {
+    for (int i = wv; i < K; i += WAVES) {
+      const size_t idx = (size_t)i * ldc + c;
+      const float x = ev.z[idx];
+      sx[0] += x * x;
+      ev.grad[idx] = x * e;
+    }
+  }
+  wave_block_sum<1>(sx, lds);
+  if (act && wv == 0) {
+    const float Kf = (float)K;
+    ev.pe[c] = y * y / 18.0f + 2.0175508218727822f + 0.5f * e * sx[0] + Kf * (0.5f * y + 0.9189385332046727f);
+    ev.grad[(size_t)K * ldc + c] = y / 9.0f + 0.5f * Kf - 0.5f * e * sx[0];
+  }
+}
+
+int check_ev(const nmx_eval_batch* ev) {
+  if (!ev || !ev->z || !ev->grad || !ev->pe) return nmx_fail(NMX_ERR_INVALID, "eval batch has NULL pointers");
+  if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
+    return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
+  return NMX_OK;
+}
+
+}  // namespace
+
+extern "C" int nmx_pe_stochastic_volatility(const float* returns, int T, const nmx_eval_batch* ev, void* stream) {
+  if (int st = check_ev(ev)) return st;
+  if (!returns || T <= 1) return nmx_fail(NMX_ERR_INVALID, "stochastic_volatility: need T > 1 returns");
+  hipLaunchKernelGGL(k_sv, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, (hipStream_t)stream, returns, T, *ev);
+  return nmx_check_launch("k_sv");
+}
+
+extern "C" int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* stream) {
+  if (int st = check_ev(ev)) return st;
+  if (dim < 2) return nmx_fail(NMX_ERR_INVALID, "funnel: dim must be >= 2");
+  hipLaunchKernelGGL(k_funnel, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, (hipStream_t)stream, dim, *ev);
+  return nmx_check_launch("k_funnel");
+}

@@ -144,6 +144,35 @@ class LogisticRegression(Potential):
         return 4.0 * self.N * self.dim * num_chains
 
 
+class StochasticVolatility(Potential):
+    """examples/stochastic_volatility.py:57-65 (sigma ~ Exp(50), s ~ GRW(sigma), nu ~ Exp(0.1),
+    r ~ StudentT(nu, 0, exp(s)))."""
+
+    def __init__(self, returns):
+        self.r_in = returns
+        self.T = int(np.asarray(returns.cpu() if torch.is_tensor(returns) else returns).shape[0])
+        self.dim = self.T + 2
+        self.sites = [("nu", (), POSITIVE), ("s", (self.T,), REAL), ("sigma", (), POSITIVE)]
+
+    def _bind(self, C, ldc, device):
+        self.r = _dev(self.r_in, device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_stochastic_volatility(ptr(self.r), self.T, ctypes.byref(ev), stream),
+              "nmx_pe_stochastic_volatility")
+
+
+class Funnel(Potential):
+    """examples/funnel.py:44-46, centred: y ~ N(0, 3), x ~ N(0, exp(y/2))^(dim-1)."""
+
+    def __init__(self, dim=10):
+        self.dim = int(dim)
+        self.sites = [("x", (self.dim - 1,), REAL), ("y", (), REAL)]
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_funnel(self.dim, ctypes.byref(ev), stream), "nmx_pe_funnel")
+
+
 # ------------------------------------------------------------------------------------------
 # Model functions (the reference's examples) -> fused potentials.
 # ------------------------------------------------------------------------------------------
@@ -175,5 +204,11 @@ eight_schools = FusedModel(
     "README.md:47-55 eight_schools(J, sigma, y)")
 
 diag_normal = FusedModel("diag_normal", lambda mu, sd: DiagNormal(mu, sd))
+
+stochastic_volatility = FusedModel(
+    "stochastic_volatility", lambda returns: StochasticVolatility(returns),
+    "examples/stochastic_volatility.py:57-65 model(returns)")
+
+funnel = FusedModel("funnel", lambda dim=10: Funnel(dim), "examples/funnel.py:44-46 model(dim)")
 
 LOG_2PI = math.log(2 * math.pi)

@@ -229,3 +229,23 @@ def test_resume_from_post_warmup_state(device):
     mcmc.run(4, *args)  # post_warmup_state still set -> same samples again
     np.testing.assert_array_equal(first, mcmc.get_samples()["mu"].cpu().numpy())
     assert int(mcmc.last_state.i[0]) == 150
+
+
+def test_stochastic_volatility_runs_and_is_sane(device):
+    """Config C4 shape (T=2517) at small chain count: finite draws, sigma and nu in range."""
+    r = datasets.sp500_synthetic()
+    mcmc = MCMC(NUTS(P.stochastic_volatility), num_warmup=100, num_samples=50, num_chains=64)
+    mcmc.run(0, r, extra_fields=("num_steps", "diverging"))
+    s = mcmc.get_samples()
+    assert s["s"].shape == (64 * 50, r.size)
+    assert torch.isfinite(s["s"]).all()
+    sig = s["sigma"].cpu().numpy()
+    assert 0.0 < np.median(sig) < 0.2
+    assert np.median(s["nu"].cpu().numpy()) > 1.0
+
+
+def test_funnel_diag_runs(device):
+    mcmc = MCMC(NUTS(P.funnel), num_warmup=200, num_samples=200, num_chains=128)
+    mcmc.run(0, 10, extra_fields=("diverging",))
+    y = mcmc.get_samples()["y"].cpu().numpy()
+    assert abs(y.mean()) < 1.5 and 1.5 < y.std() < 4.0  # y ~ N(0, 3) (centred funnel is hard)

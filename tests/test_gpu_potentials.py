@@ -167,3 +167,38 @@ def test_compacted_active_list_is_bitwise_equal_to_dense(device, which):
     np.testing.assert_array_equal(g_l[chosen], g_dense[chosen])
     others = np.setdiff1d(np.arange(C), chosen)
     assert np.all(np.isnan(pe_l[others]))
+
+
+def test_stochastic_volatility_matches_oracle(device):
+    """examples/stochastic_volatility.py model at the SP500 length (T = 2517, D = 2519).
+    U sums ~3T terms of magnitude up to ~10 with cancellation, so the fp32 tolerance is
+    absolute: |dU| <= 2e-2 (~ T * eps_f32 * 10 with margin)."""
+    from numpyro_amd.potentials import StochasticVolatility
+
+    r = datasets.sp500_synthetic()
+    rs = np.random.RandomState(0)
+    C = 70
+    Z = np.empty((C, r.size + 2), np.float32)
+    Z[:, 0] = rs.uniform(0.5, 3.5, C)        # log nu
+    Z[:, -1] = rs.uniform(-5.0, -2.0, C)     # log sigma
+    Z[:, 1:-1] = (np.log(np.abs(r)).mean() + np.cumsum(0.05 * rs.randn(C, r.size), axis=1)).astype(np.float32)
+    pe, g = _eval(StochasticVolatility(r), Z, device)
+    ref = OP.StochasticVolatility(r)
+    for c in range(C):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c], pr, rtol=0, atol=2e-2)
+        np.testing.assert_allclose(g[c], gr, rtol=2e-3, atol=2e-2 + 2e-4 * np.abs(gr).max())
+
+
+@pytest.mark.parametrize("dim", [10, 10000])
+def test_funnel_matches_oracle(device, dim):
+    from numpyro_amd.potentials import Funnel
+
+    rs = np.random.RandomState(dim)
+    Z = rs.uniform(-2, 2, (65, dim)).astype(np.float32)
+    pe, g = _eval(Funnel(dim), Z, device)
+    ref = OP.Funnel(dim)
+    for c in range(65):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c], pr, rtol=2e-5)
+        np.testing.assert_allclose(g[c], gr, rtol=1e-4, atol=1e-3 * max(1.0, np.abs(gr).max() * 1e-2))
