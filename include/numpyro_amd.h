@@ -106,7 +106,8 @@ typedef struct nmx_nuts_config {
   int32_t adapt_step_size;       /* hmc_util.py:518-707 flags */
   int32_t adapt_mass_matrix;
   int32_t regularize_mass_matrix;
-  int32_t dense_mass;            /* must be 0 (diag) in this version */
+  int32_t dense_mass;            /* must be 0: dense mass runs as identity mass on whitened
+                                    coordinates around the potential (nmx_gemm_chains) */
   int32_t sync_chains;           /* 1: reference vmap lockstep per transition */
   float target_accept_prob;
   float max_delta_energy;        /* hmc.py:188 */
@@ -204,6 +205,25 @@ int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, const nmx_ev
 /* Number of row splits the kernel uses for n_rows (depends on n_rows only, so results
  * do not depend on how many chains or GPUs share the work). */
 int nmx_logreg_num_splits(int64_t n_rows);
+
+/* ---- dense mass matrix (hmc_util.py:1203-1220 dense matvecs, hmc.py:103-108 momentum,
+ *      hmc_util.py:612-620 dense Welford finalize) ----
+ * With inverse mass M^-1 = T T^T, NUTS with dense mass on z is NUTS with identity mass on
+ * w, z = mu + T w (kinetic energy, U-turn dot products and momentum draws map exactly;
+ * with T = tril_inv^T the whitened momentum is the reference's `eps`).  Each leapfrog then
+ * costs z = mu + T w and g_w = T^T g_z, two chain-batched products:
+ *   Out[i][c] = sum_k At[k][i] * In[k][c] (+ bias[i])
+ * over every 64-chain tile holding a chain with phase[c] >= NMX_PH_LEAF (phase NULL: all).
+ * At = A^T row-major with leading dimension lda (multiple of 128, >= padded dim) and zero
+ * padding in rows/columns >= dim; In/Out are [dim][ldc] chain-major; f32 MFMA. */
+int nmx_dense_padded_dim(int dim);
+int nmx_gemm_chains(const float* At, int lda, int dim, const float* In, float* Out, const float* bias,
+                    int ldc, const int32_t* phase, int num_chains, void* stream);
+/* Multivariate normal, U = 0.5 (z-mu)^T P (z-mu), grad = P z - P mu (one nmx_gemm_chains
+ * with At = P^T, bias = -P mu) then the per-chain quadratic form: the dense-mass test
+ * targets of test/infer/test_mcmc.py:73-100 and :313-343. */
+int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const float* neg_prec_mu, int dim,
+               const nmx_eval_batch* ev, void* stream);
 
 /* ---- self tests (no reference counterpart; used by tests and smoke()) ---- */
 /* Philox4x32-10 on device: ctr_key is n x {c0,c1,c2,c3,k0,k1}, out is n x 4 words. */

@@ -1,0 +1,158 @@
+// Chain-batched dense transforms on f32 MFMA: Out[:, c] = A . In[:, c] (+ bias) for every
+// 64-chain tile that holds an evaluated chain.  Used by the dense-mass path: with
+// M^-1 = T T^T the reference's dense-mass NUTS (hmc_util.py:1203-1220 matvecs, hmc.py:103-108
+// momentum) is identity-mass NUTS on w with z = mu + T w, so each leapfrog costs the two
+// products z = T w and g_w = T^T g_z (4 D^2 FLOP per chain).
+//
+// The kernel takes At = A^T (row-major, padded to Dp x Dp with zeros, Dp = round_up(D, 128))
+// so that both LDS tiles are filled by coalesced row reads: As[k][i] = At[k][i] (by
+// global_load_lds) and Bs[k][c] = In[k][c] (register staged, rows >= D masked to zero).
+// Wave w computes rows [32w, 32w+32) x 64 chains with two 32x32 accumulators of
+// v_mfma_f32_32x32x2_f32; A operand lane l = As[2s + (l>>5)][32w + (l&31)], B operand
+// = Bs[2s + (l>>5)][(l&31) + 32b] -- both bank-conflict free without padding.
+#include "nmx_api_internal.h"
+#include "nmx_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TM = 128;  // output rows per workgroup
+constexpr int TN = 64;   // chains per workgroup
+constexpr int BK = 32;   // k per stage
+
+__global__ __launch_bounds__(256, 2) void k_gemm_chains(const float* __restrict__ At, int lda, int D,
+                                                        const float* __restrict__ In, float* __restrict__ Out,
+                                                        const float* __restrict__ bias, int ldc,
+                                                        const int32_t* __restrict__ phase, int C) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK * TM];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * TN];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int i0 = blockIdx.x * TM;
+  const int c0 = blockIdx.y * TN;
+  // tile has an evaluated chain?
+  {
+    const int c = c0 + lane;
+    const bool act = c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+    if (!__any(act)) return;  // same result in every wave
+  }
+  const int nk = (D + BK - 1) / BK;
+
+  auto load_a = [&](int kt, int buf) {
+    // BK rows x TM floats = 16 KiB = 16 wave-instructions of 1 KiB; 4 per wave
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int inst = w * 4 + q;             // 0..15
+      const int row = inst * 2 + (lane >> 5); // two 512-byte rows per instruction
+      const int col = (lane & 31) * 4;
+      const float* src = At + (size_t)(kt * BK + row) * lda + i0 + col;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(&As[buf][inst * 256]), 16, 0, 0);
+    }
+  };
+  auto load_b = [&](int kt, float4 (&reg)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = (q * 256 + tid);  // float4 index in the 32 x 64 tile
+      const int row = e >> 4;         // 16 float4 per row
+      const int col = (e & 15) * 4;
+      const int k = kt * BK + row;
+      const int c = c0 + col;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < D && c < ldc) v = *reinterpret_cast<const float4*>(In + (size_t)k * ldc + c);
+      reg[q] = v;
+    }
+  };
+  auto store_b = [&](int buf, const float4 (&reg)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) reinterpret_cast<float4*>(Bs[buf])[q * 256 + tid] = reg[q];
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.0f;
+    acc1[r] = 0.0f;
+  }
+  float4 breg[2];
+  load_a(0, 0);
+  load_b(0, breg);
+  store_b(0, breg);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_a(kt + 1, buf ^ 1);
+      load_b(kt + 1, breg);
+    }
+    const float* as = As[buf];
+    const float* bs = Bs[buf];
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      const int k = 2 * s + h;
+      const float a = as[k * TM + w * 32 + l31];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bs[k * TN + l31], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bs[k * TN + 32 + l31], acc1, 0, 0, 0);
+    }
+    if (more) store_b(buf ^ 1, breg);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = i0 + w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (i < D) {
+      const float bi = bias ? bias[i] : 0.0f;
+      const int ca = c0 + l31, cb = c0 + 32 + l31;
+      if (ca < ldc) Out[(size_t)i * ldc + ca] = acc0[r] + bi;
+      if (cb < ldc) Out[(size_t)i * ldc + cb] = acc1[r] + bi;
+    }
+  }
+}
+
+// pe[c] = 0.5 sum_d (z[d][c] - mu[d]) * g[d][c] for evaluated chains; 4 waves split d,
+// partials combined in fixed order.
+__global__ __launch_bounds__(256) void k_quad_pe(const float* __restrict__ mu, int D, nmx_eval_batch ev) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + lane);
+  float s = 0.0f;
+  if (c >= 0) {
+    for (int d = w; d < D; d += 4) {
+      const size_t idx = (size_t)d * ev.ldc + c;
+      s += (ev.z[idx] - mu[d]) * ev.grad[idx];
+    }
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c >= 0) ev.pe[c] = 0.5f * (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+}
+
+}  // namespace
+
+extern "C" int nmx_dense_padded_dim(int D) { return (D + TM - 1) / TM * TM; }
+
+extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In, float* Out, const float* bias,
+                               int ldc, const int32_t* phase, int num_chains, void* stream) {
+  if (!At || !In || !Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: NULL operand");
+  if (D <= 0 || ldc % 64 || num_chains <= 0 || num_chains > ldc)
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains: bad sizes (D=%d ldc=%d C=%d)", D, ldc, num_chains);
+  if (lda % TM || lda < nmx_dense_padded_dim(D))
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains: lda must be a multiple of %d >= padded D", TM);
+  if (In == Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: In and Out must not alias");
+  dim3 grid(lda / TM, ldc / TN);
+  hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, ldc,
+                     phase, num_chains);
+  return nmx_check_launch("k_gemm_chains");
+}
+
+extern "C" int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const float* neg_prec_mu, int dim,
+                          const nmx_eval_batch* ev, void* stream) {
+  if (!ev || !ev->z || !ev->grad || !ev->pe || !mu || !neg_prec_mu)
+    return nmx_fail(NMX_ERR_INVALID, "mvn: NULL operand");
+  if (int st = nmx_gemm_chains(prec_t, lda, dim, ev->z, ev->grad, neg_prec_mu, ev->ldc, ev->phase, ev->num_chains,
+                               stream))
+    return st;
+  hipLaunchKernelGGL(k_quad_pe, dim3(ev->ldc / 64), dim3(256), 0, (hipStream_t)stream, mu, dim, *ev);
+  return nmx_check_launch("k_quad_pe");
+}

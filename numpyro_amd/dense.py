@@ -1,0 +1,166 @@
+"""Dense mass matrix by whitening (hmc.py:92-110 momentum, hmc_util.py:1183-1220 kinetic
+energy, hmc_util.py:198-237 dense Welford finalize, hmc_util.py:488-515 initialisation).
+
+The reference's dense-mass NUTS draws r = mass_matrix_sqrt @ eps, moves z by
+dt * M^-1 r and tests U-turns with (M^-1 r) . r_sum.  With T = tril_inv^T (upper
+triangular, T T^T = M^-1 = cov) and the change of variables z = mu + T w, p_w = T^T r:
+
+* p_w = tril_inv @ mass_matrix_sqrt @ eps = eps          (identity-mass momentum)
+* 0.5 r^T M^-1 r = 0.5 |p_w|^2                           (kinetic energy)
+* (M^-1 r_a) . r_b = p_w,a . p_w,b                        (U-turn criterion)
+* the leapfrog on (z, r) with M^-1 is the leapfrog on (w, p_w) with identity mass
+  and U_w(w) = U(mu + T w), grad_w = T^T grad_z.
+
+So the device state machine runs unchanged with identity mass on w, and the model's
+potential is wrapped by two chain-batched MFMA products per leapfrog (`nmx_gemm_chains`):
+z = mu + T w before, g_w = T^T g_z after.  Results equal the reference's in exact
+arithmetic; in f32 they differ by rounding (the parity test follows the oracle's dense
+path at fixed step size).
+
+Adaptation is pooled across all chains of the job (an opt-in deviation, SURVEY.md §8a
+a18): at the end of every middle adaptation window the covariance of every chain's
+samples in that window (all ranks, reduced over RCCL) replaces M^-1 for every chain,
+regularised as in the reference with n = the pooled sample count.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import native
+from .native import EvalBatch, check, lib, ptr
+from .potentials import REAL, Potential
+
+
+class Whitening:
+    """z = mu + T w, T T^T = M^-1.  Holds the two padded At operands of nmx_gemm_chains."""
+
+    def __init__(self, dim: int, device):
+        self.D = int(dim)
+        self.device = torch.device(device)
+        self.lda = int(lib().nmx_dense_padded_dim(self.D))
+        self.fwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T^T
+        self.bwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T
+        self.mu = torch.zeros(self.D, dtype=torch.float32, device=self.device)
+        self.set(torch.eye(self.D, dtype=torch.float64, device=self.device), None)
+
+    def set(self, inverse_mass_matrix, mu=None):
+        """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
+        imm = torch.as_tensor(inverse_mass_matrix, dtype=torch.float64).to(self.device)
+        if imm.dim() == 1:
+            imm = torch.diag(imm)
+        if imm.shape != (self.D, self.D):
+            raise ValueError(f"inverse_mass_matrix must be [{self.D}, {self.D}]")
+        # tril_inv = swap(chol(cov[::-1, ::-1])[::-1, ::-1])  (hmc_util.py:228-231); T = tril_inv^T
+        T = torch.linalg.cholesky(imm.flip(0, 1)).flip(0, 1)
+        self.inverse_mass_matrix = imm
+        self.T = T
+        self.fwd_t[:self.D, :self.D] = T.t().to(torch.float32)
+        self.bwd_t[:self.D, :self.D] = T.to(torch.float32)
+        if mu is not None:
+            self.mu.copy_(torch.as_tensor(mu, dtype=torch.float32))
+
+    # reference-named views (HMCAdaptState fields)
+    def mass_matrix_sqrt_inv(self):
+        return self.T.t()  # tril_inv
+
+    def mass_matrix_sqrt(self):
+        eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
+        return torch.linalg.solve_triangular(self.T.t(), eye, upper=False)
+
+    def to_model(self, w, out, phase=None, num_chains=None, stream=0):
+        """out[:, c] = mu + T w[:, c] for [D, ldc] buffers."""
+        ldc = w.shape[-1]
+        check(lib().nmx_gemm_chains(ptr(self.fwd_t), self.lda, self.D, ptr(w), ptr(out), ptr(self.mu), ldc,
+                                    ptr(phase), int(num_chains or ldc), stream), "nmx_gemm_chains")
+
+    def grad_to_w(self, g, out, phase=None, num_chains=None, stream=0):
+        """out[:, c] = T^T g[:, c]."""
+        ldc = g.shape[-1]
+        check(lib().nmx_gemm_chains(ptr(self.bwd_t), self.lda, self.D, ptr(g), ptr(out), None, ldc,
+                                    ptr(phase), int(num_chains or ldc), stream), "nmx_gemm_chains")
+
+    def to_whitened(self, z):
+        """w = T^-1 (z - mu) for z [D, n] (host-side re-expression at window ends)."""
+        zz = z.to(torch.float64) - self.mu.to(torch.float64)[:, None]
+        return torch.linalg.solve_triangular(self.T, zz, upper=True).to(torch.float32)
+
+
+class WhitenedPotential(Potential):
+    """U_w(w) = U(mu + T w), grad_w = T^T grad U (see module docstring)."""
+
+    def __init__(self, base: Potential):
+        self.base = base
+        self.dim = base.dim
+        self.sites = [(n, s, REAL) for n, s, _ in base.sites]
+        self.whitening = None
+
+    def _bind(self, C, ldc, device):
+        self.base.bind(C, ldc, device)
+        if self.whitening is None or self.whitening.device != device:
+            self.whitening = Whitening(self.dim, device)
+        self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
+        self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
+        self._batches = {}
+
+    def _base_batch(self, ev):
+        key = (ev.active_idx, ev.active_count, ev.pe, ev.phase)
+        b = self._batches.get(key)
+        if b is None:
+            b = EvalBatch(z=ptr(self.zb), grad=ptr(self.gb), pe=ev.pe, phase=ev.phase, active_idx=ev.active_idx,
+                          active_count=ev.active_count, num_chains=ev.num_chains, ldc=ev.ldc)
+            self._batches[key] = b
+        return b
+
+    def evaluate(self, ev, stream):
+        wt = self.whitening
+        C, ldc = ev.num_chains, ev.ldc
+        check(lib().nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, self.dim, ev.z, ptr(self.zb), ptr(wt.mu), ldc,
+                                    ev.phase, C, stream), "nmx_gemm_chains")
+        self.base.evaluate(self._base_batch(ev), stream)
+        check(lib().nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, self.dim, ptr(self.gb), ev.grad, None, ldc,
+                                    ev.phase, C, stream), "nmx_gemm_chains")
+
+    def flops_per_eval(self, num_chains):
+        return 4.0 * self.dim * self.dim * num_chains
+
+
+class PooledCovariance:
+    """Sum / outer-product accumulators of model-space samples for one window (float64),
+    shifted by a reference point to avoid cancellation; reduced over ranks on finalize."""
+
+    def __init__(self, dim, device, shift):
+        self.D = dim
+        self.shift = shift.to(torch.float64).to(device)
+        self.n = 0
+        self.s1 = torch.zeros(dim, dtype=torch.float64, device=device)
+        self.s2 = torch.zeros(dim, dim, dtype=torch.float64, device=device)
+
+    def add(self, z):
+        """z: [D, m] samples (columns)."""
+        y = z.to(torch.float64) - self.shift[:, None]
+        self.n += y.shape[1]
+        self.s1 += y.sum(1)
+        self.s2 += y @ y.t()
+
+    def all_reduce(self):
+        dist = torch.distributed
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            n = torch.tensor([float(self.n)], dtype=torch.float64, device=self.s1.device)
+            for t in (n, self.s1, self.s2):
+                dist.all_reduce(t)
+            self.n = int(round(float(n.item())))
+
+    def finalize(self, regularize=True):
+        """(cov, mean) as welford_covariance.final_fn (hmc_util.py:212-226) over the pool."""
+        n = self.n
+        if n < 2:
+            raise RuntimeError("pooled dense adaptation needs at least 2 samples per window")
+        mean_y = self.s1 / n
+        cov = (self.s2 - n * torch.outer(mean_y, mean_y)) / (n - 1)
+        cov = 0.5 * (cov + cov.t())
+        if regularize:
+            cov = (n / (n + 5.0)) * cov + 1e-3 * (5.0 / (n + 5.0)) * torch.eye(self.D, dtype=cov.dtype,
+                                                                              device=cov.device)
+        return cov, mean_y + self.shift

@@ -70,8 +70,11 @@ class Engine:
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
-        if opts.dense_mass:
-            raise NotImplementedError("dense_mass=True is not supported by this engine build")
+        self.dense = bool(opts.dense_mass)
+        self.model_potential = potential
+        if self.dense:
+            from .dense import WhitenedPotential
+            potential = WhitenedPotential(potential)
         self.potential = potential
         self.C = int(num_chains)
         self.D = int(potential.dim)
@@ -138,7 +141,8 @@ class Engine:
         c.iter_end = int(iter_end)
         c.iter_capacity = self.iter_capacity
         c.adapt_step_size = int(bool(o.adapt_step_size))
-        c.adapt_mass_matrix = int(bool(o.adapt_mass_matrix))
+        # dense mass: identity on the device (whitened coordinates), pooled on the host side
+        c.adapt_mass_matrix = int(bool(o.adapt_mass_matrix) and not self.dense)
         c.regularize_mass_matrix = int(bool(o.regularize_mass_matrix))
         c.dense_mass = 0
         c.sync_chains = int(self.sync_chains)
@@ -170,7 +174,10 @@ class Engine:
         self._fill_cfg(0, 0, num_warmup, seed, 0, 1, 0)
         imm = self.opts.inverse_mass_matrix
         imm_t = None
-        if imm is not None:
+        if self.dense:
+            # chains are initialised in model coordinates (w = z), then re-expressed
+            self.potential.whitening.set(torch.eye(self.D, dtype=torch.float64), torch.zeros(self.D))
+        elif imm is not None:
             imm_t = torch.as_tensor(imm, dtype=torch.float32, device=self.device).reshape(-1)
             if imm_t.numel() != self.D:
                 raise ValueError("inverse_mass_matrix must be a diagonal of size D")
@@ -200,6 +207,61 @@ class Engine:
                 raise RuntimeError("Cannot find valid initial parameters. Please check your model "
                                    "again.")  # infer/util.py:795-797
         self.iteration = 0
+        if self.dense and imm is not None:
+            self._reexpress(imm, None, s)
+
+    # ------------------------------------------------------------------ dense mass
+    def _reexpress(self, inverse_mass_matrix, mu, s):
+        """Change the whitening of every chain (at an iteration boundary): z is kept,
+        w = T_new^-1 (z - mu_new), and U, grad_w are re-evaluated at the new w."""
+        wt = self.potential.whitening
+        z = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
+        wt.to_model(self.view("z"), z, stream=s)
+        wt.set(inverse_mass_matrix, mu)
+        w = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device)
+        w[:, :self.C] = wt.to_whitened(z[:, :self.C])
+        check(lib().nmx_nuts_init_from(ctypes.byref(self.cfg), ptr(self.arena), ptr(w), s))
+        self.potential.evaluate(self.eval_batch, s)
+        check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
+        bad = int(self.view("counters")[1].item())
+        if bad:
+            raise RuntimeError(f"{bad} chains have a non-finite potential after the mass-matrix update")
+
+    def _convert_slots(self, samples, slots, s):
+        """In place: whitened draws of collection slots -> model space -> constrained."""
+        if len(slots) == 0:
+            return
+        wt = self.potential.whitening
+        tmp = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
+        pos = self.model_potential.transform_codes().to(torch.bool)
+        for k in slots:
+            wt.to_model(samples[k], tmp, stream=s)
+            samples[k].copy_(tmp)
+            if bool(pos.any()):
+                samples[k][pos] = torch.exp(samples[k][pos])
+
+    def _dense_segments(self, it0, it1):
+        """Split [it0, it1) at the ends of middle adaptation windows; yields
+        (a, b, window_is_middle)."""
+        bounds = []
+        if self.opts.adapt_mass_matrix and self.num_warmup > 0:
+            sched = build_adaptation_schedule(self.num_warmup)
+            for i, (ws, we) in enumerate(sched):
+                if 0 < i < len(sched) - 1:
+                    bounds.append((ws, we + 1))
+        segs, a = [], it0
+        for ws, we1 in bounds:
+            if we1 <= a or ws >= it1:
+                continue
+            if ws > a:
+                segs.append((a, ws, False))
+                a = ws
+            b = min(we1, it1)
+            segs.append((a, b, b == we1 and a == ws))
+            a = b
+        if a < it1:
+            segs.append((a, it1, False))
+        return segs
 
     def run(self, num_iters: int, seed: int, collect_begin: int = 0, collection_size: int | None = None,
             thinning: int = 1, poll_every: int = 16, stream=None, max_launches: int | None = None):
@@ -215,12 +277,72 @@ class Engine:
         it0 = self.iteration
         if self.sync_chains and num_iters > self.iter_capacity:
             self._grow_finished(num_iters)
-        self._fill_cfg(it0, it0 + num_iters, self.num_warmup, seed, it0 + start_idx, thinning,
-                       collection_size)
         S = max(int(collection_size), 0)
         samples = torch.empty((max(S, 1), self.D, self.ldc), dtype=torch.float32, device=self.device)
         fields = torch.zeros((max(S, 1), len(native.COLLECT), self.ldc), dtype=torch.float32,
                              device=self.device)
+        cstart = it0 + start_idx
+        if not self.dense:
+            launches = self._run_segment(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
+                                         poll_every, s, max_launches)
+        else:
+            launches = self._run_dense(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
+                                       poll_every, s, max_launches)
+        self.iteration = it0 + num_iters
+        return samples[:S], fields[:S], launches
+
+    @staticmethod
+    def _slot_of(i, cstart, thinning, S):
+        """Collection slot whose final value transition i writes (util.py:330-346: slot
+        (i - start) // thinning, last write wins), or -1."""
+        off = i - cstart
+        if off < 0 or off % thinning != thinning - 1 or off // thinning >= S:
+            return -1
+        return off // thinning
+
+    def _slots_in(self, a, b, cstart, thinning, S):
+        """Collection slots completed by transitions [a, b)."""
+        return [k for k in (self._slot_of(i, cstart, thinning, S) for i in range(a, b)) if k >= 0]
+
+    def _run_dense(self, it0, it1, seed, cstart, thinning, S, samples, fields, poll_every, s, max_launches):
+        from .dense import PooledCovariance
+        budget = int(float(__import__("os").environ.get("NMX_DENSE_ADAPT_BYTES", 4 << 30)))
+        chunk = max(1, budget // (4 * self.D * self.ldc))
+        wt = self.potential.whitening
+        pos = self.model_potential.transform_codes().to(torch.bool)
+        launches = 0
+        for a, b, middle in self._dense_segments(it0, it1):
+            if not middle:
+                launches += self._run_segment(a, b, seed, cstart, thinning, S, samples, fields, poll_every, s,
+                                              max_launches)
+                self._convert_slots(samples, self._slots_in(a, b, cstart, thinning, S), s)
+                continue
+            pool = PooledCovariance(self.D, self.device, wt.mu)
+            zbuf = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
+            for ca in range(a, b, chunk):
+                cb = min(b, ca + chunk)
+                n = cb - ca
+                abuf = torch.empty((n, self.D, self.ldc), dtype=torch.float32, device=self.device)
+                afld = torch.zeros((n, len(native.COLLECT), self.ldc), dtype=torch.float32, device=self.device)
+                launches += self._run_segment(ca, cb, seed, ca, 1, n, abuf, afld, poll_every, s, max_launches)
+                for k in range(n):
+                    wt.to_model(abuf[k], zbuf, stream=s)
+                    pool.add(zbuf[:, :self.C])
+                    slot = self._slot_of(ca + k, cstart, thinning, S)
+                    if slot >= 0:
+                        samples[slot].copy_(zbuf)
+                        if bool(pos.any()):
+                            samples[slot][pos] = torch.exp(samples[slot][pos])
+                        fields[slot].copy_(afld[k])
+                del abuf, afld
+            pool.all_reduce()
+            cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
+            self._reexpress(cov, mean, s)
+        return launches
+
+    def _run_segment(self, a, b, seed, cstart, thinning, S, samples, fields, poll_every, s, max_launches):
+        """Transitions [a, b) of every chain; collection slots per (cstart, thinning, S)."""
+        self._fill_cfg(a, b, self.num_warmup, seed, cstart, thinning, S)
         cfgp = ctypes.byref(self.cfg)
         arena = ptr(self.arena)
         tr = self.potential.transform_codes()
@@ -254,8 +376,7 @@ class Engine:
             pending = True
             if max_launches is not None and launches >= max_launches:
                 raise RuntimeError(f"chains did not finish within {max_launches} leapfrog launches")
-        self.iteration = it0 + num_iters
-        return samples[:S], fields[:S], launches
+        return launches
 
     def _grow_finished(self, n):
         # re-layout the arena with a larger sync-counter table, keeping all chain state
@@ -267,6 +388,38 @@ class Engine:
         del old
 
     # ------------------------------------------------------------------ accessors
+    def model_state(self):
+        """(z [C, D], grad U(z) [C, D]) in model coordinates (un-whitened for dense mass)."""
+        z, g = self.chain_state("z"), self.chain_state("zgrad")
+        if not self.dense:
+            return z.clone(), g.clone()
+        wt = self.potential.whitening
+        zb = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
+        wt.to_model(self.view("z"), zb, stream=stream_ptr())
+        # g_w = T^T g_z  ->  g_z = T^-T g_w
+        gz = torch.linalg.solve_triangular(wt.T.t(), g.t().to(torch.float64), upper=False)
+        return zb[:, :self.C].t().clone(), gz.t().to(torch.float32)
+
+    def mass_state(self):
+        """(inverse_mass_matrix, mass_matrix_sqrt, mass_matrix_sqrt_inv) as HMCAdaptState holds
+        them: per-chain diagonals [C, D], or the pooled dense matrices [D, D]."""
+        if self.dense:
+            wt = self.potential.whitening
+            return (wt.inverse_mass_matrix.to(torch.float32).clone(), wt.mass_matrix_sqrt().to(torch.float32),
+                    wt.mass_matrix_sqrt_inv().to(torch.float32).clone())
+        ms = self.chain_state("mass_sqrt").clone()
+        return self.chain_state("inv_mass").clone(), ms, 1.0 / ms
+
+    def whitening_state(self):
+        if not self.dense:
+            return None
+        wt = self.potential.whitening
+        return (wt.inverse_mass_matrix.clone(), wt.mu.clone())
+
+    def set_whitening_state(self, st):
+        if st is not None:
+            self.potential.whitening.set(st[0], st[1])
+
     def chain_state(self, name):
         """Per-chain view without padding: scalars [C], vectors [C, D]."""
         v = self.view(name)

@@ -88,8 +88,9 @@ class HMC(MCMCKernel):
             raise NotImplementedError("custom kinetic_fn: the engine uses the Euclidean kinetic energy")
         if find_heuristic_step_size:
             raise NotImplementedError("find_heuristic_step_size=True is not supported yet")
-        if dense_mass not in (False, [], None):
-            raise NotImplementedError("dense_mass is not supported by this engine build (diagonal only)")
+        if isinstance(dense_mass, (list, tuple)) and len(dense_mass) > 0:
+            raise NotImplementedError("structured dense_mass (list of site groups) is not supported; "
+                                      "use dense_mass=True for a full dense mass matrix")
         if model is not None and not isinstance(model, FusedModel):
             raise TypeError("`model` must be a fused model (numpyro_amd.potentials.*); arbitrary "
                             "Python models cannot run on the device engine")
@@ -132,7 +133,7 @@ class HMC(MCMCKernel):
         md = tuple(md) if isinstance(md, (tuple, list)) else (int(md), int(md))
         return SamplerOptions(
             algo=self._algo, step_size=self._step_size, adapt_step_size=self._adapt_step_size,
-            adapt_mass_matrix=self._adapt_mass_matrix, dense_mass=False,
+            adapt_mass_matrix=self._adapt_mass_matrix, dense_mass=bool(self._dense_mass),
             target_accept_prob=self._target_accept_prob, max_tree_depth=md,
             trajectory_length=self._trajectory_length, num_steps=self._num_steps,
             regularize_mass_matrix=self._regularize_mass_matrix,

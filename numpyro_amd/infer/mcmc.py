@@ -97,12 +97,12 @@ class MCMC:
 
     def _snapshot(self, eng, seed):
         C = eng.C
-        z_flat = eng.chain_state("z").clone()
+        z_flat, zgrad = eng.model_state()
         pot = eng.potential
         z = pot.unflatten(z_flat) if len(pot.sites) else z_flat
+        imm, msq, msq_inv = eng.mass_state()
         adapt = HMCAdaptState(
-            eng.chain_state("step_size").clone(), eng.chain_state("inv_mass").clone(),
-            eng.chain_state("mass_sqrt").clone(), 1.0 / eng.chain_state("mass_sqrt").clone(),
+            eng.chain_state("step_size").clone(), imm, msq, msq_inv,
             (eng.chain_state("da_xt").clone(), eng.chain_state("da_xavg").clone(),
              eng.chain_state("da_gavg").clone(), eng.chain_state("da_t").clone(),
              eng.chain_state("da_prox").clone()),
@@ -110,12 +110,13 @@ class MCMC:
              eng.chain_state("wf_n").clone()),
             eng.chain_state("window_idx").clone(), seed)
         st = HMCState(
-            eng.chain_state("iter").clone(), z, eng.chain_state("zgrad").clone(),
+            eng.chain_state("iter").clone(), z, zgrad,
             eng.chain_state("pe").clone(), eng.chain_state("energy").clone(), None,
             eng.opts.trajectory_length, eng.chain_state("last_nsteps").clone(),
             eng.chain_state("last_acc").clone(), eng.chain_state("mean_acc").clone(),
             eng.chain_state("last_div").clone().bool(), adapt, seed)
         st._arena = eng.arena.clone()
+        st._whitening = eng.whitening_state()
         st._iteration = eng.iteration
         st._num_warmup = eng.num_warmup
         st._engine = eng
@@ -126,6 +127,7 @@ class MCMC:
         if getattr(state, "_engine", None) is not eng:
             raise ValueError("post_warmup_state belongs to a different model/data binding")
         eng.arena.copy_(state._arena)
+        eng.set_whitening_state(state._whitening)
         eng.iteration = state._iteration
         eng.num_warmup = state._num_warmup
 

@@ -173,6 +173,37 @@ class Funnel(Potential):
         check(lib().nmx_pe_funnel(self.dim, ctypes.byref(ev), stream), "nmx_pe_funnel")
 
 
+class MultivariateNormal(Potential):
+    """U = 0.5 (z - mu)^T P (z - mu): the MultivariateNormal targets of
+    test/infer/test_mcmc.py:73-100 (`test_correlated_mvn`) and :313-343 (`test_dense_mass`).
+    grad = P z - P mu is one chain-batched MFMA product (nmx_gemm_chains)."""
+
+    def __init__(self, loc=None, covariance_matrix=None, precision_matrix=None, name="x"):
+        if (covariance_matrix is None) == (precision_matrix is None):
+            raise ValueError("give exactly one of covariance_matrix / precision_matrix")
+        if precision_matrix is None:
+            prec = np.linalg.inv(np.asarray(covariance_matrix, np.float64))
+        else:
+            prec = np.asarray(precision_matrix, np.float64)
+        self.prec_h = 0.5 * (prec + prec.T)
+        self.dim = self.prec_h.shape[0]
+        self.mu_h = (np.zeros(self.dim) if loc is None else np.asarray(loc, np.float64)).reshape(-1)
+        self.sites = [(name, (self.dim,), REAL)]
+
+    def _bind(self, C, ldc, device):
+        lda = lib().nmx_dense_padded_dim(self.dim)
+        pt = np.zeros((lda, lda), np.float32)
+        pt[:self.dim, :self.dim] = self.prec_h.T
+        self.lda = lda
+        self.prec_t = _dev(pt, device)
+        self.mu = _dev(self.mu_h, device)
+        self.neg_prec_mu = _dev(-(self.prec_h @ self.mu_h), device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_mvn(ptr(self.prec_t), self.lda, ptr(self.mu), ptr(self.neg_prec_mu), self.dim,
+                               ctypes.byref(ev), stream), "nmx_pe_mvn")
+
+
 # ------------------------------------------------------------------------------------------
 # Model functions (the reference's examples) -> fused potentials.
 # ------------------------------------------------------------------------------------------
@@ -210,5 +241,11 @@ stochastic_volatility = FusedModel(
     "examples/stochastic_volatility.py:57-65 model(returns)")
 
 funnel = FusedModel("funnel", lambda dim=10: Funnel(dim), "examples/funnel.py:44-46 model(dim)")
+
+multivariate_normal = FusedModel(
+    "multivariate_normal",
+    lambda loc=None, covariance_matrix=None, precision_matrix=None: MultivariateNormal(
+        loc, covariance_matrix, precision_matrix),
+    "x ~ MultivariateNormal(loc, covariance_matrix | precision_matrix)")
 
 LOG_2PI = math.log(2 * math.pi)

@@ -224,3 +224,19 @@ class IsoNormal:
         z = np.asarray(z, np.float64)
         d = (z - self.mu) / self.sd
         return self.dtype(0.5 * (d * d).sum()), (d / self.sd).astype(self.dtype)
+
+
+class MVN:
+    """Unnormalized N(mu, P^-1): U = 0.5 (z-mu)^T P (z-mu) (test/infer/test_mcmc.py:73-100,
+    :313-343 targets)."""
+
+    def __init__(self, prec, mu=None, dtype=np.float64):
+        self.prec = np.asarray(prec, np.float64)
+        self.dim = self.prec.shape[0]
+        self.mu = np.zeros(self.dim) if mu is None else np.asarray(mu, np.float64)
+        self.dtype = dtype
+
+    def pe_grad(self, z):
+        d = np.asarray(z, np.float64) - self.mu
+        g = self.prec @ d
+        return self.dtype(0.5 * d @ g), g.astype(self.dtype)

@@ -1,0 +1,246 @@
+"""Dense mass matrix (whitening around the potential, numpyro_amd/dense.py) on the GPU.
+
+* `nmx_gemm_chains` (f32 MFMA) vs a float64 product; inactive chain tiles untouched.
+  Tolerance |out - ref| <= 2e-6 * (|A| |In|) + 1e-6 (k-ordered f32 fma chain).
+* MVN and whitened potentials vs the float64 oracle.
+* Fixed dense mass, fixed step: device paths vs the oracle's dense-mass sample kernel
+  (oracle/hmc_ref.py, which follows hmc.py:92-110 / hmc_util.py:1183-1220 directly, i.e.
+  without whitening): >= 90% of chains take the identical discrete path, draws to 1e-3.
+* Pooled adaptation: ports of test/infer/test_mcmc.py:75-100 (test_correlated_mvn) and
+  :313-343 (test_dense_mass) with the reference's tolerances, at fewer iterations (the
+  pooled estimate uses every chain's window samples).
+"""
+import numpy as np
+import pytest
+import torch
+
+from numpyro_amd import native
+from numpyro_amd import potentials as P
+from numpyro_amd.dense import Whitening, WhitenedPotential
+from numpyro_amd.infer import HMC, MCMC, NUTS
+from oracle import hmc_ref as H
+from oracle import philox
+from oracle import potentials as OP
+
+pytestmark = pytest.mark.gpu
+
+
+def _eval(pot, Z, device, phase=None, bind=True):
+    C, D = Z.shape
+    ldc = (C + 63) // 64 * 64
+    if bind:
+        pot.bind(C, ldc, device)
+    z = torch.zeros(D, ldc, device=device)
+    z[:, :C] = torch.from_numpy(Z.T.astype(np.float32)).to(device)
+    g = torch.full((D, ldc), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    ph = torch.zeros(ldc, dtype=torch.int32, device=device)
+    ph[:C] = native.PH_LEAF if phase is None else torch.from_numpy(phase.astype(np.int32)).to(device)
+    ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), phase=native.ptr(ph),
+                          num_chains=C, ldc=ldc)
+    pot.evaluate(ev, native.stream_ptr())
+    torch.cuda.synchronize()
+    return pe[:C].cpu().numpy().astype(np.float64), g[:, :C].cpu().numpy().T.astype(np.float64)
+
+
+@pytest.mark.parametrize("D,C", [(3, 64), (55, 200), (130, 130), (300, 256), (1000, 70)])
+def test_gemm_chains_matches_fp64(device, D, C):
+    rs = np.random.RandomState(D)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    ldc = (C + 63) // 64 * 64
+    A = rs.randn(D, D)
+    At = np.zeros((lda, lda), np.float32)
+    At[:D, :D] = A.T
+    In = rs.randn(D, ldc).astype(np.float32)
+    bias = rs.randn(D).astype(np.float32)
+    phase = np.full(ldc, native.PH_DONE, np.int32)
+    act = rs.rand(C) < 0.5
+    act[64:128] = False  # a fully idle tile (when present) must be left untouched
+    phase[:C][act] = native.PH_LEAF
+    dAt, dIn, db = (torch.from_numpy(x).to(device) for x in (At, In, bias))
+    dph = torch.from_numpy(phase).to(device)
+    out = torch.full((D, ldc), float("nan"), device=device)
+    native.check(lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(out), native.ptr(db),
+                                     ldc, native.ptr(dph), C, native.stream_ptr()))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().astype(np.float64)
+    A32 = At[:D, :D].T.astype(np.float64)
+    ref = A32 @ In.astype(np.float64) + bias[:, None]
+    bound = 2e-6 * (np.abs(A32) @ np.abs(In.astype(np.float64)) + np.abs(bias)[:, None]) + 1e-6
+    for t in range(ldc // 64):
+        cols = slice(64 * t, 64 * t + 64)
+        tile_active = bool((phase[cols] >= native.PH_LEAF).any())
+        if tile_active:
+            assert np.all(np.abs(o[:, cols] - ref[:, cols]) <= bound[:, cols])
+        else:
+            assert np.all(np.isnan(o[:, cols]))
+    # error paths
+    assert lib.nmx_gemm_chains(native.ptr(dAt), lda - 1, D, native.ptr(dIn), native.ptr(out), None, ldc, None, C,
+                               None) != 0
+    assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(dIn), None, ldc, None, C,
+                               None) != 0
+
+
+def _corr_cov(D, seed=0):
+    rs = np.random.RandomState(seed)
+    a = np.tril(0.5 * np.fliplr(np.eye(D)) + 0.1 * np.exp(rs.randn(D, D)))
+    return a @ a.T
+
+
+@pytest.mark.parametrize("D", [2, 5, 40, 200])
+def test_mvn_potential_matches_oracle(device, D):
+    cov = _corr_cov(D, D) + 0.1 * np.eye(D)
+    mu = np.linspace(-1, 1, D)
+    rs = np.random.RandomState(1)
+    Z = rs.randn(100, D).astype(np.float32)
+    pe, g = _eval(P.MultivariateNormal(mu, cov), Z, device)
+    ref = OP.MVN(np.linalg.inv(cov), mu)
+    prec = np.linalg.inv(cov)
+    for c in range(Z.shape[0]):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        scale = np.abs(prec) @ (np.abs(Z[c]) + np.abs(mu))
+        assert np.all(np.abs(g[c] - gr) <= 1e-5 * scale + 1e-5)
+        np.testing.assert_allclose(pe[c], pr, rtol=1e-4, atol=1e-4)
+
+
+def test_whitened_potential_matches_oracle(device):
+    D = 12
+    cov = _corr_cov(D, 3) + 0.05 * np.eye(D)
+    target = P.MultivariateNormal(np.ones(D), cov)
+    wp = WhitenedPotential(target)
+    C = 96
+    wp.bind(C, 128, device)
+    imm = _corr_cov(D, 4) + 0.2 * np.eye(D)
+    mu = np.linspace(0, 2, D)
+    wp.whitening.set(torch.from_numpy(imm), torch.from_numpy(mu))
+    rs = np.random.RandomState(2)
+    W = rs.randn(C, D).astype(np.float32)
+    pe, gw = _eval(wp, W, device, bind=False)
+    T = wp.whitening.T.cpu().numpy()
+    np.testing.assert_allclose(T @ T.T, imm, rtol=1e-10, atol=1e-12)
+    assert np.allclose(np.tril(T, -1), 0)  # T = tril_inv^T is upper triangular
+    ref = OP.MVN(np.linalg.inv(cov), np.ones(D))
+    for c in range(C):
+        z = mu + T @ W[c].astype(np.float64)
+        pr, gz = ref.pe_grad(z)
+        np.testing.assert_allclose(pe[c], pr, rtol=2e-4, atol=2e-4)
+        np.testing.assert_allclose(gw[c], T.T @ gz, rtol=1e-3, atol=1e-3)
+
+
+def _oracle_chain(pe_grad, dim, seed, chain, num_iters, algo, **kw):
+    o = H.NUTSOracle(lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)
+                                     for v in pe_grad(z)), dim, 0, algo=algo, **kw)
+    s = o.init(philox.init_uniform(seed, chain, 0, dim), seed, chain)
+    out = []
+    for _ in range(num_iters):
+        s = o.sample(s)
+        out.append(s)
+    return out
+
+
+@pytest.mark.parametrize("algo", ["NUTS", "HMC"])
+@pytest.mark.parametrize("model", ["logreg", "mvn"])
+def test_dense_fixed_mass_matches_oracle(device, algo, model):
+    seed, C, T, D = 31, 64, 3, 6
+    rs = np.random.RandomState(7)
+    imm = _corr_cov(D, 11) * 0.05 + 0.01 * np.eye(D)
+    if model == "logreg":
+        X = rs.randn(400, D).astype(np.float32)
+        beta = rs.randn(D) * 0.3
+        y = (rs.rand(400) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
+        args, fm = (X, y), P.logistic_regression
+        ref = OP.LogisticRegression(X, y, dtype=np.float32)
+        site, step = "coefs", 0.1
+    else:
+        cov = _corr_cov(D, 12) + 0.1 * np.eye(D)
+        args, fm = (None, cov), P.multivariate_normal
+        ref = OP.MVN(np.linalg.inv(cov))
+        site, step = "x", 0.2
+    kw = dict(step_size=step, adapt_step_size=False, adapt_mass_matrix=False, dense_mass=True,
+              inverse_mass_matrix=imm)
+    if algo == "HMC":
+        kw["trajectory_length"] = 10 * step
+    kcls = NUTS if algo == "NUTS" else HMC
+    mcmc = MCMC(kcls(fm, **kw), num_warmup=0, num_samples=T, num_chains=C, progress_bar=False)
+    mcmc.run(seed, *args, extra_fields=("num_steps",))
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
+    zs = mcmc.get_samples(True)[site].cpu().numpy()
+    okw = dict(step_size=step, adapt_step_size=False, adapt_mass_matrix=False, dense_mass=True,
+               inverse_mass_matrix=imm.astype(np.float32))
+    if algo == "HMC":
+        okw["trajectory_length"] = 10 * step
+    match = 0
+    for c in range(C):
+        states = _oracle_chain(ref.pe_grad, D, seed, c, T, algo, **okw)
+        ns = np.array([s.num_steps for s in states])
+        if np.array_equal(ns, ns_dev[c]):
+            match += 1
+            np.testing.assert_allclose(zs[c], np.stack([s.z for s in states]), rtol=1e-3, atol=1e-3)
+    assert match >= int(0.9 * C), f"only {match}/{C} chains reproduced the oracle path"
+    # HMCAdaptState carries the reference's matrices
+    st = mcmc.last_state.adapt_state
+    np.testing.assert_allclose(st.inverse_mass_matrix.cpu().numpy(), imm, rtol=1e-5, atol=1e-7)
+    msq = st.mass_matrix_sqrt.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(msq @ msq.T, np.linalg.inv(imm), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("kernel_cls", [NUTS, HMC])
+@pytest.mark.parametrize("rho", [-0.7, 0.8])
+def test_dense_mass_pooled_adaptation(device, kernel_cls, rho):
+    """test/infer/test_mcmc.py:313-343 (2-d MVN, trajectory_length=2): the adapted dense
+    mass recovers the target covariance (rtol 0.10) and the sample moments match."""
+    true_cov = np.array([[10.0, rho], [rho, 0.1]])
+    kernel = kernel_cls(P.multivariate_normal, trajectory_length=2.0, dense_mass=True)
+    mcmc = MCMC(kernel, num_warmup=1000, num_samples=1000, num_chains=64, progress_bar=False)
+    mcmc.run(0, None, true_cov)
+    msq = mcmc.last_state.adapt_state.mass_matrix_sqrt.cpu().numpy().astype(np.float64)
+    est_cov = np.linalg.inv(msq @ msq.T)
+    np.testing.assert_allclose(est_cov, true_cov, rtol=0.10)
+    x = mcmc.get_samples()["x"].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(x[:, 0].mean(), 0.0, atol=0.50)
+    np.testing.assert_allclose(x[:, 1].mean(), 0.0, atol=0.05)
+    np.testing.assert_allclose((x[:, 0] * x[:, 1]).mean(), rho, atol=0.20)
+    np.testing.assert_allclose(x.var(0), [10.0, 0.1], rtol=0.20)
+
+
+@pytest.mark.parametrize("regularize", [True, False])
+def test_correlated_mvn(device, regularize):
+    """test/infer/test_mcmc.py:75-100 (D = 5, dense NUTS from zeros)."""
+    D = 5
+    true_cov = _corr_cov(D, 0)
+    kernel = NUTS(P.multivariate_normal, dense_mass=True, regularize_mass_matrix=regularize)
+    C = 64
+    mcmc = MCMC(kernel, num_warmup=1000, num_samples=1000, num_chains=C, progress_bar=False)
+    mcmc.run(0, None, None, np.linalg.inv(true_cov), init_params=torch.zeros(C, D))
+    x = mcmc.get_samples()["x"].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(x.mean(), 0.0, atol=0.02)
+    assert np.sum(np.abs(np.cov(x.T) - true_cov)) / D ** 2 < 0.02
+
+
+def test_dense_resume_from_post_warmup_state(device):
+    cov = _corr_cov(4, 5) + 0.1 * np.eye(4)
+    mcmc = MCMC(NUTS(P.multivariate_normal, dense_mass=True), num_warmup=200, num_samples=50, num_chains=64)
+    mcmc.warmup(1, None, cov)
+    st = mcmc.post_warmup_state
+    mcmc.run(2, None, cov)
+    a = mcmc.get_samples()["x"].cpu().numpy()
+    mcmc.post_warmup_state = st
+    mcmc.run(2, None, cov)
+    np.testing.assert_array_equal(a, mcmc.get_samples()["x"].cpu().numpy())
+    assert st.adapt_state.inverse_mass_matrix.shape == (4, 4)
+
+
+def test_whitening_roundtrip(device):
+    D = 9
+    wt = Whitening(D, device)
+    imm = _corr_cov(D, 9) + 0.3 * np.eye(D)
+    wt.set(torch.from_numpy(imm), torch.arange(D, dtype=torch.float32))
+    z = torch.randn(D, 64, device=device)
+    w = wt.to_whitened(z)
+    wpad = torch.zeros(D, 64, device=device)
+    wpad[:] = w
+    zb = torch.empty(D, 64, device=device)
+    wt.to_model(wpad, zb, stream=native.stream_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(zb.cpu().numpy(), z.cpu().numpy(), rtol=1e-4, atol=1e-4)

@@ -172,7 +172,8 @@ def test_compacted_active_list_is_bitwise_equal_to_dense(device, which):
 def test_stochastic_volatility_matches_oracle(device):
     """examples/stochastic_volatility.py model at the SP500 length (T = 2517, D = 2519).
     U sums ~3T terms of magnitude up to ~10 with cancellation, so the fp32 tolerance is
-    absolute: |dU| <= 2e-2 (~ T * eps_f32 * 10 with margin)."""
+    absolute: |dU| <= 2e-2 (~ T * eps_f32 * 10 with margin) plus 1e-6 |U| (the f32 ulp of
+    the result itself when sigma is small and U reaches ~3e5)."""
     from numpyro_amd.potentials import StochasticVolatility
 
     r = datasets.sp500_synthetic()
@@ -186,7 +187,7 @@ def test_stochastic_volatility_matches_oracle(device):
     ref = OP.StochasticVolatility(r)
     for c in range(C):
         pr, gr = ref.pe_grad(Z[c].astype(np.float64))
-        np.testing.assert_allclose(pe[c], pr, rtol=0, atol=2e-2)
+        np.testing.assert_allclose(pe[c], pr, rtol=1e-6, atol=2e-2)  # fp32 ulp of |U| ~ 3e5 is 0.03
         np.testing.assert_allclose(g[c], gr, rtol=2e-3, atol=2e-2 + 2e-4 * np.abs(gr).max())
 
 
