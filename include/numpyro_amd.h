@@ -66,6 +66,8 @@ enum nmx_field {
   NMX_F_PHASE = 0, NMX_F_ITER, NMX_F_DEPTH, NMX_F_SUB_N, NMX_F_DIR, NMX_F_TREE_N,
   NMX_F_WINDOW_IDX, NMX_F_DA_T, NMX_F_WF_N, NMX_F_TURNING, NMX_F_TREE_DIV, NMX_F_SUB_DIV,
   NMX_F_HMC_K, NMX_F_HMC_N, NMX_F_LAST_NSTEPS, NMX_F_LAST_DIV, NMX_F_MAXDEPTH_CUR,
+  /* decisions of the last step, consumed by the wide (D-split) vector kernels */
+  NMX_F_ACTION, NMX_F_SLOT, NMX_F_ACT_WFN,
   /* per-chain float scalars */
   NMX_F_STEP_SIZE, NMX_F_E0, NMX_F_PE, NMX_F_ENERGY, NMX_F_TREE_W, NMX_F_TREE_ACC,
   NMX_F_SUB_W, NMX_F_SUB_ACC, NMX_F_PE_SUB, NMX_F_E_SUB, NMX_F_DA_XT, NMX_F_DA_XAVG,
@@ -83,6 +85,9 @@ enum nmx_field {
   NMX_F_COUNTERS,
   /* sync_chains: int32[iter_capacity] #chains that finished transition iter_begin + i */
   NMX_F_FINISHED,
+  /* wide (D-split) step only: per-slice partial dot products f32 [NS][2*MAXD+2][ldc] and
+   * momentum kinetic-energy partials [NS][ldc]; NS = nmx_nuts_num_slices(dim) (0: fused) */
+  NMX_F_PART, NMX_F_PART0,
   NMX_NUM_FIELDS
 };
 
@@ -125,6 +130,9 @@ typedef struct nmx_nuts_config {
                                     active list [parity] (and clears [parity ^ 1]) */
 } nmx_nuts_config;
 
+/* D-slices of the wide step (0 when dim is small enough for the fused one-kernel step).
+ * Depends on dim only, so results never depend on how chains are sharded. */
+int nmx_nuts_num_slices(int dim);
 /* Arena size/offsets for (C, D, max_depth_alloc, iter_capacity). */
 size_t nmx_nuts_arena_bytes(int num_chains, int dim, int max_depth_alloc, int iter_capacity);
 int nmx_nuts_field_info(int num_chains, int dim, int max_depth_alloc, int iter_capacity,

@@ -22,24 +22,30 @@
 namespace {
 
 constexpr int MAXD = NMX_MAX_TREE_DEPTH;
-constexpr int NRED = 2 * MAXD + 2;
+constexpr int NPART = 2 * MAXD + 3;  // KE, checkpoint dots (2 per level), whole-tree dots
+constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide schedule)
+
+inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
+inline int num_slices(int D) { return D >= WIDE_MIN_D ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
 constexpr size_t ALIGN = 256;
 
 inline size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 inline int ldc_of(int C) { return (C + 63) / 64 * 64; }
 
-constexpr int NUM_INT_SCALARS = NMX_F_MAXDEPTH_CUR - NMX_F_PHASE + 1;
+constexpr int NUM_INT_SCALARS = NMX_F_ACT_WFN - NMX_F_PHASE + 1;
 constexpr int NUM_FLOAT_SCALARS = NMX_F_PE_EVAL - NMX_F_STEP_SIZE + 1;
 constexpr int NUM_VECTORS = NMX_F_G_EVAL - NMX_F_Z + 1;
 
 size_t field_bytes(int field, int ldc, int D, int MD, int iter_cap) {
-  if (field <= NMX_F_MAXDEPTH_CUR) return (size_t)ldc * 4;
+  if (field <= NMX_F_ACT_WFN) return (size_t)ldc * 4;
   if (field <= NMX_F_PE_EVAL) return (size_t)ldc * 4;
   if (field <= NMX_F_G_EVAL) return (size_t)D * ldc * 4;
   if (field <= NMX_F_CKPT_RSUM) return (size_t)MD * D * ldc * 4;
   if (field == NMX_F_ACTIVE_IDX) return (size_t)2 * ldc * 4;
   if (field == NMX_F_COUNTERS) return 16 * 4;
   if (field == NMX_F_FINISHED) return (size_t)(iter_cap > 0 ? iter_cap : 1) * 4;
+  if (field == NMX_F_PART) return (size_t)num_slices(D) * NPART * ldc * 4;
+  if (field == NMX_F_PART0) return (size_t)num_slices(D) * ldc * 4;
   return 0;
 }
 
@@ -59,6 +65,8 @@ struct Arena {
   int32_t* active_idx;
   int32_t* counters;
   int32_t* finished;
+  float* part;
+  float* part0;
 };
 
 #define AI(f) a.is[(f) - NMX_F_PHASE]
@@ -68,7 +76,7 @@ struct Arena {
 Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
   Arena a;
   char* b = (char*)base;
-  for (int f = NMX_F_PHASE; f <= NMX_F_MAXDEPTH_CUR; ++f)
+  for (int f = NMX_F_PHASE; f <= NMX_F_ACT_WFN; ++f)
     a.is[f - NMX_F_PHASE] = (int32_t*)(b + field_offset(f, ldc, D, MD, iter_cap));
   for (int f = NMX_F_STEP_SIZE; f <= NMX_F_PE_EVAL; ++f)
     a.fs[f - NMX_F_STEP_SIZE] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
@@ -79,6 +87,8 @@ Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
   a.active_idx = (int32_t*)(b + field_offset(NMX_F_ACTIVE_IDX, ldc, D, MD, iter_cap));
   a.counters = (int32_t*)(b + field_offset(NMX_F_COUNTERS, ldc, D, MD, iter_cap));
   a.finished = (int32_t*)(b + field_offset(NMX_F_FINISHED, ldc, D, MD, iter_cap));
+  a.part = (float*)(b + field_offset(NMX_F_PART, ldc, D, MD, iter_cap));
+  a.part0 = (float*)(b + field_offset(NMX_F_PART0, ldc, D, MD, iter_cap));
   return a;
 }
 
@@ -115,12 +125,18 @@ __device__ __forceinline__ float transform_value(int8_t code, float z) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The step kernel.
+// The step.
 //
-// Per-chain scalar state is loaded into registers by every wave of the block before the
-// first barrier, updated identically by all waves (decisions only depend on block-reduced
-// sums and the chain's own registers) and written back by wave 0 only, so no wave can
-// observe another wave's partial update.  Vector work is split by coordinate across waves.
+// Per-chain scalar state is loaded into registers before the first barrier, updated
+// identically by all waves of a block (decisions only depend on block-reduced sums and
+// the chain's own registers) and written back by wave 0 only, so no wave can observe
+// another wave's partial update.  Vector work is split by coordinate.
+//
+// The scalar logic (leaf_phase / tree_phase) is shared by two schedules of the same step:
+//  * fused: one kernel, block = 64 chains x TPC waves owning all D coordinates (small D);
+//  * wide (D >= WIDE_MIN_D): V1 (leapfrog end + partial dots per D-slice) -> S (fixed-order
+//    reduction + scalar logic, one block per 64 chains) -> V2 (apply the decisions per
+//    D-slice), so the grid is chain-groups x D-slices and fills the GPU at any C.
 // ---------------------------------------------------------------------------------------
 struct ChainScalars {
   int phase, it, depth, sub_n, dir, tree_n, widx, da_t, wf_n, turning, tree_div, sub_div;
@@ -203,30 +219,34 @@ __device__ __forceinline__ void store_scalars(const Arena& a, int c, const Chain
   AF(NMX_F_STEP_EFF)[c] = s.step_eff;
 }
 
-template <int TPC>
-__global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
-  __shared__ float lds[TPC > 1 ? NRED * TPC * 64 : 1];
-  const nmx_nuts_config& cfg = A.cfg;
-  const Arena& a = A.a;
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  const int ldc = cfg.ldc;
-  const int D = cfg.dim;
-  const bool valid = c < cfg.num_chains;
-  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
-  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
-  const uint64_t seed = cfg.seed;
+// Decisions of one step for one chain.
+struct Act {
+  bool leaf, take_leaf, done_sub, take_biased, hmc_accept, iter_done, wf_update, finalize;
+  bool start_iter, prep_leaf, fin_done, fin_wait, div_new;
+  int dirR, new_dir, k, j, imin, imax, slot, fin_t, wfn;
+  float pe_eval, E_new, acc_new, w_new;
+};
 
-  // active list [parity ^ 1] was consumed by the previous potential launch; clear it for
-  // the next step (which appends to it).  List [parity] was cleared by the previous step.
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+enum : int {
+  ACT_TAKE_LEAF = 1 << 0, ACT_DONE_SUB = 1 << 1, ACT_TAKE_BIASED = 1 << 2, ACT_HMC_ACCEPT = 1 << 3,
+  ACT_ITER_DONE = 1 << 4, ACT_WF_UPDATE = 1 << 5, ACT_FINALIZE = 1 << 6, ACT_START = 1 << 7,
+  ACT_PREP = 1 << 8, ACT_DIRR = 1 << 9, ACT_NEWDIR = 1 << 10, ACT_KE0_PENDING = 1 << 11,
+};
 
-  ChainScalars S;
+__device__ __forceinline__ int pack_act(const Act& A) {
+  return (A.take_leaf ? ACT_TAKE_LEAF : 0) | (A.done_sub ? ACT_DONE_SUB : 0) |
+         (A.take_biased ? ACT_TAKE_BIASED : 0) | (A.hmc_accept ? ACT_HMC_ACCEPT : 0) |
+         (A.iter_done ? ACT_ITER_DONE : 0) | (A.wf_update ? ACT_WF_UPDATE : 0) |
+         (A.finalize ? ACT_FINALIZE : 0) | (A.start_iter ? ACT_START : 0) | (A.prep_leaf ? ACT_PREP : 0) |
+         (A.dirR ? ACT_DIRR : 0) | (A.new_dir ? ACT_NEWDIR : 0) | (A.start_iter ? ACT_KE0_PENDING : 0);
+}
+
+// Resolve WAIT (sync_chains) and set up the step's inputs.
+__device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid,
+                                          ChainScalars& S, Act& A) {
   if (valid) load_scalars(a, c, S);
   else S.phase = NMX_PH_DONE;
-  const int ph_in = S.phase;
-  int ph = ph_in;
+  int ph = S.phase;
   if (ph == NMX_PH_WAIT) {
     const int slot_w = S.it - 1 - cfg.iter_begin;
     const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
@@ -234,206 +254,129 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
                         : cfg.num_chains;
     if (fin >= cfg.num_chains) ph = NMX_PH_START;
   }
+  A = Act{};
+  A.leaf = ph == NMX_PH_LEAF;
+  A.start_iter = ph == NMX_PH_START;
+  A.dirR = A.leaf ? S.dir : 0;
+  A.new_dir = A.dirR;
+  A.pe_eval = A.leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
+  A.slot = -1;
+  A.imin = 1;
+  A.imax = 0;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  A.k = (A.leaf && is_nuts) ? S.sub_n : 0;
+  A.j = (A.leaf && is_nuts) ? S.depth : 0;
+  if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);  // :1036
+  return ph;
+}
 
-  float* const INVM = AV(NMX_F_INV_MASS);
-  const bool leaf = ph == NMX_PH_LEAF;
-  const int dirR = leaf ? S.dir : 0;
-  const float seff = valid ? S.step_eff : 0.0f;
-  float* ZF = dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
-  float* RF = dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
-  float* GF = dirR ? AV(NMX_F_GR) : AV(NMX_F_GL);
-  float* const ZE = AV(NMX_F_Z_EVAL);
-  float* const GE = AV(NMX_F_G_EVAL);
-  const float pe_eval = leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
-
-  // ---------------- L1: finish the pending leapfrog (hmc_util.py:306-308) + kinetic energy
-  float red[NRED];
-#pragma unroll
-  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
-  {
-    const float es = dirR ? seff : -seff;
-    const float half = 0.5f * es;
-    if (leaf) {
-      for (int d = wv; d < D; d += TPC) {
-        const size_t idx = (size_t)d * ldc + c;
-        const float g = GE[idx];
-        const float r = RF[idx] - half * g;
-        RF[idx] = r;
-        ZF[idx] = ZE[idx];
-        GF[idx] = g;
-        red[0] += (INVM[idx] * r) * r;
-      }
-    }
+// Leaf scalars (_build_basetree, hmc_util.py:851-894) and the NUTS leaf bookkeeping of
+// _iterative_build_subtree (:999-1061) that only needs the kinetic energy.
+__device__ __forceinline__ void leaf_phase(const nmx_nuts_config& cfg, ChainScalars& S, Act& A, float ke,
+                                           uint64_t seed, uint32_t gch) {
+  if (!A.leaf) return;
+  A.E_new = A.pe_eval + ke;
+  float dE = A.E_new - S.E0;
+  if (isnan(dE)) dE = INFINITY;
+  A.w_new = -dE;
+  A.div_new = dE > cfg.max_delta_energy;
+  A.acc_new = fminf(expf(-dE), 1.0f);
+  if (cfg.algo != NMX_ALGO_NUTS) return;
+  const int k = A.k, j = A.j;
+  if (k == 0) {  // new_tree = new_leaf (:1019-1021)
+    A.take_leaf = true;
+    S.sub_w = A.w_new;
+    S.sub_acc = A.acc_new;
+  } else {  // _combine_tree(..., biased_transition=False) (:767-848, :749-753)
+    const float p = nmx_sigmoid(A.w_new - S.sub_w);
+    const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_LEAF, j, k).x);
+    A.take_leaf = u < p;
+    S.sub_w = nmx_logaddexp(S.sub_w, A.w_new);
+    S.sub_acc = S.sub_acc + A.acc_new;
   }
-  block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
-
-  // leaf scalars (_build_basetree, hmc_util.py:851-894)
-  float E_new = 0.f, dE = 0.f, w_new = 0.f, acc_new = 0.f;
-  bool div_new = false;
-  if (leaf) {
-    const float ke = 0.5f * red[0];
-    E_new = pe_eval + ke;
-    dE = E_new - S.E0;
-    if (isnan(dE)) dE = INFINITY;
-    w_new = -dE;
-    div_new = dE > cfg.max_delta_energy;
-    acc_new = fminf(expf(-dE), 1.0f);
+  S.sub_div = A.div_new;
+  S.sub_n = k + 1;
+  if (A.take_leaf) {
+    S.pe_sub = A.pe_eval;
+    S.e_sub = A.E_new;
   }
+}
 
-  bool prep_leaf = false;     // continue integrating from the same frontier
-  bool new_doubling = false;  // pick a new direction, then prep_leaf
-  bool iter_done = false;     // transition finished
+// Everything after the U-turn dots: subtree end / tree combine, HMC accept, transition end
+// (adaptation scalars, mean accept prob, collection slot + fields), next transition or
+// doubling.  turn(i, side) = reduced checkpoint dot, tree(side) = reduced tree dot.
+template <class TurnF, class TreeF>
+__device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScalars& S, Act& A, TurnF turn,
+                                           TreeF tree, uint64_t seed, uint32_t gch, float* fields, int c,
+                                           bool writer) {
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const int ldc = cfg.ldc;
   float it_accept = 0.f;
   int it_nsteps = 0;
   bool it_div = false;
-
-  // ---------------- NUTS leaf bookkeeping (_iterative_build_subtree body, hmc_util.py:999-1061)
-  const int k = (leaf && is_nuts) ? S.sub_n : 0;
-  const int j = (leaf && is_nuts) ? S.depth : 0;
-  bool take_leaf = false;
-  int imin = 1, imax = 0;
-  if (leaf && is_nuts) {
-    if (k == 0) {  // new_tree = new_leaf (:1019-1021)
-      take_leaf = true;
-      S.sub_w = w_new;
-      S.sub_acc = acc_new;
-    } else {  // _combine_tree(..., biased_transition=False) (:767-848, :749-753)
-      const float p = nmx_sigmoid(w_new - S.sub_w);
-      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_LEAF, j, k).x);
-      take_leaf = u < p;
-      S.sub_w = nmx_logaddexp(S.sub_w, w_new);
-      S.sub_acc = S.sub_acc + acc_new;
-    }
-    S.sub_div = div_new;
-    S.sub_n = k + 1;
-    if (take_leaf) {
-      S.pe_sub = pe_eval;
-      S.e_sub = E_new;
-    }
-    nmx_leaf_idx_to_ckpt_idxs(k, imin, imax);  // :1036
-  }
-
-  // ---------------- L2: subtree r_sum, proposal copy, checkpoints, turning partial dots
-#pragma unroll
-  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
-  if (leaf && is_nuts) {
-    float* const RS = AV(NMX_F_RSUM_SUB);
-    float* const RST = AV(NMX_F_RSUM);
-    float* const ZS = AV(NMX_F_ZSUB);
-    float* const GS = AV(NMX_F_GSUB);
-    float* const RL = AV(NMX_F_RL);
-    float* const RR = AV(NMX_F_RR);
-    const bool even = (k & 1) == 0;
-    const size_t ck_stride = (size_t)D * ldc;
-    for (int d = wv; d < D; d += TPC) {
-      const size_t idx = (size_t)d * ldc + c;
-      const float r = RF[idx];
-      const float im = INVM[idx];
-      const float rs = (k == 0) ? r : RS[idx] + r;
-      RS[idx] = rs;
-      if (take_leaf) {
-        ZS[idx] = ZF[idx];
-        GS[idx] = GF[idx];
-      }
-      if (even) {  // checkpoint update (:1040-1047)
-        a.ckr[imax * ck_stride + idx] = r;
-        a.ckrs[imax * ck_stride + idx] = rs;
-      }
-      // _is_iterative_turning (:961-981): all checkpoints in [imin, imax]; the reference
-      // stops at the first turning one, the OR below is the same predicate.
-#pragma unroll
-      for (int i = 0; i < MAXD; ++i) {
-        if (i >= imin && i <= imax) {
-          const float rl = a.ckr[i * ck_stride + idx];
-          const float rsub = (rs - a.ckrs[i * ck_stride + idx]) + rl;
-          const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
-          red[2 * i] += (im * rl) * rss;
-          red[2 * i + 1] += (im * r) * rss;
-        }
-      }
-      // tentative whole-tree turning check with the tree's outer momenta (:795-799)
-      const float rst = RST[idx] + rs;
-      const float rlv = dirR ? RL[idx] : r;
-      const float rrv = dirR ? r : RR[idx];
-      const float rss2 = rst - (rlv + rrv) / 2.0f;
-      red[2 * MAXD] += (im * rlv) * rss2;
-      red[2 * MAXD + 1] += (im * rrv) * rss2;
-    }
-  }
-  block_sum<TPC, NRED>(red, lds);
-
-  bool done_sub = false, take_biased = false;
-  if (leaf && is_nuts) {
+  bool new_doubling = false;
+  if (A.leaf && is_nuts) {
     bool turning_sub = false;
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
-      if (i >= imin && i <= imax) turning_sub |= (red[2 * i] <= 0.0f) | (red[2 * i + 1] <= 0.0f);
-    done_sub = (S.sub_n >= (1 << j)) || turning_sub || div_new;  // loop exit (:992-997)
-    if (done_sub) {
+      if (i >= A.imin && i <= A.imax) turning_sub |= (turn(i, 0) <= 0.0f) | (turn(i, 1) <= 0.0f);
+    A.done_sub = (S.sub_n >= (1 << A.j)) || turning_sub || A.div_new;  // loop exit (:992-997)
+    if (A.done_sub) {
       // _double_tree -> _combine_tree(..., biased_transition=True) (:936-938, :756-764)
-      const bool turning_tree =
-          turning_sub || (red[2 * MAXD] <= 0.0f) || (red[2 * MAXD + 1] <= 0.0f);
+      const bool turning_tree = turning_sub || (tree(0) <= 0.0f) || (tree(1) <= 0.0f);
       float pb = expf(S.sub_w - S.tree_w);
       pb = isnan(pb) ? pb : fminf(pb, 1.0f);  // jnp.clip keeps NaN
-      if (turning_sub || div_new) pb = 0.0f;
-      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_BIASED, j, 0).x);
-      take_biased = u < pb;
-      if (take_biased) {
+      if (turning_sub || A.div_new) pb = 0.0f;
+      const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_BIASED, A.j, 0).x);
+      A.take_biased = u < pb;
+      if (A.take_biased) {
         S.pe = S.pe_sub;
         S.energy = S.e_sub;
       }
-      S.depth = j + 1;
+      S.depth = A.j + 1;
       S.tree_w = nmx_logaddexp(S.tree_w, S.sub_w);
-      S.tree_div = div_new;
+      S.tree_div = A.div_new;
       S.tree_acc = S.tree_acc + S.sub_acc;
       S.tree_n = S.tree_n + S.sub_n;
       S.turning = turning_tree;
       // build_tree loop condition (:1153-1157)
-      if (S.depth >= S.maxdepth || turning_tree || div_new) {
-        iter_done = true;
+      if (S.depth >= S.maxdepth || turning_tree || A.div_new) {
+        A.iter_done = true;
         it_accept = S.tree_acc / (float)S.tree_n;  // _nuts_next :441
         it_nsteps = S.tree_n;
-        it_div = div_new;
+        it_div = A.div_new;
       } else {
         new_doubling = true;
       }
     } else {
-      prep_leaf = true;
+      A.prep_leaf = true;
     }
   }
-
-  // ---------------- HMC leaf bookkeeping (_hmc_next, hmc.py:364-414)
-  bool hmc_accept = false;
-  if (leaf && !is_nuts) {
+  // HMC leaf bookkeeping (_hmc_next, hmc.py:364-414)
+  if (A.leaf && !is_nuts) {
     S.hmc_k = S.hmc_k + 1;
     if (S.hmc_k < S.hmc_n) {
-      prep_leaf = true;
+      A.prep_leaf = true;
     } else {
       const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_ACCEPT, 0, 0).x);
-      hmc_accept = u < acc_new;
-      if (hmc_accept) {
-        S.pe = pe_eval;
-        S.energy = E_new;
+      A.hmc_accept = u < A.acc_new;
+      if (A.hmc_accept) {
+        S.pe = A.pe_eval;
+        S.energy = A.E_new;
       } else {
         S.energy = S.E0;
       }
-      iter_done = true;
-      it_accept = acc_new;
+      A.iter_done = true;
+      it_accept = A.acc_new;
       it_nsteps = S.hmc_n;
-      it_div = div_new;
+      it_div = A.div_new;
     }
   }
-
-  // ---------------- transition end: adaptation scalars (warmup_adapter update_fn,
-  // hmc_util.py:637-705), mean accept prob (hmc.py:509-513), collection slot.
-  bool wf_update = false, finalize = false;
-  int slot = -1;
-  bool start_iter = ph == NMX_PH_START;
-  bool fin_done = false, fin_wait = false;
-  int fin_t = 0;
-  if (iter_done) {
+  // transition end: warmup_adapter update_fn (hmc_util.py:637-705), mean accept prob
+  // (hmc.py:509-513), collection slot.
+  if (A.iter_done) {
     const int t = S.it;
-    fin_t = t;
+    A.fin_t = t;
     if (t < cfg.num_warmup) {
       float new_step = S.step;
       if (cfg.adapt_step_size) {  // dual_averaging update_fn (:103-126)
@@ -449,12 +392,12 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       }
       const int widx = S.widx;
       const bool middle = (0 < widx) && (widx < cfg.num_windows - 1);
-      wf_update = cfg.adapt_mass_matrix && middle;
-      if (wf_update) S.wf_n = S.wf_n + 1;
+      A.wf_update = cfg.adapt_mass_matrix && middle;
+      if (A.wf_update) S.wf_n = S.wf_n + 1;
       const bool at_end = t == cfg.window_end[widx];
       S.widx = widx + (at_end ? 1 : 0);
-      finalize = at_end && middle;  // _update_at_window_end (:596-635)
-      if (finalize && cfg.adapt_step_size) {
+      A.finalize = at_end && middle && cfg.adapt_mass_matrix;  // _update_at_window_end (:596-635)
+      if (at_end && middle && cfg.adapt_step_size) {
         S.da_prox = logf(10.0f) + logf(new_step);
         S.da_xt = 0.0f;
         S.da_xavg = 0.0f;
@@ -463,6 +406,8 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       }
       S.step = new_step;
     }
+    A.wfn = S.wf_n;
+    if (A.finalize) S.wf_n = 0;
     const int itr = t + 1;
     const int nn = t < cfg.num_warmup ? itr : itr - cfg.num_warmup;
     S.mean_acc = S.mean_acc + (it_accept - S.mean_acc) / (float)nn;
@@ -475,11 +420,11 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       const int off = t - cfg.collect_start;
       if (off % cfg.collect_thinning == cfg.collect_thinning - 1) {
         const int s = off / cfg.collect_thinning;
-        if (s < cfg.collection_size) slot = s;
+        if (s < cfg.collection_size) A.slot = s;
       }
     }
-    if (slot >= 0 && wv == 0) {
-      float* F = A.fields + (size_t)slot * NMX_NUM_COLLECT * ldc;
+    if (A.slot >= 0 && writer) {
+      float* F = fields + (size_t)A.slot * NMX_NUM_COLLECT * ldc;
       F[NMX_C_POTENTIAL_ENERGY * ldc + c] = S.pe;
       F[NMX_C_ENERGY * ldc + c] = S.energy;
       F[NMX_C_ACCEPT_PROB * ldc + c] = it_accept;
@@ -491,78 +436,21 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
     }
     if (itr >= cfg.iter_end) {
       S.phase = NMX_PH_DONE;
-      fin_done = true;
+      A.fin_done = true;
     } else if (cfg.sync_chains) {
       S.phase = NMX_PH_WAIT;
-      fin_wait = true;
+      A.fin_wait = true;
     } else {
-      start_iter = true;
+      A.start_iter = true;
     }
   }
-
-  // ---------------- L3/L4: tree r_sum + biased proposal copy; HMC accept copy;
-  //                  Welford update / window finalize; sample collection.
-  const bool l3 = done_sub || hmc_accept || iter_done;
-  if (l3) {
-    float* const ZP = AV(NMX_F_Z);
-    float* const GP = AV(NMX_F_ZGRAD);
-    float* const RST = AV(NMX_F_RSUM);
-    float* const RS = AV(NMX_F_RSUM_SUB);
-    float* const ZS = AV(NMX_F_ZSUB);
-    float* const GS = AV(NMX_F_GSUB);
-    float* const WM = AV(NMX_F_WF_MEAN);
-    float* const W2 = AV(NMX_F_WF_M2);
-    float* const MS = AV(NMX_F_MASS_SQRT);
-    float* const samp = slot >= 0 ? A.samples + (size_t)slot * D * ldc : nullptr;
-    const int wf_n = S.wf_n;
-    const float wfn = (float)wf_n;
-    for (int d = wv; d < D; d += TPC) {
-      const size_t idx = (size_t)d * ldc + c;
-      if (done_sub) RST[idx] = RST[idx] + RS[idx];
-      if (take_biased) {
-        ZP[idx] = ZS[idx];
-        GP[idx] = GS[idx];
-      }
-      if (hmc_accept) {
-        ZP[idx] = AV(NMX_F_ZR)[idx];
-        GP[idx] = AV(NMX_F_GR)[idx];
-      }
-      if (iter_done) {
-        const float z = ZP[idx];
-        if (wf_update) {  // welford_covariance update_fn, diagonal (:172-196)
-          const float mean = WM[idx];
-          const float delta_pre = z - mean;
-          const float mean_new = mean + delta_pre / wfn;
-          const float delta_post = z - mean_new;
-          WM[idx] = mean_new;
-          W2[idx] = W2[idx] + delta_pre * delta_post;
-        }
-        if (finalize && cfg.adapt_mass_matrix) {  // final_fn (:198-237)
-          float cov = W2[idx] / (float)(wf_n - 1);
-          if (cfg.regularize_mass_matrix) {
-            const float scaled = ((float)wf_n / (float)(wf_n + 5)) * cov;
-            const float shrink = 1e-3f * (5.0f / (float)(wf_n + 5));
-            cov = scaled + shrink;
-          }
-          INVM[idx] = cov;
-          MS[idx] = 1.0f / sqrtf(cov);
-          WM[idx] = 0.0f;
-          W2[idx] = 0.0f;
-        }
-        if (samp) samp[idx] = transform_value(A.transform[d], z);
-      }
-    }
-  }
-  if (finalize && cfg.adapt_mass_matrix) S.wf_n = 0;
-
-  // ---------------- new transition: momentum, tree init (sample_kernel hmc.py:471-481,
-  // build_tree :1127-1151), first direction; new doubling direction (:1160-1162).
-  int new_dir = dirR;
-  if (start_iter) {
+  // new transition: tree init (sample_kernel hmc.py:471-481, build_tree :1127-1151), first
+  // direction; new doubling direction (:1160-1162).
+  if (A.start_iter) {
     if (is_nuts) {
       S.step_eff = S.step;
       S.maxdepth = S.it < cfg.num_warmup ? cfg.max_tree_depth_warmup : cfg.max_tree_depth;  // hmc.py:488-490
-      new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, 0, 0).x) < 0.5f;
+      A.new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, 0, 0).x) < 0.5f;
     } else {
       int n;
       if (cfg.num_steps > 0) n = cfg.num_steps;
@@ -571,7 +459,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
       S.step_eff = cfg.trajectory_length > 0.0f ? cfg.trajectory_length / (float)n : S.step;
       S.hmc_n = n;
       S.hmc_k = 0;
-      new_dir = 1;
+      A.new_dir = 1;
     }
     S.depth = 0;
     S.sub_n = 0;
@@ -580,105 +468,434 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs A) {
     S.tree_div = 0;
     S.tree_w = 0.0f;
     S.tree_acc = 0.0f;
-    S.dir = new_dir;
+    S.dir = A.new_dir;
     S.phase = NMX_PH_LEAF;
   } else if (new_doubling) {
-    new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, S.depth, 0).x) < 0.5f;
-    S.dir = new_dir;
+    A.new_dir = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_DIRECTION, S.depth, 0).x) < 0.5f;
+    S.dir = A.new_dir;
     S.sub_n = 0;
-    prep_leaf = true;
+    A.prep_leaf = true;
   }
+  if (A.prep_leaf) S.phase = NMX_PH_LEAF;
+}
 
-  // ---------------- L5: momentum draw + tree init; L6: half momentum step and the next
-  // position z_eval (velocity_verlet update_fn first half, hmc_util.py:297-301).
-#pragma unroll
-  for (int i = 0; i < NRED; ++i) red[i] = 0.0f;
-  const float step_eff = S.step_eff;
-  if (start_iter || prep_leaf) {
-    float* const ZFn = new_dir ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
-    float* const RFn = new_dir ? AV(NMX_F_RR) : AV(NMX_F_RL);
-    float* const GFn = new_dir ? AV(NMX_F_GR) : AV(NMX_F_GL);
-    float* const ZO = new_dir ? AV(NMX_F_ZL) : AV(NMX_F_ZR);
-    float* const RO = new_dir ? AV(NMX_F_RL) : AV(NMX_F_RR);
-    float* const GO = new_dir ? AV(NMX_F_GL) : AV(NMX_F_GR);
-    const float es = new_dir ? step_eff : -step_eff;
-    const float half = 0.5f * es;
-    if (start_iter) {
-      float* const ZP = AV(NMX_F_Z);
-      float* const GP = AV(NMX_F_ZGRAD);
-      float* const MS = AV(NMX_F_MASS_SQRT);
-      float* const RST = AV(NMX_F_RSUM);
-      const uint32_t it = (uint32_t)S.it;
-      // blocks of 4 coordinates share one Philox call (momentum_generator hmc.py:92-110)
-      for (int blk = wv; 4 * blk < D; blk += TPC) {
-        const nmx_u4 x = nmx_rng(seed, gch, it, NMX_EV_MOMENTUM, blk, 0);
-        float n[4];
-        nmx_box_muller(x.x, x.y, n[0], n[1]);
-        nmx_box_muller(x.z, x.w, n[2], n[3]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int d = 4 * blk + q;
-          if (d < D) {
-            const size_t idx = (size_t)d * ldc + c;
-            const float r = MS[idx] * n[q];
-            const float z = ZP[idx];
-            const float g = GP[idx];
-            const float im = INVM[idx];
-            red[0] += (im * r) * r;
-            RST[idx] = r;
-            ZO[idx] = z;
-            GO[idx] = g;
-            RO[idx] = r;
-            ZFn[idx] = z;
-            GFn[idx] = g;
-            const float rh = r - half * g;
-            RFn[idx] = rh;
-            ZE[idx] = z + es * (im * rh);
-          }
-        }
-      }
-    } else {
-      for (int d = wv; d < D; d += TPC) {
-        const size_t idx = (size_t)d * ldc + c;
-        const float rh = RFn[idx] - half * GFn[idx];
-        RFn[idx] = rh;
-        ZE[idx] = ZFn[idx] + es * (INVM[idx] * rh);
-      }
-      S.phase = NMX_PH_LEAF;
-    }
-  }
-  block_sum<TPC, 1>(*reinterpret_cast<float(*)[1]>(red), lds);
-  if (start_iter) {
-    S.E0 = S.pe + 0.5f * red[0];  // build_tree :1130
-    S.energy = S.E0;              // proposal energy of the initial tree (:1137)
-  }
-
-  if (wv == 0 && valid) {
-    if (S.phase != ph_in || leaf || start_iter || iter_done) store_scalars(a, c, S);
-    if (fin_done) atomicAdd(&a.counters[0], 1);
-    if (fin_wait) {
-      const int fs = fin_t - cfg.iter_begin;
+// End of step, wave 0: write scalars back, DONE / sync counters, compacted list.
+__device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid, int ph_in,
+                                         const ChainScalars& S, const Act& A) {
+  if (valid) {
+    if (S.phase != ph_in || A.leaf || A.start_iter || A.iter_done) store_scalars(a, c, S);
+    if (A.fin_done) atomicAdd(&a.counters[0], 1);
+    if (A.fin_wait) {
+      const int fs = A.fin_t - cfg.iter_begin;
       if (fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
     }
   }
-  // ---------------- compacted list of chains whose next leaf is pending: the potential
-  // kernels then cost in proportion to the chains still integrating (tail of a run,
-  // chains waiting in sync mode).  List order is arbitrary; a chain's result does not
-  // depend on its position.
-  if (wv == 0) {
-    const bool pend = (start_iter || prep_leaf);
-    const uint64_t m = __ballot(pend);
-    if (m) {
-      int base = 0;
-      if (lane == __builtin_ctzll(m))
-        base = atomicAdd(&a.counters[2 + cfg.parity], __builtin_popcountll(m));
-      base = __shfl(base, __builtin_ctzll(m));
-      if (pend) {
-        const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
-        a.active_idx[(size_t)cfg.parity * ldc + pos] = c;
+  // compacted list of chains whose next leaf is pending: the potential kernels then cost
+  // in proportion to the chains still integrating.  List order is arbitrary; a chain's
+  // result does not depend on its position.
+  const int lane = threadIdx.x & 63;
+  const bool pend = valid && (A.start_iter || A.prep_leaf);
+  const uint64_t m = __ballot(pend);
+  if (m) {
+    int base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(&a.counters[2 + cfg.parity], __builtin_popcountll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (pend) {
+      const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
+      a.active_idx[(size_t)cfg.parity * cfg.ldc + pos] = c;
+    }
+  }
+}
+
+// ---- per-coordinate vector bodies shared by both schedules -----------------------------
+struct VecCtx {
+  const Arena* a;
+  int ldc, D;
+  size_t ck_stride;
+};
+
+// L1 + L2 minus the proposal copy: finish the pending leapfrog (hmc_util.py:306-308),
+// kinetic energy, subtree r_sum, checkpoints and the U-turn partial dots.
+// red[0] = KE partial, red[1 + 2i + side] = checkpoint i, red[1 + 2 MAXD + side] = tree.
+template <bool NUTS>
+__device__ __forceinline__ void leaf_coord(const VecCtx& v, const Act& A, float seff, size_t idx, float* red) {
+  const Arena& a = *v.a;
+  float* const INVM = AV(NMX_F_INV_MASS);
+  float* ZF = A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
+  float* RF = A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  float* GF = A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL);
+  const float es = A.dirR ? seff : -seff;
+  const float half = 0.5f * es;
+  const float g = AV(NMX_F_G_EVAL)[idx];
+  const float r = RF[idx] - half * g;
+  const float im = INVM[idx];
+  RF[idx] = r;
+  ZF[idx] = AV(NMX_F_Z_EVAL)[idx];
+  GF[idx] = g;
+  red[0] += (im * r) * r;
+  if constexpr (NUTS) {
+    float* const RS = AV(NMX_F_RSUM_SUB);
+    const float rs = (A.k == 0) ? r : RS[idx] + r;
+    RS[idx] = rs;
+    if ((A.k & 1) == 0) {  // checkpoint update (:1040-1047)
+      a.ckr[A.imax * v.ck_stride + idx] = r;
+      a.ckrs[A.imax * v.ck_stride + idx] = rs;
+    }
+    // _is_iterative_turning (:961-981): all checkpoints in [imin, imax]; the reference
+    // stops at the first turning one, the OR over them is the same predicate.
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+      if (i >= A.imin && i <= A.imax) {
+        const float rl = a.ckr[i * v.ck_stride + idx];
+        const float rsub = (rs - a.ckrs[i * v.ck_stride + idx]) + rl;
+        const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
+        red[1 + 2 * i] += (im * rl) * rss;
+        red[2 + 2 * i] += (im * r) * rss;
+      }
+    }
+    // tentative whole-tree turning check with the tree's outer momenta (:795-799)
+    const float rst = AV(NMX_F_RSUM)[idx] + rs;
+    const float rlv = A.dirR ? AV(NMX_F_RL)[idx] : r;
+    const float rrv = A.dirR ? r : AV(NMX_F_RR)[idx];
+    const float rss2 = rst - (rlv + rrv) / 2.0f;
+    red[1 + 2 * MAXD] += (im * rlv) * rss2;
+    red[2 + 2 * MAXD] += (im * rrv) * rss2;
+  }
+}
+
+// Proposal copies, tree r_sum, HMC accept copy, Welford / window finalize, collection
+// (L3/L4), then the momentum draw + tree init or the next half step and z_eval (L5/L6,
+// velocity_verlet first half, hmc_util.py:297-301).  Returns the momentum KE partial.
+__device__ __forceinline__ float apply_coord(const VecCtx& v, const Act& A, float step_eff, int d, size_t idx,
+                                             const float* mom, float* samp, const int8_t* transform,
+                                             const nmx_nuts_config& cfg) {
+  const Arena& a = *v.a;
+  float* const INVM = AV(NMX_F_INV_MASS);
+  float* const ZP = AV(NMX_F_Z);
+  float* const GP = AV(NMX_F_ZGRAD);
+  if (A.take_leaf) {
+    AV(NMX_F_ZSUB)[idx] = (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
+    AV(NMX_F_GSUB)[idx] = (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+  }
+  if (A.done_sub) AV(NMX_F_RSUM)[idx] = AV(NMX_F_RSUM)[idx] + AV(NMX_F_RSUM_SUB)[idx];
+  if (A.take_biased) {
+    ZP[idx] = AV(NMX_F_ZSUB)[idx];
+    GP[idx] = AV(NMX_F_GSUB)[idx];
+  }
+  if (A.hmc_accept) {
+    ZP[idx] = AV(NMX_F_ZR)[idx];
+    GP[idx] = AV(NMX_F_GR)[idx];
+  }
+  if (A.iter_done) {
+    const float z = ZP[idx];
+    float* const WM = AV(NMX_F_WF_MEAN);
+    float* const W2 = AV(NMX_F_WF_M2);
+    if (A.wf_update) {  // welford_covariance update_fn, diagonal (:172-196)
+      const float mean = WM[idx];
+      const float delta_pre = z - mean;
+      const float mean_new = mean + delta_pre / (float)A.wfn;
+      const float delta_post = z - mean_new;
+      WM[idx] = mean_new;
+      W2[idx] = W2[idx] + delta_pre * delta_post;
+    }
+    if (A.finalize) {  // final_fn (:198-237)
+      float cov = W2[idx] / (float)(A.wfn - 1);
+      if (cfg.regularize_mass_matrix) {
+        const float scaled = ((float)A.wfn / (float)(A.wfn + 5)) * cov;
+        const float shrink = 1e-3f * (5.0f / (float)(A.wfn + 5));
+        cov = scaled + shrink;
+      }
+      INVM[idx] = cov;
+      AV(NMX_F_MASS_SQRT)[idx] = 1.0f / sqrtf(cov);
+      WM[idx] = 0.0f;
+      W2[idx] = 0.0f;
+    }
+    if (samp) samp[idx] = transform_value(transform[d], z);
+  }
+  float ke0 = 0.0f;
+  if (A.start_iter || A.prep_leaf) {
+    const int nd = A.new_dir;
+    float* const ZFn = nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
+    float* const RFn = nd ? AV(NMX_F_RR) : AV(NMX_F_RL);
+    float* const GFn = nd ? AV(NMX_F_GR) : AV(NMX_F_GL);
+    const float es = nd ? step_eff : -step_eff;
+    const float half = 0.5f * es;
+    float* const ZE = AV(NMX_F_Z_EVAL);
+    if (A.start_iter) {
+      float* const ZO = nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR);
+      float* const RO = nd ? AV(NMX_F_RL) : AV(NMX_F_RR);
+      float* const GO = nd ? AV(NMX_F_GL) : AV(NMX_F_GR);
+      const float r = AV(NMX_F_MASS_SQRT)[idx] * (*mom);  // momentum_generator hmc.py:92-110
+      const float z = ZP[idx];
+      const float g = GP[idx];
+      const float im = INVM[idx];
+      ke0 = (im * r) * r;
+      AV(NMX_F_RSUM)[idx] = r;
+      ZO[idx] = z;
+      GO[idx] = g;
+      RO[idx] = r;
+      ZFn[idx] = z;
+      GFn[idx] = g;
+      const float rh = r - half * g;
+      RFn[idx] = rh;
+      ZE[idx] = z + es * (im * rh);
+    } else {
+      const float rh = RFn[idx] - half * GFn[idx];
+      RFn[idx] = rh;
+      ZE[idx] = ZFn[idx] + es * (INVM[idx] * rh);
+    }
+  }
+  return ke0;
+}
+
+// Momentum normals of coordinates 4 blk .. 4 blk + 3 (one Philox call per block of 4).
+__device__ __forceinline__ void momentum_block(uint64_t seed, uint32_t gch, int it, int blk, float (&n)[4]) {
+  const nmx_u4 x = nmx_rng(seed, gch, (uint32_t)it, NMX_EV_MOMENTUM, blk, 0);
+  nmx_box_muller(x.x, x.y, n[0], n[1]);
+  nmx_box_muller(x.z, x.w, n[2], n[3]);
+}
+
+// ---- fused schedule ----------------------------------------------------------------------
+template <int TPC>
+__global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
+  __shared__ float lds[TPC > 1 ? NPART * TPC * 64 : 1];
+  const nmx_nuts_config& cfg = P.cfg;
+  const Arena& a = P.a;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int ldc = cfg.ldc;
+  const int D = cfg.dim;
+  const bool valid = c < cfg.num_chains;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+  // active list [parity ^ 1] was consumed by the previous potential launch; clear it for
+  // the next step (which appends to it).  List [parity] was cleared by the previous step.
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+
+  ChainScalars S;
+  Act A;
+  const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  begin_step(cfg, a, c, valid, S, A);
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  const float seff = valid ? S.step_eff : 0.0f;
+
+  float red[NPART];
+#pragma unroll
+  for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+  if (A.leaf) {
+    if (is_nuts) {
+      for (int d = wv; d < D; d += TPC) leaf_coord<true>(v, A, seff, (size_t)d * ldc + c, red);
+    } else {
+      for (int d = wv; d < D; d += TPC) leaf_coord<false>(v, A, seff, (size_t)d * ldc + c, red);
+    }
+  }
+  block_sum<TPC, NPART>(red, lds);
+  leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
+  tree_phase(
+      cfg, S, A, [&](int i, int side) { return red[1 + 2 * i + side]; },
+      [&](int side) { return red[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, wv == 0);
+
+  float ke0[1] = {0.0f};
+  const bool vec2 = A.take_leaf || A.done_sub || A.take_biased || A.hmc_accept || A.iter_done || A.start_iter ||
+                    A.prep_leaf;
+  if (vec2) {
+    float* const samp = A.slot >= 0 ? P.samples + (size_t)A.slot * D * ldc : nullptr;
+    const float step_eff = S.step_eff;
+    for (int blk = wv; 4 * blk < D; blk += TPC) {
+      float n[4] = {0.f, 0.f, 0.f, 0.f};
+      if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * blk + q;
+        if (d < D) ke0[0] += apply_coord(v, A, step_eff, d, (size_t)d * ldc + c, &n[q], samp, P.transform, cfg);
       }
     }
   }
+  block_sum<TPC, 1>(ke0, lds);
+  if (A.start_iter) {
+    S.E0 = S.pe + 0.5f * ke0[0];  // build_tree :1130
+    S.energy = S.E0;              // proposal energy of the initial tree (:1137)
+  }
+  if (wv == 0) end_step(cfg, a, c, valid, ph_in, S, A);
+}
+
+// ---- wide schedule -----------------------------------------------------------------------
+constexpr int WIDE_WAVES = 4;   // waves per V1/V2 block (64 chains x one D-slice)
+constexpr int WIDE_SWAVES = 4;  // waves per S block (slices split across waves)
+
+struct WideArgs {
+  StepArgs p;
+  int ns;  // slices
+  int sw;  // slice width (multiple of 4)
+};
+
+__device__ __forceinline__ float* part_ptr(const Arena& a, int ldc, int s, int i) {
+  return a.part + ((size_t)s * NPART + i) * ldc;
+}
+
+__global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
+  __shared__ float lds[NPART * WIDE_WAVES * 64];
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int s = blockIdx.y;
+  const int ldc = cfg.ldc, D = cfg.dim;
+  const bool valid = c < cfg.num_chains;
+  const int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  if (!__syncthreads_or(ph == NMX_PH_LEAF)) return;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  Act A{};
+  A.leaf = ph == NMX_PH_LEAF;
+  A.dirR = A.leaf ? AI(NMX_F_DIR)[c] : 0;
+  A.k = (A.leaf && is_nuts) ? AI(NMX_F_SUB_N)[c] : 0;
+  A.imin = 1;
+  A.imax = 0;
+  if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);
+  const float seff = A.leaf ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  float red[NPART];
+#pragma unroll
+  for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+  const int d0 = s * W.sw, d1 = min(D, d0 + W.sw);
+  if (A.leaf) {
+    if (is_nuts) {
+      for (int d = d0 + wv; d < d1; d += WIDE_WAVES) leaf_coord<true>(v, A, seff, (size_t)d * ldc + c, red);
+    } else {
+      for (int d = d0 + wv; d < d1; d += WIDE_WAVES) leaf_coord<false>(v, A, seff, (size_t)d * ldc + c, red);
+    }
+  }
+  block_sum<WIDE_WAVES, NPART>(red, lds);
+  if (wv == 0 && A.leaf) {
+    *(part_ptr(a, ldc, s, 0) + c) = red[0];
+    if (is_nuts) {
+#pragma unroll
+      for (int i = 0; i < MAXD; ++i)
+        if (i >= A.imin && i <= A.imax) {
+          *(part_ptr(a, ldc, s, 1 + 2 * i) + c) = red[1 + 2 * i];
+          *(part_ptr(a, ldc, s, 2 + 2 * i) + c) = red[2 + 2 * i];
+        }
+      *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c) = red[1 + 2 * MAXD];
+      *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c) = red[2 + 2 * MAXD];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_s(WideArgs W) {
+  __shared__ float lds[(NPART + 1) * WIDE_SWAVES * 64];
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int ldc = cfg.ldc;
+  const bool valid = c < cfg.num_chains;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+
+  ChainScalars S;
+  Act A;
+  const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  begin_step(cfg, a, c, valid, S, A);
+  const bool ke0_pending = valid && (AI(NMX_F_ACTION)[c] & ACT_KE0_PENDING);
+  // fixed-order reduction of the slice partials: wave w sums slices w, w+4, ... in order,
+  // then wave 0 sums the waves in order.
+  float red[NPART + 1];
+#pragma unroll
+  for (int i = 0; i < NPART + 1; ++i) red[i] = 0.0f;
+  for (int s = wv; s < W.ns; s += WIDE_SWAVES) {
+    if (A.leaf) {
+      red[0] += *(part_ptr(a, ldc, s, 0) + c);
+      if (is_nuts) {
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i)
+          if (i >= A.imin && i <= A.imax) {
+            red[1 + 2 * i] += *(part_ptr(a, ldc, s, 1 + 2 * i) + c);
+            red[2 + 2 * i] += *(part_ptr(a, ldc, s, 2 + 2 * i) + c);
+          }
+        red[1 + 2 * MAXD] += *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c);
+        red[2 + 2 * MAXD] += *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c);
+      }
+    }
+    if (ke0_pending) red[NPART] += a.part0[(size_t)s * ldc + c];
+  }
+#pragma unroll
+  for (int i = 0; i < NPART + 1; ++i) lds[(i * WIDE_SWAVES + wv) * 64 + lane] = red[i];
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int i = 0; i < NPART + 1; ++i) {
+    float t = 0.0f;
+    for (int w = 0; w < WIDE_SWAVES; ++w) t += lds[(i * WIDE_SWAVES + w) * 64 + lane];
+    red[i] = t;
+  }
+  if (ke0_pending) {
+    S.E0 = S.pe + 0.5f * red[NPART];  // build_tree :1130 (momentum KE from the last V2)
+    S.energy = S.E0;
+  }
+  leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
+  tree_phase(
+      cfg, S, A, [&](int i, int side) { return red[1 + 2 * i + side]; },
+      [&](int side) { return red[1 + 2 * MAXD + side]; }, seed, gch, W.p.fields, c, true);
+  if (valid) {
+    AI(NMX_F_ACTION)[c] = pack_act(A);
+    AI(NMX_F_SLOT)[c] = A.slot;
+    AI(NMX_F_ACT_WFN)[c] = A.wfn;
+  }
+  // (a chain with ke0_pending is a LEAF chain, so end_step stores its E0)
+  end_step(cfg, a, c, valid, ph_in, S, A);
+}
+
+__global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
+  __shared__ float lds[WIDE_WAVES * 64];
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int s = blockIdx.y;
+  const int ldc = cfg.ldc, D = cfg.dim;
+  const bool valid = c < cfg.num_chains;
+  const int act = valid ? AI(NMX_F_ACTION)[c] : 0;
+  constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_START |
+                      ACT_PREP;
+  if (!__syncthreads_or((act & VEC) != 0)) return;
+  Act A{};
+  A.take_leaf = act & ACT_TAKE_LEAF;
+  A.done_sub = act & ACT_DONE_SUB;
+  A.take_biased = act & ACT_TAKE_BIASED;
+  A.hmc_accept = act & ACT_HMC_ACCEPT;
+  A.iter_done = act & ACT_ITER_DONE;
+  A.wf_update = act & ACT_WF_UPDATE;
+  A.finalize = act & ACT_FINALIZE;
+  A.start_iter = act & ACT_START;
+  A.prep_leaf = act & ACT_PREP;
+  A.dirR = (act & ACT_DIRR) ? 1 : 0;
+  A.new_dir = (act & ACT_NEWDIR) ? 1 : 0;
+  A.slot = valid ? AI(NMX_F_SLOT)[c] : -1;
+  A.wfn = valid ? AI(NMX_F_ACT_WFN)[c] : 0;
+  const float step_eff = valid ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
+  const int it = valid ? AI(NMX_F_ITER)[c] : 0;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  float* const samp = (A.iter_done && A.slot >= 0) ? W.p.samples + (size_t)A.slot * D * ldc : nullptr;
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  float ke0[1] = {0.0f};
+  if (act & VEC) {
+    const int b0 = (s * W.sw) / 4, b1 = (min(D, (s + 1) * W.sw) + 3) / 4;
+    for (int blk = b0 + wv; blk < b1; blk += WIDE_WAVES) {
+      float n[4] = {0.f, 0.f, 0.f, 0.f};
+      if (A.start_iter) momentum_block(cfg.seed, gch, it, blk, n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * blk + q;
+        if (d < D) ke0[0] += apply_coord(v, A, step_eff, d, (size_t)d * ldc + c, &n[q], samp, W.p.transform, cfg);
+      }
+    }
+  }
+  block_sum<WIDE_WAVES, 1>(ke0, lds);
+  if (wv == 0 && A.start_iter) a.part0[(size_t)s * ldc + c] = ke0[0];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -801,13 +1018,12 @@ Arena arena_of(const nmx_nuts_config* cfg, void* base) {
   return make_arena(base, cfg->ldc, cfg->dim, cfg->max_depth_alloc, cfg->iter_capacity);
 }
 
-int tpc_for_dim(int D) {
-  if (D < 16) return 1;
-  if (D <= 256) return 8;
-  return 16;
-}
+// fused schedule only (D < WIDE_MIN_D)
+int tpc_for_dim(int D) { return D < 16 ? 1 : 8; }
 
 }  // namespace
+
+extern "C" int nmx_nuts_num_slices(int dim) { return num_slices(dim); }
 
 extern "C" size_t nmx_nuts_arena_bytes(int num_chains, int dim, int max_depth_alloc, int iter_capacity) {
   const int ldc = ldc_of(num_chains);
@@ -890,10 +1106,15 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   const int grid = cfg->ldc / 64;
   hipStream_t s = (hipStream_t)stream;
   if (cfg->parity != 0 && cfg->parity != 1) return nmx_fail(NMX_ERR_INVALID, "parity must be 0 or 1");
-  switch (tpc_for_dim(cfg->dim)) {
-    case 1: hipLaunchKernelGGL(k_nuts_step<1>, dim3(grid), dim3(64), 0, s, args); break;
-    case 8: hipLaunchKernelGGL(k_nuts_step<8>, dim3(grid), dim3(512), 0, s, args); break;
-    default: hipLaunchKernelGGL(k_nuts_step<16>, dim3(grid), dim3(1024), 0, s, args); break;
+  const int ns = num_slices(cfg->dim);
+  if (ns > 0) {
+    WideArgs w{args, ns, slice_width(cfg->dim)};
+    hipLaunchKernelGGL(k_wide_v1, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
+    hipLaunchKernelGGL(k_wide_s, dim3(grid), dim3(64 * WIDE_SWAVES), 0, s, w);
+    hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
+    return nmx_check_launch("k_nuts_step (wide)");
   }
+  if (tpc_for_dim(cfg->dim) == 1) hipLaunchKernelGGL(k_nuts_step<1>, dim3(grid), dim3(64), 0, s, args);
+  else hipLaunchKernelGGL(k_nuts_step<8>, dim3(grid), dim3(512), 0, s, args);
   return nmx_check_launch("k_nuts_step");
 }

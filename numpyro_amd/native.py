@@ -37,11 +37,12 @@ PH_DONE, PH_WAIT, PH_START, PH_LEAF, PH_INITEVAL, PH_NEEDINIT = range(6)
 FIELDS = [
     "phase", "iter", "depth", "sub_n", "dir", "tree_n", "window_idx", "da_t", "wf_n", "turning",
     "tree_div", "sub_div", "hmc_k", "hmc_n", "last_nsteps", "last_div", "maxdepth_cur",
+    "action", "slot", "act_wfn",
     "step_size", "e0", "pe", "energy", "tree_w", "tree_acc", "sub_w", "sub_acc", "pe_sub", "e_sub",
     "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "pe_eval",
     "z", "zgrad", "zl", "rl", "gl", "zr", "rr", "gr", "zsub", "gsub", "rsum", "rsum_sub",
     "inv_mass", "mass_sqrt", "wf_mean", "wf_m2", "z_eval", "g_eval",
-    "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished",
+    "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished", "part", "part0",
 ]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 INT_FIELDS = set(FIELDS[:FIELDS.index("step_size")]) | {"counters", "finished", "active_idx"}
@@ -93,6 +94,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_selftest_philox": (c_int, [c_vp, c_vp, c_int, c_vp]),
     "nmx_selftest_mfma": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_nuts_arena_bytes": (c_size, [c_int, c_int, c_int, c_int]),
+    "nmx_nuts_num_slices": (c_int, [c_int]),
     "nmx_nuts_field_info": (c_int, [c_int, c_int, c_int, c_int, c_int, _P(c_size), _P(c_size)]),
     "nmx_nuts_reset": (c_int, [_cfgp, c_vp, c_float, c_vp, c_vp]),
     "nmx_nuts_init_draw": (c_int, [_cfgp, c_vp, c_int, c_float, c_vp]),

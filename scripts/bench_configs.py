@@ -1,0 +1,152 @@
+"""Throughput of the BASELINE.json secondary configs (one GPU), plus kernel microbenchmarks.
+
+    python scripts/bench_configs.py gemm  [D] [C]          # nmx_gemm_chains alone
+    python scripts/bench_configs.py funnel [--dim 10000 --chains 4096 --warmup W --steps K]
+    python scripts/bench_configs.py sv     [--chains 1024 ...]
+    python scripts/bench_configs.py bnn    [--chains 2048 ...]
+    python scripts/bench_configs.py covtype [--chains 1024 ...]
+
+Each model run does `mcmc.warmup` (untimed) then times `mcmc.run` between synchronizes and
+prints one JSON line: leapfrogs/s (= sum num_steps / wall), average potential-launch time
+(HIP events on the launch stream) and the roofline fraction of the dominant kernel.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from numpyro_amd import datasets, native  # noqa: E402
+from numpyro_amd import potentials as P  # noqa: E402
+from numpyro_amd.infer import MCMC, NUTS  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def bench_gemm(D, C, reps=10):
+    dev = torch.device("cuda:0")
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    ldc = (C + 63) // 64 * 64
+    At = torch.zeros(lda, lda, device=dev)
+    At[:D, :D] = torch.randn(D, D, device=dev)
+    x = torch.randn(D, ldc, device=dev)
+    y = torch.empty(D, ldc, device=dev)
+    s = native.stream_ptr()
+    for _ in range(2):
+        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, ldc, None, C, s))
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, ldc, None, C, s))
+    b.record()
+    b.synchronize()
+    ms = a.elapsed_time(b) / reps
+    tf = 2.0 * D * D * C / (ms * 1e-3) / 1e12
+    ref = (At[:D, :D].t().double() @ x[:, :8].double())
+    err = float((y[:, :8].double() - ref).abs().max() / ref.abs().max())
+    print(json.dumps({"kernel": "k_gemm_chains", "D": D, "C": C, "ms": round(ms, 4), "tflops": round(tf, 2),
+                      "frac": round(tf / PEAK_F32_TFLOPS, 3), "max_rel_err": err}), flush=True)
+
+
+class Timed:
+    """Wraps Potential.evaluate with HIP events on the launch stream."""
+
+    def __init__(self, pot):
+        self.pot, self.orig, self.events = pot, pot.evaluate, []
+        self.on = False
+        pot.evaluate = self
+
+    def __call__(self, ev, s):
+        if not self.on:
+            return self.orig(ev, s)
+        st = torch.cuda.ExternalStream(s)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        self.orig(ev, s)
+        b.record(st)
+        self.events.append((a, b))
+
+    def total_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None, bytes_per_leapfrog=None,
+              **kernel_kw):
+    kernel = NUTS(model, **kernel_kw)
+    mcmc = MCMC(kernel, num_warmup=warmup, num_samples=steps, num_chains=chains, progress_bar=False)
+    t0 = time.time()
+    mcmc.warmup(0, *args, extra_fields=("num_steps",))
+    torch.cuda.synchronize()
+    t_warm = time.time() - t0
+    eng = mcmc._engine
+    timer = Timed(eng.potential)
+    timer.on = True
+    torch.cuda.synchronize()
+    t0 = time.time()
+    mcmc.run(1, *args, extra_fields=("num_steps",))
+    torch.cuda.synchronize()
+    wall = time.time() - t0
+    timer.on = False
+    ns = int(mcmc.get_extra_fields()["num_steps"].sum().item())
+    pot_ms = timer.total_ms()
+    launches = len(timer.events)
+    out = {"config": name, "chains": chains, "dim": eng.D, "warmup": warmup, "steps": steps,
+           "leapfrogs": ns, "wall_s": round(wall, 3), "leapfrog_per_s": round(ns / wall, 1),
+           "launches": launches, "potential_ms_avg": round(pot_ms / max(launches, 1), 4),
+           "potential_share": round(pot_ms / 1e3 / wall, 3), "warmup_wall_s": round(t_warm, 2),
+           "dense": bool(eng.dense)}
+    if flops_per_leapfrog:
+        tf = flops_per_leapfrog * ns / (pot_ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved_tflops": round(tf, 2), "frac": round(tf / PEAK_F32_TFLOPS, 3)}
+    if bytes_per_leapfrog:
+        gbs = bytes_per_leapfrog * ns / (pot_ms * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 3)}
+    print(json.dumps(out), flush=True)
+    return mcmc
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("what")
+    p.add_argument("rest", nargs="*")
+    p.add_argument("--chains", type=int, default=None)
+    p.add_argument("--dim", type=int, default=10000)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--max-tree-depth", type=int, default=10)
+    p.add_argument("--dense", type=int, default=1)
+    a = p.parse_args()
+    if a.what == "gemm":
+        D = int(a.rest[0]) if a.rest else 10000
+        C = int(a.rest[1]) if len(a.rest) > 1 else 4096
+        bench_gemm(D, C)
+    elif a.what == "funnel":
+        D = a.dim
+        # dense: two products z = T w, g = T^T g_z (2 D^2 FLOP each as executed, full T)
+        run_model("funnel", P.funnel, (D,), a.chains or 4096, a.warmup, a.steps,
+                  flops_per_leapfrog=4.0 * D * D if a.dense else None,
+                  bytes_per_leapfrog=None if a.dense else 3 * D * 4,
+                  dense_mass=bool(a.dense), max_tree_depth=a.max_tree_depth)
+    elif a.what == "sv":
+        r = datasets.sp500_synthetic()
+        D = r.size + 2
+        run_model("stochastic_volatility", P.stochastic_volatility, (r,), a.chains or 1024, a.warmup, a.steps,
+                  bytes_per_leapfrog=2 * D * 4, max_tree_depth=a.max_tree_depth)
+    elif a.what == "covtype":
+        X, y = datasets.covtype_synthetic(seed=0)
+        dev = torch.device("cuda:0")
+        Xd, yd = torch.from_numpy(X).to(dev), torch.from_numpy(y).to(dev)
+        run_model("covtype", P.logistic_regression, (Xd, yd), a.chains or 1024, a.warmup, a.steps,
+                  flops_per_leapfrog=4.0 * X.shape[0] * X.shape[1], max_tree_depth=a.max_tree_depth)
+    else:
+        raise SystemExit(f"unknown config {a.what}")
+
+
+if __name__ == "__main__":
+    main()

@@ -87,11 +87,13 @@ def test_engine_matches_oracle_eight_schools(device, algo):
 
 
 @pytest.mark.parametrize("algo", ["NUTS", "HMC"])
-@pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300)])
+@pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300),
+                                       ("diag_normal", 1500)])
 def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     """No adaptation, fixed step size: every transition is a deterministic function of
-    the Philox stream; device and oracle must take the same discrete path.  dim 40 / 300
-    exercise the multi-wave (8 / 16 waves per 64 chains) step kernel."""
+    the Philox stream; device and oracle must take the same discrete path.  dim 40 runs the
+    fused multi-wave step kernel (8 waves per 64 chains), dim 300 / 1500 the wide D-split
+    schedule (nmx_nuts_num_slices > 0; slice widths 32)."""
     seed, C, T = 77, 64, 3
     rs = np.random.RandomState(dim)
     if model == "logreg":
@@ -126,13 +128,20 @@ def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     assert match >= int(0.95 * C), f"only {match}/{C} chains reproduced the oracle path"
 
 
-def test_num_steps_equals_potential_evaluations(device):
+@pytest.mark.parametrize("model", ["logreg", "wide"])
+def test_num_steps_equals_potential_evaluations(device, model):
     """Every leaf consumes exactly one potential evaluation (the compacted list length),
-    summed over the run -- guards the multi-wave step kernel's state handling."""
+    summed over the run -- guards the multi-wave / D-split step kernels' state handling."""
     rs = np.random.RandomState(3)
-    X = rs.randn(2000, 55).astype(np.float32)
-    y = (rs.rand(2000) < 0.5).astype(np.float32)
-    mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=20, num_samples=10, num_chains=200)
+    if model == "logreg":
+        X = rs.randn(2000, 55).astype(np.float32)
+        y = (rs.rand(2000) < 0.5).astype(np.float32)
+        fm = P.logistic_regression
+    else:
+        X = rs.randn(900).astype(np.float32)
+        y = (0.3 + rs.rand(900)).astype(np.float32)
+        fm = P.diag_normal
+    mcmc = MCMC(NUTS(fm), num_warmup=20, num_samples=10, num_chains=200)
     mcmc.warmup(0, X, y)
     eng = mcmc._engine
     cnt = eng.view("counters")
@@ -163,6 +172,26 @@ def test_sync_and_async_schedules_are_bitwise_identical(device):
                                   b.get_extra_fields()["num_steps"].cpu().numpy())
     # the sync schedule wastes leapfrogs waiting for the slowest chain
     assert b.last_run_stats["launches"] >= a.last_run_stats["launches"]
+
+
+def test_wide_schedule_invariances(device):
+    """D-split step (dim >= 257): sync == async and sharded == unsharded, bitwise; and
+    every leaf consumes exactly one evaluation."""
+    assert native.lib().nmx_nuts_num_slices(700) > 0 and native.lib().nmx_nuts_num_slices(200) == 0
+    rs = np.random.RandomState(0)
+    mu = rs.randn(700).astype(np.float32)
+    sd = (0.5 + rs.rand(700)).astype(np.float32)
+    args = (mu, sd)
+    a, _ = _run_engine(args, P.diag_normal, 96, 40, 15, 3, sync=False)
+    b, _ = _run_engine(args, P.diag_normal, 96, 40, 15, 3, sync=True)
+    lo, _ = _run_engine(args, P.diag_normal, 30, 40, 15, 3, chain_offset=0)
+    hi, _ = _run_engine(args, P.diag_normal, 66, 40, 15, 3, chain_offset=30)
+    xa = a.get_samples(True)["x"].cpu().numpy()
+    np.testing.assert_array_equal(xa, b.get_samples(True)["x"].cpu().numpy())
+    np.testing.assert_array_equal(xa[:30], lo.get_samples(True)["x"].cpu().numpy())
+    np.testing.assert_array_equal(xa[30:], hi.get_samples(True)["x"].cpu().numpy())
+    x = xa.reshape(-1, 700)
+    assert np.abs(x.mean(0) - mu).mean() < 0.2 and np.abs(x.std(0) / sd - 1).mean() < 0.2
 
 
 def test_chain_sharding_is_bitwise_invariant(device):
