@@ -194,10 +194,13 @@ int nmx_pe_eight_schools(const float* y, const float* sigma, int J, const nmx_ev
 /* Stochastic volatility (examples/stochastic_volatility.py:57-65): sigma ~ Exponential(50),
  * s ~ GaussianRandomWalk(sigma, T), nu ~ Exponential(0.1), r ~ StudentT(nu, 0, exp(s));
  * z = (log nu, s[T], log sigma).  HBM-bound stencil, lgamma/digamma for nu. */
-int nmx_pe_stochastic_volatility(const float* returns, int T, const nmx_eval_batch* ev, void* stream);
+int nmx_pe_stochastic_volatility(const float* returns, int T, const nmx_eval_batch* ev, void* workspace,
+                                 void* stream);
 /* Centred funnel (examples/funnel.py:44-46): y ~ N(0,3), x ~ N(0, exp(y/2))^(dim-1);
  * z = (x[dim-1], y). */
-int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* stream);
+int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* workspace, void* stream);
+/* Workspace (per-slice partial sums) of the two kernels above for num_chains chains. */
+size_t nmx_pe_wide_workspace_bytes(int dim, int num_chains);
 
 /* Logistic regression (examples/covtype.py:66-71): coefs ~ N(0,1)^D,
  * obs ~ BernoulliLogits(X @ coefs).  X is first packed (row tiles with the label in a pad

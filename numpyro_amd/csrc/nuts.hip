@@ -517,26 +517,51 @@ struct VecCtx {
 // L1 + L2 minus the proposal copy: finish the pending leapfrog (hmc_util.py:306-308),
 // kinetic energy, subtree r_sum, checkpoints and the U-turn partial dots.
 // red[0] = KE partial, red[1 + 2i + side] = checkpoint i, red[1 + 2 MAXD + side] = tree.
-template <bool NUTS>
-__device__ __forceinline__ void leaf_coord(const VecCtx& v, const Act& A, float seff, size_t idx, float* red) {
+// Split into a load stage and a compute/store stage so that several rows' loads are in
+// flight before the (possibly aliasing, from the compiler's view) stores.
+struct LeafIn {
+  float g, rf, im, ze, rs_old, rst, ro;
+  float ckr[MAXD], ckrs[MAXD];
+};
+
+template <bool NUTS, bool PRE>
+__device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t idx, LeafIn& x) {
   const Arena& a = *v.a;
-  float* const INVM = AV(NMX_F_INV_MASS);
-  float* ZF = A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
-  float* RF = A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
-  float* GF = A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL);
+  x.g = AV(NMX_F_G_EVAL)[idx];
+  x.rf = (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
+  x.im = AV(NMX_F_INV_MASS)[idx];
+  x.ze = AV(NMX_F_Z_EVAL)[idx];
+  if constexpr (NUTS) {
+    x.rs_old = A.k == 0 ? 0.0f : AV(NMX_F_RSUM_SUB)[idx];
+    x.rst = AV(NMX_F_RSUM)[idx];
+    x.ro = (A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx];  // the other end's momentum
+    // checkpoints read by the U-turn check; the range is empty for even leaves, whose
+    // checkpoint write below therefore never feeds this step's check (:1036-1047)
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+      if (PRE && i >= A.imin && i <= A.imax) {
+        x.ckr[i] = a.ckr[i * v.ck_stride + idx];
+        x.ckrs[i] = a.ckrs[i * v.ck_stride + idx];
+      }
+    }
+  }
+}
+
+template <bool NUTS, bool PRE>
+__device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float seff, size_t idx, const LeafIn& x,
+                                           float* red) {
+  const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
-  const float g = AV(NMX_F_G_EVAL)[idx];
-  const float r = RF[idx] - half * g;
-  const float im = INVM[idx];
-  RF[idx] = r;
-  ZF[idx] = AV(NMX_F_Z_EVAL)[idx];
-  GF[idx] = g;
+  const float r = x.rf - half * x.g;
+  (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = r;
+  (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = x.ze;
+  (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = x.g;
+  const float im = x.im;
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
-    float* const RS = AV(NMX_F_RSUM_SUB);
-    const float rs = (A.k == 0) ? r : RS[idx] + r;
-    RS[idx] = rs;
+    const float rs = (A.k == 0) ? r : x.rs_old + r;
+    AV(NMX_F_RSUM_SUB)[idx] = rs;
     if ((A.k & 1) == 0) {  // checkpoint update (:1040-1047)
       a.ckr[A.imax * v.ck_stride + idx] = r;
       a.ckrs[A.imax * v.ck_stride + idx] = rs;
@@ -546,104 +571,210 @@ __device__ __forceinline__ void leaf_coord(const VecCtx& v, const Act& A, float 
 #pragma unroll
     for (int i = 0; i < MAXD; ++i) {
       if (i >= A.imin && i <= A.imax) {
-        const float rl = a.ckr[i * v.ck_stride + idx];
-        const float rsub = (rs - a.ckrs[i * v.ck_stride + idx]) + rl;
+        const float rl = PRE ? x.ckr[i] : a.ckr[i * v.ck_stride + idx];
+        const float rsub = (rs - (PRE ? x.ckrs[i] : a.ckrs[i * v.ck_stride + idx])) + rl;
         const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
         red[1 + 2 * i] += (im * rl) * rss;
         red[2 + 2 * i] += (im * r) * rss;
       }
     }
     // tentative whole-tree turning check with the tree's outer momenta (:795-799)
-    const float rst = AV(NMX_F_RSUM)[idx] + rs;
-    const float rlv = A.dirR ? AV(NMX_F_RL)[idx] : r;
-    const float rrv = A.dirR ? r : AV(NMX_F_RR)[idx];
+    const float rst = x.rst + rs;
+    const float rlv = A.dirR ? x.ro : r;
+    const float rrv = A.dirR ? r : x.ro;
     const float rss2 = rst - (rlv + rrv) / 2.0f;
     red[1 + 2 * MAXD] += (im * rlv) * rss2;
     red[2 + 2 * MAXD] += (im * rrv) * rss2;
   }
 }
 
+// rows d0, d0 + step, ... < d1 of chain column c, ROWS rows per iteration
+template <bool NUTS, int ROWS>
+__device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float seff, int d0, int d1, int step, int c,
+                                          float* red) {
+  int d = d0;
+  if constexpr (ROWS == 2) {
+    for (; d + step < d1; d += 2 * step) {
+      LeafIn x0, x1;
+      const size_t i0 = (size_t)d * v.ldc + c, i1 = (size_t)(d + step) * v.ldc + c;
+      leaf_load<NUTS, true>(v, A, i0, x0);
+      leaf_load<NUTS, true>(v, A, i1, x1);
+      leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
+      leaf_store<NUTS, true>(v, A, seff, i1, x1, red);
+    }
+  }
+  for (; d < d1; d += step) {
+    LeafIn x0;
+    const size_t i0 = (size_t)d * v.ldc + c;
+    leaf_load<NUTS, ROWS == 2>(v, A, i0, x0);
+    leaf_store<NUTS, ROWS == 2>(v, A, seff, i0, x0, red);
+  }
+}
+
 // Proposal copies, tree r_sum, HMC accept copy, Welford / window finalize, collection
 // (L3/L4), then the momentum draw + tree init or the next half step and z_eval (L5/L6,
-// velocity_verlet first half, hmc_util.py:297-301).  Returns the momentum KE partial.
-__device__ __forceinline__ float apply_coord(const VecCtx& v, const Act& A, float step_eff, int d, size_t idx,
-                                             const float* mom, float* samp, const int8_t* transform,
-                                             const nmx_nuts_config& cfg) {
+// velocity_verlet first half, hmc_util.py:297-301).  Load stage first (values the
+// stores below would otherwise serialise behind), then compute/store.
+struct ApplyIn {
+  float zf, gf;     // old frontier (take_leaf)
+  float rst, rss;   // tree / subtree r_sum (done_sub)
+  float zs, gs;     // subtree proposal (take_biased)
+  float zr, gr;     // HMC end point
+  float zp, gp;     // state
+  float wm, w2;     // Welford
+  float ms, im;     // mass
+  float zfn, rfn, gfn;  // new frontier (prep_leaf)
+};
+
+__device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t idx, ApplyIn& x) {
   const Arena& a = *v.a;
-  float* const INVM = AV(NMX_F_INV_MASS);
-  float* const ZP = AV(NMX_F_Z);
-  float* const GP = AV(NMX_F_ZGRAD);
   if (A.take_leaf) {
-    AV(NMX_F_ZSUB)[idx] = (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
-    AV(NMX_F_GSUB)[idx] = (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+    x.zf = (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
+    x.gf = (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
   }
-  if (A.done_sub) AV(NMX_F_RSUM)[idx] = AV(NMX_F_RSUM)[idx] + AV(NMX_F_RSUM_SUB)[idx];
-  if (A.take_biased) {
-    ZP[idx] = AV(NMX_F_ZSUB)[idx];
-    GP[idx] = AV(NMX_F_GSUB)[idx];
+  if (A.done_sub) {
+    x.rst = AV(NMX_F_RSUM)[idx];
+    x.rss = AV(NMX_F_RSUM_SUB)[idx];
+  }
+  if (A.take_biased && !A.take_leaf) {
+    x.zs = AV(NMX_F_ZSUB)[idx];
+    x.gs = AV(NMX_F_GSUB)[idx];
   }
   if (A.hmc_accept) {
-    ZP[idx] = AV(NMX_F_ZR)[idx];
-    GP[idx] = AV(NMX_F_GR)[idx];
+    x.zr = AV(NMX_F_ZR)[idx];
+    x.gr = AV(NMX_F_GR)[idx];
   }
+  const bool need_state = (A.iter_done || A.start_iter) && !A.take_biased && !A.hmc_accept;
+  if (need_state) {
+    x.zp = AV(NMX_F_Z)[idx];
+    x.gp = AV(NMX_F_ZGRAD)[idx];
+  }
+  if (A.wf_update || A.finalize) {
+    x.wm = AV(NMX_F_WF_MEAN)[idx];
+    x.w2 = AV(NMX_F_WF_M2)[idx];
+  }
+  if (A.start_iter) x.ms = AV(NMX_F_MASS_SQRT)[idx];
+  if (A.start_iter || A.prep_leaf) x.im = AV(NMX_F_INV_MASS)[idx];
+  if (A.prep_leaf) {
+    const int nd = A.new_dir;
+    x.zfn = (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
+    x.rfn = (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
+    x.gfn = (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+  }
+}
+
+// Returns the momentum KE partial (start_iter).
+__device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, float step_eff, int d, size_t idx,
+                                             ApplyIn& x, float mom, float* samp, const int8_t* transform,
+                                             const nmx_nuts_config& cfg) {
+  const Arena& a = *v.a;
+  if (A.take_leaf) {
+    AV(NMX_F_ZSUB)[idx] = x.zf;
+    AV(NMX_F_GSUB)[idx] = x.gf;
+    x.zs = x.zf;
+    x.gs = x.gf;
+  }
+  if (A.done_sub) AV(NMX_F_RSUM)[idx] = x.rst + x.rss;
+  if (A.take_biased) {
+    AV(NMX_F_Z)[idx] = x.zs;
+    AV(NMX_F_ZGRAD)[idx] = x.gs;
+    x.zp = x.zs;
+    x.gp = x.gs;
+  }
+  if (A.hmc_accept) {
+    AV(NMX_F_Z)[idx] = x.zr;
+    AV(NMX_F_ZGRAD)[idx] = x.gr;
+    x.zp = x.zr;
+    x.gp = x.gr;
+  }
+  float im = x.im;
   if (A.iter_done) {
-    const float z = ZP[idx];
-    float* const WM = AV(NMX_F_WF_MEAN);
-    float* const W2 = AV(NMX_F_WF_M2);
+    const float z = x.zp;
     if (A.wf_update) {  // welford_covariance update_fn, diagonal (:172-196)
-      const float mean = WM[idx];
+      const float mean = x.wm;
       const float delta_pre = z - mean;
       const float mean_new = mean + delta_pre / (float)A.wfn;
       const float delta_post = z - mean_new;
-      WM[idx] = mean_new;
-      W2[idx] = W2[idx] + delta_pre * delta_post;
+      x.wm = mean_new;
+      x.w2 = x.w2 + delta_pre * delta_post;
+      AV(NMX_F_WF_MEAN)[idx] = x.wm;
+      AV(NMX_F_WF_M2)[idx] = x.w2;
     }
     if (A.finalize) {  // final_fn (:198-237)
-      float cov = W2[idx] / (float)(A.wfn - 1);
+      float cov = x.w2 / (float)(A.wfn - 1);
       if (cfg.regularize_mass_matrix) {
         const float scaled = ((float)A.wfn / (float)(A.wfn + 5)) * cov;
         const float shrink = 1e-3f * (5.0f / (float)(A.wfn + 5));
         cov = scaled + shrink;
       }
-      INVM[idx] = cov;
-      AV(NMX_F_MASS_SQRT)[idx] = 1.0f / sqrtf(cov);
-      WM[idx] = 0.0f;
-      W2[idx] = 0.0f;
+      im = cov;
+      x.ms = 1.0f / sqrtf(cov);
+      AV(NMX_F_INV_MASS)[idx] = cov;
+      AV(NMX_F_MASS_SQRT)[idx] = x.ms;
+      AV(NMX_F_WF_MEAN)[idx] = 0.0f;
+      AV(NMX_F_WF_M2)[idx] = 0.0f;
     }
     if (samp) samp[idx] = transform_value(transform[d], z);
   }
   float ke0 = 0.0f;
   if (A.start_iter || A.prep_leaf) {
     const int nd = A.new_dir;
-    float* const ZFn = nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL);
-    float* const RFn = nd ? AV(NMX_F_RR) : AV(NMX_F_RL);
-    float* const GFn = nd ? AV(NMX_F_GR) : AV(NMX_F_GL);
     const float es = nd ? step_eff : -step_eff;
     const float half = 0.5f * es;
     float* const ZE = AV(NMX_F_Z_EVAL);
     if (A.start_iter) {
-      float* const ZO = nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR);
-      float* const RO = nd ? AV(NMX_F_RL) : AV(NMX_F_RR);
-      float* const GO = nd ? AV(NMX_F_GL) : AV(NMX_F_GR);
-      const float r = AV(NMX_F_MASS_SQRT)[idx] * (*mom);  // momentum_generator hmc.py:92-110
-      const float z = ZP[idx];
-      const float g = GP[idx];
-      const float im = INVM[idx];
+      const float r = x.ms * mom;  // momentum_generator hmc.py:92-110
+      const float z = x.zp;
+      const float g = x.gp;
       ke0 = (im * r) * r;
       AV(NMX_F_RSUM)[idx] = r;
-      ZO[idx] = z;
-      GO[idx] = g;
-      RO[idx] = r;
-      ZFn[idx] = z;
-      GFn[idx] = g;
+      (nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR))[idx] = z;
+      (nd ? AV(NMX_F_GL) : AV(NMX_F_GR))[idx] = g;
+      (nd ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx] = r;
+      (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = z;
+      (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = g;
       const float rh = r - half * g;
-      RFn[idx] = rh;
+      (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
       ZE[idx] = z + es * (im * rh);
     } else {
-      const float rh = RFn[idx] - half * GFn[idx];
-      RFn[idx] = rh;
-      ZE[idx] = ZFn[idx] + es * (INVM[idx] * rh);
+      const float rh = x.rfn - half * x.gfn;
+      (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
+      ZE[idx] = x.zfn + es * (im * rh);
     }
+  }
+  return ke0;
+}
+
+// One block of 4 coordinates (the momentum block).  BATCH: loads of all 4 rows, then the
+// stores (wide schedule); otherwise row by row (fused kernel, register-bound).
+template <bool BATCH>
+__device__ __forceinline__ float apply_block(const VecCtx& v, const Act& A, float step_eff, int blk, int c,
+                                             const float (&n)[4], float* samp, const int8_t* transform,
+                                             const nmx_nuts_config& cfg) {
+  if constexpr (!BATCH) {
+    float ke0 = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = 4 * blk + q;
+      if (d < v.D) {
+        ApplyIn x;
+        apply_load(v, A, (size_t)d * v.ldc + c, x);
+        ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x, n[q], samp, transform, cfg);
+      }
+    }
+    return ke0;
+  }
+  ApplyIn x[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int d = 4 * blk + q;
+    if (d < v.D) apply_load(v, A, (size_t)d * v.ldc + c, x[q]);
+  }
+  float ke0 = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int d = 4 * blk + q;
+    if (d < v.D) ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x[q], n[q], samp, transform, cfg);
   }
   return ke0;
 }
@@ -685,11 +816,8 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
 #pragma unroll
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
   if (A.leaf) {
-    if (is_nuts) {
-      for (int d = wv; d < D; d += TPC) leaf_coord<true>(v, A, seff, (size_t)d * ldc + c, red);
-    } else {
-      for (int d = wv; d < D; d += TPC) leaf_coord<false>(v, A, seff, (size_t)d * ldc + c, red);
-    }
+    if (is_nuts) leaf_rows<true, 1>(v, A, seff, wv, D, TPC, c, red);
+    else leaf_rows<false, 1>(v, A, seff, wv, D, TPC, c, red);
   }
   block_sum<TPC, NPART>(red, lds);
   leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
@@ -706,11 +834,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
     for (int blk = wv; 4 * blk < D; blk += TPC) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * blk + q;
-        if (d < D) ke0[0] += apply_coord(v, A, step_eff, d, (size_t)d * ldc + c, &n[q], samp, P.transform, cfg);
-      }
+      ke0[0] += apply_block<false>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
     }
   }
   block_sum<TPC, 1>(ke0, lds);
@@ -761,11 +885,8 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
   const int d0 = s * W.sw, d1 = min(D, d0 + W.sw);
   if (A.leaf) {
-    if (is_nuts) {
-      for (int d = d0 + wv; d < d1; d += WIDE_WAVES) leaf_coord<true>(v, A, seff, (size_t)d * ldc + c, red);
-    } else {
-      for (int d = d0 + wv; d < d1; d += WIDE_WAVES) leaf_coord<false>(v, A, seff, (size_t)d * ldc + c, red);
-    }
+    if (is_nuts) leaf_rows<true, 2>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
+    else leaf_rows<false, 2>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
   }
   block_sum<WIDE_WAVES, NPART>(red, lds);
   if (wv == 0 && A.leaf) {
@@ -887,11 +1008,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
     for (int blk = b0 + wv; blk < b1; blk += WIDE_WAVES) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(cfg.seed, gch, it, blk, n);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * blk + q;
-        if (d < D) ke0[0] += apply_coord(v, A, step_eff, d, (size_t)d * ldc + c, &n[q], samp, W.p.transform, cfg);
-      }
+      ke0[0] += apply_block<true>(v, A, step_eff, blk, c, n, samp, W.p.transform, cfg);
     }
   }
   block_sum<WIDE_WAVES, 1>(ke0, lds);

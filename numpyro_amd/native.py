@@ -104,8 +104,9 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_nuts_step": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nmx_pe_diag_normal": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
-    "nmx_pe_stochastic_volatility": (c_int, [c_vp, c_int, _evp, c_vp]),
-    "nmx_pe_funnel": (c_int, [c_int, _evp, c_vp]),
+    "nmx_pe_stochastic_volatility": (c_int, [c_vp, c_int, _evp, c_vp, c_vp]),
+    "nmx_pe_funnel": (c_int, [c_int, _evp, c_vp, c_vp]),
+    "nmx_pe_wide_workspace_bytes": (c_size, [c_int, c_int]),
     "nmx_logreg_packed_bytes": (c_size, [c_i64, c_int]),
     "nmx_logreg_pack": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
     "nmx_logreg_workspace_bytes": (c_size, [c_i64, c_int, c_int]),

@@ -156,10 +156,16 @@ class StochasticVolatility(Potential):
 
     def _bind(self, C, ldc, device):
         self.r = _dev(self.r_in, device)
+        self.workspace = torch.empty(lib().nmx_pe_wide_workspace_bytes(self.dim, C), dtype=torch.uint8,
+                                     device=device)
 
     def evaluate(self, ev, stream):
-        check(lib().nmx_pe_stochastic_volatility(ptr(self.r), self.T, ctypes.byref(ev), stream),
-              "nmx_pe_stochastic_volatility")
+        check(lib().nmx_pe_stochastic_volatility(ptr(self.r), self.T, ctypes.byref(ev), ptr(self.workspace),
+                                                 stream), "nmx_pe_stochastic_volatility")
+
+    def bytes_per_eval(self):
+        """Algorithmic HBM bytes per chain evaluation: read z, write grad (f32)."""
+        return 2 * 4 * self.dim
 
 
 class Funnel(Potential):
@@ -169,8 +175,15 @@ class Funnel(Potential):
         self.dim = int(dim)
         self.sites = [("x", (self.dim - 1,), REAL), ("y", (), REAL)]
 
+    def _bind(self, C, ldc, device):
+        self.workspace = torch.empty(lib().nmx_pe_wide_workspace_bytes(self.dim, C), dtype=torch.uint8,
+                                     device=device)
+
     def evaluate(self, ev, stream):
-        check(lib().nmx_pe_funnel(self.dim, ctypes.byref(ev), stream), "nmx_pe_funnel")
+        check(lib().nmx_pe_funnel(self.dim, ctypes.byref(ev), ptr(self.workspace), stream), "nmx_pe_funnel")
+
+    def bytes_per_eval(self):
+        return 2 * 4 * self.dim
 
 
 class MultivariateNormal(Potential):
