@@ -202,6 +202,12 @@ int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* workspace, void* stre
 /* Workspace (per-slice partial sums) of the two kernels above for num_chains chains. */
 size_t nmx_pe_wide_workspace_bytes(int dim, int num_chains);
 
+/* Bayesian neural network (examples/bnn.py:43-74): X [N][Dx], Y [N] (D_Y = 1), H hidden
+ * units, tanh; z = (log prec_obs, w1[Dx][H], w2[H][H], w3[H]).  One workgroup per evaluated
+ * chain with weights and activations in LDS (needs 4 (Dx H + H^2 + H + N Dx + 2N + 2 N H + 256)
+ * bytes <= 160 KiB). */
+int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev, void* stream);
+
 /* Logistic regression (examples/covtype.py:66-71): coefs ~ N(0,1)^D,
  * obs ~ BernoulliLogits(X @ coefs).  X is first packed (row tiles with the label in a pad
  * column); U and dU are computed by two f32 MFMA GEMMs per 32-row tile
@@ -224,12 +230,22 @@ int nmx_logreg_num_splits(int64_t n_rows);
  * with T = tril_inv^T the whitened momentum is the reference's `eps`).  Each leapfrog then
  * costs z = mu + T w and g_w = T^T g_z, two chain-batched products:
  *   Out[i][c] = sum_k At[k][i] * In[k][c] (+ bias[i])
- * over every 64-chain tile holding a chain with phase[c] >= NMX_PH_LEAF (phase NULL: all).
+ * over every 64-chain tile holding a chain with phase[c] >= NMX_PH_LEAF (phase NULL: all);
+ * with active_count set, In/Out are packed columns and tiles c0 < *active_count run.
  * At = A^T row-major with leading dimension lda (multiple of 128, >= padded dim) and zero
- * padding in rows/columns >= dim; In/Out are [dim][ldc] chain-major; f32 MFMA. */
+ * padding in rows/columns >= dim; In/Out are [dim][ldc] chain-major; f32 MFMA.
+ * triangle: 0 dense A; 1 A upper triangular; 2 A lower triangular (all-zero K-tiles are
+ * skipped: half the MFMA work for T w and T^T g). */
 int nmx_dense_padded_dim(int dim);
 int nmx_gemm_chains(const float* At, int lda, int dim, const float* In, float* Out, const float* bias,
-                    int ldc, const int32_t* phase, int num_chains, void* stream);
+                    int triangle, int ldc, const int32_t* phase, const int32_t* active_count, int num_chains,
+                    void* stream);
+/* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
+ * (p < *count, device-side count, grid sized for ldo / ldi positions). */
+int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
+                     int ldo, void* stream);
+int nmx_unpack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
+                       int ldo, const float* pe_in, float* pe_out, void* stream);
 /* Multivariate normal, U = 0.5 (z-mu)^T P (z-mu), grad = P z - P mu (one nmx_gemm_chains
  * with At = P^T, bias = -P mu) then the per-chain quadratic form: the dense-mass test
  * targets of test/infer/test_mcmc.py:73-100 and :313-343. */

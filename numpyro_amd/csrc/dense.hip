@@ -23,20 +23,26 @@ constexpr int BK = 32;   // k per stage
 
 __global__ __launch_bounds__(256, 2) void k_gemm_chains(const float* __restrict__ At, int lda, int D,
                                                         const float* __restrict__ In, float* __restrict__ Out,
-                                                        const float* __restrict__ bias, int ldc,
-                                                        const int32_t* __restrict__ phase, int C) {
+                                                        const float* __restrict__ bias, int triangle, int ldc,
+                                                        const int32_t* __restrict__ phase,
+                                                        const int32_t* __restrict__ count, int C) {
   __shared__ __attribute__((aligned(16))) float As[2][BK * TM];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * TN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
   const int i0 = blockIdx.x * TM;
   const int c0 = blockIdx.y * TN;
-  // tile has an evaluated chain?
-  {
+  // tile has an evaluated chain?  (packed columns: the first *count positions)
+  if (count) {
+    if (c0 >= *count) return;
+  } else {
     const int c = c0 + lane;
     const bool act = c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
     if (!__any(act)) return;  // same result in every wave
   }
-  const int nk = (D + BK - 1) / BK;
+  // A upper triangular (triangle 1): out rows [i0, i0+TM) need k >= i0 only; A lower
+  // triangular (2): k < i0 + TM only.  Skipped K-tiles are exact zeros.
+  const int kt_begin = triangle == 1 ? i0 / BK : 0;
+  const int nk = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
 
   auto load_a = [&](int kt, int buf) {
     // BK rows x TM floats = 16 KiB = 16 wave-instructions of 1 KiB; 4 per wave
@@ -75,12 +81,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_chains(const float* __restrict_
     acc1[r] = 0.0f;
   }
   float4 breg[2];
-  load_a(0, 0);
-  load_b(0, breg);
+  load_a(kt_begin, 0);
+  load_b(kt_begin, breg);
   store_b(0, breg);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+  for (int kt = kt_begin; kt < nk; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
     const bool more = kt + 1 < nk;
     if (more) {
       load_a(kt + 1, buf ^ 1);
@@ -128,21 +134,70 @@ __global__ __launch_bounds__(256) void k_quad_pe(const float* __restrict__ mu, i
   if (w == 0 && c >= 0) ev.pe[c] = 0.5f * (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
 }
 
+// Column compaction for the dense products: packed[d][p] = in[d][list[p]] for p < *count.
+constexpr int PACK_ROWS = 16;
+__global__ __launch_bounds__(256) void k_pack(const float* __restrict__ in, int ldi, int D,
+                                              const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                              float* __restrict__ out, int ldo) {
+  const int p = blockIdx.y * 64 + (threadIdx.x & 63);
+  if (blockIdx.y * 64 >= *count) return;
+  if (p >= *count) return;
+  const int c = list[p];
+  const int d0 = blockIdx.x * PACK_ROWS;
+  for (int d = d0 + (threadIdx.x >> 6); d < min(D, d0 + PACK_ROWS); d += 4)
+    out[(size_t)d * ldo + p] = in[(size_t)d * ldi + c];
+}
+
+// Scatter back: out[d][list[p]] = packed[d][p]; pe_out[list[p]] = pe_packed[p].
+__global__ __launch_bounds__(256) void k_unpack(const float* __restrict__ in, int ldi, int D,
+                                                const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                                float* __restrict__ out, int ldo, const float* __restrict__ pe_in,
+                                                float* __restrict__ pe_out) {
+  const int p = blockIdx.y * 64 + (threadIdx.x & 63);
+  if (blockIdx.y * 64 >= *count) return;
+  if (p >= *count) return;
+  const int c = list[p];
+  const int d0 = blockIdx.x * PACK_ROWS;
+  for (int d = d0 + (threadIdx.x >> 6); d < min(D, d0 + PACK_ROWS); d += 4)
+    out[(size_t)d * ldo + c] = in[(size_t)d * ldi + p];
+  if (pe_in && blockIdx.x == 0 && threadIdx.x < 64) pe_out[c] = pe_in[p];
+}
+
 }  // namespace
+
+extern "C" int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count,
+                                float* out, int ldo, void* stream) {
+  if (!in || !list || !count || !out || dim <= 0 || ldo % 64 || ldi <= 0)
+    return nmx_fail(NMX_ERR_INVALID, "pack_columns: bad arguments");
+  hipLaunchKernelGGL(k_pack, dim3((dim + PACK_ROWS - 1) / PACK_ROWS, ldo / 64), dim3(256), 0, (hipStream_t)stream,
+                     in, ldi, dim, list, count, out, ldo);
+  return nmx_check_launch("k_pack");
+}
+
+extern "C" int nmx_unpack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count,
+                                  float* out, int ldo, const float* pe_in, float* pe_out, void* stream) {
+  if (!in || !list || !count || !out || dim <= 0 || ldi % 64 || ldo <= 0 || (pe_in && !pe_out))
+    return nmx_fail(NMX_ERR_INVALID, "unpack_columns: bad arguments");
+  hipLaunchKernelGGL(k_unpack, dim3((dim + PACK_ROWS - 1) / PACK_ROWS, ldi / 64), dim3(256), 0,
+                     (hipStream_t)stream, in, ldi, dim, list, count, out, ldo, pe_in, pe_out);
+  return nmx_check_launch("k_unpack");
+}
 
 extern "C" int nmx_dense_padded_dim(int D) { return (D + TM - 1) / TM * TM; }
 
 extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In, float* Out, const float* bias,
-                               int ldc, const int32_t* phase, int num_chains, void* stream) {
+                               int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
+                               int num_chains, void* stream) {
   if (!At || !In || !Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: NULL operand");
   if (D <= 0 || ldc % 64 || num_chains <= 0 || num_chains > ldc)
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains: bad sizes (D=%d ldc=%d C=%d)", D, ldc, num_chains);
   if (lda % TM || lda < nmx_dense_padded_dim(D))
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains: lda must be a multiple of %d >= padded D", TM);
   if (In == Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: In and Out must not alias");
+  if (triangle < 0 || triangle > 2) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: triangle must be 0, 1 or 2");
   dim3 grid(lda / TM, ldc / TN);
-  hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, ldc,
-                     phase, num_chains);
+  hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, triangle,
+                     ldc, phase, active_count, num_chains);
   return nmx_check_launch("k_gemm_chains");
 }
 
@@ -150,8 +205,8 @@ extern "C" int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const f
                           const nmx_eval_batch* ev, void* stream) {
   if (!ev || !ev->z || !ev->grad || !ev->pe || !mu || !neg_prec_mu)
     return nmx_fail(NMX_ERR_INVALID, "mvn: NULL operand");
-  if (int st = nmx_gemm_chains(prec_t, lda, dim, ev->z, ev->grad, neg_prec_mu, ev->ldc, ev->phase, ev->num_chains,
-                               stream))
+  if (int st = nmx_gemm_chains(prec_t, lda, dim, ev->z, ev->grad, neg_prec_mu, 0, ev->ldc, ev->phase, nullptr,
+                               ev->num_chains, stream))
     return st;
   hipLaunchKernelGGL(k_quad_pe, dim3(ev->ldc / 64), dim3(256), 0, (hipStream_t)stream, mu, dim, *ev);
   return nmx_check_launch("k_quad_pe");

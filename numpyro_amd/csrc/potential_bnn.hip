@@ -1,0 +1,258 @@
+// Bayesian neural network of examples/bnn.py:43-74 (D_X -> H -> H -> 1, tanh):
+//   w1 [Dx,H], w2 [H,H], w3 [H,1] ~ N(0,1), prec_obs ~ Gamma(3,1),
+//   Y ~ N(tanh(tanh(X w1) w2) w3, 1/sqrt(prec_obs)),
+// z = (log prec_obs, w1, w2, w3) row-major (ravel_pytree of the sorted sites).
+//
+// U and dU per chain with the hand-derived adjoint (oracle
+// BNN.pe_grad).  One workgroup (256 threads) owns one evaluated chain: its weights, both
+// activation layers and the adjoints live in LDS (N=100, H=69: 78 KB), the three
+// N x H x H products run as 4x4 register-blocked FMA loops.  The model is ~3 MFLOP per
+// chain-leapfrog -- ~3% of the dense-mass products it runs between (dense.hip), so it is
+// written for clarity and LDS residency rather than MFMA.  Blocks are mapped so that
+// consecutive list positions run on one XCD (blockIdx % 8): the strided per-chain column
+// gathers of neighbouring chains then share L2 lines.
+#include <math.h>
+
+#include "nmx_api_internal.h"
+#include "nmx_common.h"
+
+namespace {
+
+constexpr int THREADS = 256;
+
+struct BnnDims {
+  int N, Dx, H;
+  int o_w1, o_w2, o_w3;  // offsets of the sites in z
+};
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += red[w * 64 + threadIdx.x];
+    red[threadIdx.x] = s;
+  }
+  __syncthreads();
+  float t = 0.0f;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 64; ++i) t += red[i];
+    red[0] = t;
+  }
+  __syncthreads();
+  t = red[0];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, const float* __restrict__ Y, BnnDims dm,
+                                               nmx_eval_batch ev) {
+  extern __shared__ float sm[];
+  const int N = dm.N, Dx = dm.Dx, H = dm.H;
+  // XCD-aware position: blocks b, b+8, b+16, ... (one XCD) take consecutive positions
+  const int nb = gridDim.x;
+  const int b = blockIdx.x;
+  const int per = (nb + 7) / 8;
+  const int pos = (b % 8) * per + b / 8;
+  if (pos >= nb) return;
+  const int c = nmx_eval_chain(ev, pos);
+  if (c < 0) return;
+  const int ldc = ev.ldc;
+  const int t = threadIdx.x;
+
+  float* W1 = sm;                  // Dx*H
+  float* W2 = W1 + Dx * H;         // H*H
+  float* w3 = W2 + H * H;          // H
+  float* Xs = w3 + H;              // N*Dx
+  float* Ys = Xs + N * Dx;         // N
+  float* h1 = Ys + N;              // N*H   (later: ga1)
+  float* h2 = h1 + N * H;          // N*H   (later: ga2)
+  float* gy = h2 + N * H;          // N     dU/dyhat
+  float* red = gy + N;             // THREADS
+
+  const float* z = ev.z;
+  float* g = ev.grad;
+  const float u = z[c];
+  const float p = expf(u);
+  float wsq = 0.0f;
+  for (int i = t; i < Dx * H; i += THREADS) {
+    const float v = z[(size_t)(dm.o_w1 + i) * ldc + c];
+    W1[i] = v;
+    wsq += v * v;
+  }
+  for (int i = t; i < H * H; i += THREADS) {
+    const float v = z[(size_t)(dm.o_w2 + i) * ldc + c];
+    W2[i] = v;
+    wsq += v * v;
+  }
+  for (int i = t; i < H; i += THREADS) {
+    const float v = z[(size_t)(dm.o_w3 + i) * ldc + c];
+    w3[i] = v;
+    wsq += v * v;
+  }
+  for (int i = t; i < N * Dx; i += THREADS) Xs[i] = X[i];
+  for (int i = t; i < N; i += THREADS) Ys[i] = Y[i];
+  __syncthreads();
+
+  // h1 = tanh(X W1)
+  for (int e = t; e < N * H; e += THREADS) {
+    const int n = e / H, j = e % H;
+    float a = 0.0f;
+    for (int k = 0; k < Dx; ++k) a += Xs[n * Dx + k] * W1[k * H + j];
+    h1[e] = tanhf(a);
+  }
+  __syncthreads();
+
+  // h2 = tanh(h1 W2): 4x4 blocks over (n, j)
+  const int nbn = (N + 3) / 4, nbh = (H + 3) / 4;
+  for (int blk = t; blk < nbn * nbh; blk += THREADS) {
+    const int n0 = (blk / nbh) * 4, j0 = (blk % nbh) * 4;
+    float acc[4][4] = {};
+    for (int i = 0; i < H; ++i) {
+      float a[4], w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = n0 + q < N ? h1[(n0 + q) * H + i] : 0.0f;
+        w[q] = j0 + q < H ? W2[i * H + j0 + q] : 0.0f;
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+        if (n0 + x < N && j0 + y < H) h2[(n0 + x) * H + j0 + y] = tanhf(acc[x][y]);
+  }
+  __syncthreads();
+
+  // yhat = h2 w3; residual; dU/dyhat = -p (Y - yhat)
+  float esq = 0.0f;
+  for (int n = t; n < N; n += THREADS) {
+    float yh = 0.0f;
+    for (int j = 0; j < H; ++j) yh += h2[n * H + j] * w3[j];
+    const float e = Ys[n] - yh;
+    esq += e * e;
+    gy[n] = -p * e;
+  }
+  __syncthreads();
+
+  // grad w3 = w3 + h2^T gy
+  for (int j = t; j < H; j += THREADS) {
+    float s = 0.0f;
+    for (int n = 0; n < N; ++n) s += h2[n * H + j] * gy[n];
+    g[(size_t)(dm.o_w3 + j) * ldc + c] = w3[j] + s;
+  }
+  __syncthreads();
+  // ga2 = (gy w3^T) * (1 - h2^2)   (in place of h2)
+  for (int e = t; e < N * H; e += THREADS) {
+    const int n = e / H, j = e % H;
+    const float v = h2[e];
+    h2[e] = gy[n] * w3[j] * (1.0f - v * v);
+  }
+  __syncthreads();
+
+  // grad W2 = W2 + h1^T ga2: 4x4 blocks over (i, j)
+  for (int blk = t; blk < nbh * nbh; blk += THREADS) {
+    const int i0 = (blk / nbh) * 4, j0 = (blk % nbh) * 4;
+    float acc[4][4] = {};
+    for (int n = 0; n < N; ++n) {
+      float a[4], w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = i0 + q < H ? h1[n * H + i0 + q] : 0.0f;
+        w[q] = j0 + q < H ? h2[n * H + j0 + q] : 0.0f;
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+        if (i0 + x < H && j0 + y < H) {
+          const int ij = (i0 + x) * H + j0 + y;
+          g[(size_t)(dm.o_w2 + ij) * ldc + c] = W2[ij] + acc[x][y];
+        }
+  }
+  __syncthreads();
+
+  // ga1 = (ga2 W2^T) * (1 - h1^2): 4x4 blocks over (n, i), in place of h1 (a block reads
+  // h1 only at its own elements; grad W2 above finished reading h1 at the barrier)
+  for (int blk = t; blk < nbn * nbh; blk += THREADS) {
+    const int n0 = (blk / nbh) * 4, i0 = (blk % nbh) * 4;
+    float acc[4][4] = {};
+    for (int j = 0; j < H; ++j) {
+      float a[4], w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = n0 + q < N ? h2[(n0 + q) * H + j] : 0.0f;
+        w[q] = i0 + q < H ? W2[(i0 + q) * H + j] : 0.0f;
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+        if (n0 + x < N && i0 + y < H) {
+          float* hp = &h1[(n0 + x) * H + i0 + y];
+          const float hv = *hp;
+          *hp = acc[x][y] * (1.0f - hv * hv);
+        }
+  }
+  __syncthreads();
+
+  // grad W1 = W1 + X^T ga1
+  for (int e = t; e < Dx * H; e += THREADS) {
+    const int k = e / H, j = e % H;
+    float s = 0.0f;
+    for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[n * H + j];
+    g[(size_t)(dm.o_w1 + e) * ldc + c] = W1[e] + s;
+  }
+
+  const float esq_t = block_sum256(esq, red);
+  const float wsq_t = block_sum256(wsq, red);
+  if (t == 0) {
+    const float Nf = (float)N;
+    const float nw = (float)(Dx * H + H * H + H);
+    const float LOG_2PI = 1.8378770664093453f;
+    float lp = -0.5f * wsq_t - 0.5f * nw * LOG_2PI;           // N(0,1) priors
+    lp += 2.0f * u - p - 0.6931471805599453f + u;              // Gamma(3,1) at p (lgamma(3)=log 2) + log|J|
+    lp += Nf * (0.5f * u - 0.5f * LOG_2PI) - 0.5f * p * esq_t;  // Normal(yhat, p^-1/2)
+    ev.pe[c] = -lp;
+    g[c] = -(3.0f - p + 0.5f * Nf - 0.5f * p * esq_t);
+  }
+}
+
+size_t lds_bytes(int N, int Dx, int H) {
+  return sizeof(float) * ((size_t)Dx * H + (size_t)H * H + H + (size_t)N * Dx + N + 2 * (size_t)N * H + N + THREADS);
+}
+
+}  // namespace
+
+extern "C" int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev,
+                          void* stream) {
+  if (!ev || !ev->z || !ev->grad || !ev->pe || !X || !Y) return nmx_fail(NMX_ERR_INVALID, "bnn: NULL operand");
+  if (N <= 0 || Dx <= 0 || H <= 0) return nmx_fail(NMX_ERR_INVALID, "bnn: bad sizes");
+  if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
+    return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
+  const size_t lds = lds_bytes(N, Dx, H);
+  if (lds > 160 * 1024)
+    return nmx_fail(NMX_ERR_UNSUPPORTED, "bnn: N=%d, H=%d needs %zu bytes of LDS (> 160 KiB)", N, H, lds);
+  BnnDims dm{N, Dx, H, 1, 1 + Dx * H, 1 + Dx * H + H * H};
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "bnn: hipFuncSetAttribute: %s", hipGetErrorString(e));
+  }
+  hipLaunchKernelGGL(k_bnn, dim3(ev->ldc), dim3(THREADS), lds, (hipStream_t)stream, X, Y, dm, *ev);
+  return nmx_check_launch("k_bnn");
+}

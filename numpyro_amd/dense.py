@@ -32,6 +32,8 @@ from . import native
 from .native import EvalBatch, check, lib, ptr
 from .potentials import REAL, Potential
 
+DENSE, UPPER, LOWER = 0, 1, 2  # nmx_gemm_chains `triangle` (shape of A in Out = A In)
+
 
 class Whitening:
     """z = mu + T w, T T^T = M^-1.  Holds the two padded At operands of nmx_gemm_chains."""
@@ -56,6 +58,7 @@ class Whitening:
         T = torch.linalg.cholesky(imm.flip(0, 1)).flip(0, 1)
         self.inverse_mass_matrix = imm
         self.T = T
+        self._tinv = None
         self.fwd_t[:self.D, :self.D] = T.t().to(torch.float32)
         self.bwd_t[:self.D, :self.D] = T.to(torch.float32)
         if mu is not None:
@@ -65,26 +68,40 @@ class Whitening:
     def mass_matrix_sqrt_inv(self):
         return self.T.t()  # tril_inv
 
+    def tinv(self):
+        """T^-1 (upper triangular, float64), by column chunks: hipBLAS trsm refuses very large
+        right-hand sides (D = 10000 x 4096 fails to allocate its workspace)."""
+        if self._tinv is None:
+            eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
+            cols = [torch.linalg.solve_triangular(self.T, eye[:, a:a + 1024], upper=True)
+                    for a in range(0, self.D, 1024)]
+            self._tinv = torch.cat(cols, dim=1)
+        return self._tinv
+
     def mass_matrix_sqrt(self):
-        eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
-        return torch.linalg.solve_triangular(self.T.t(), eye, upper=False)
+        # mass_matrix_sqrt = tril_inv^-1 = (T^T)^-1 = (T^-1)^T
+        return self.tinv().t()
 
     def to_model(self, w, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = mu + T w[:, c] for [D, ldc] buffers."""
         ldc = w.shape[-1]
-        check(lib().nmx_gemm_chains(ptr(self.fwd_t), self.lda, self.D, ptr(w), ptr(out), ptr(self.mu), ldc,
-                                    ptr(phase), int(num_chains or ldc), stream), "nmx_gemm_chains")
+        check(lib().nmx_gemm_chains(ptr(self.fwd_t), self.lda, self.D, ptr(w), ptr(out), ptr(self.mu), UPPER, ldc,
+                                    ptr(phase), None, int(num_chains or ldc), stream), "nmx_gemm_chains")
 
     def grad_to_w(self, g, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = T^T g[:, c]."""
         ldc = g.shape[-1]
-        check(lib().nmx_gemm_chains(ptr(self.bwd_t), self.lda, self.D, ptr(g), ptr(out), None, ldc,
-                                    ptr(phase), int(num_chains or ldc), stream), "nmx_gemm_chains")
+        check(lib().nmx_gemm_chains(ptr(self.bwd_t), self.lda, self.D, ptr(g), ptr(out), None, LOWER, ldc,
+                                    ptr(phase), None, int(num_chains or ldc), stream), "nmx_gemm_chains")
 
     def to_whitened(self, z):
         """w = T^-1 (z - mu) for z [D, n] (host-side re-expression at window ends)."""
         zz = z.to(torch.float64) - self.mu.to(torch.float64)[:, None]
-        return torch.linalg.solve_triangular(self.T, zz, upper=True).to(torch.float32)
+        return (self.tinv() @ zz).to(torch.float32)
+
+    def grad_to_model(self, g_w):
+        """g_z = T^-T g_w for g_w [D, n]."""
+        return (self.tinv().t() @ g_w.to(torch.float64)).to(torch.float32)
 
 
 class WhitenedPotential(Potential):
@@ -102,28 +119,53 @@ class WhitenedPotential(Potential):
             self.whitening = Whitening(self.dim, device)
         self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
+        self.wp = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)   # packed w / g_w
+        self.pe_p = torch.zeros(ldc, dtype=torch.float32, device=device)
+        self.ident = torch.arange(ldc, dtype=torch.int32, device=device)
         self._batches = {}
 
     def _base_batch(self, ev):
+        """Model-space batch: dense (phase-selected) or, for a compacted list, the packed
+        positions [0, *active_count) through an identity list."""
         key = (ev.active_idx, ev.active_count, ev.pe, ev.phase)
         b = self._batches.get(key)
         if b is None:
-            b = EvalBatch(z=ptr(self.zb), grad=ptr(self.gb), pe=ev.pe, phase=ev.phase, active_idx=ev.active_idx,
-                          active_count=ev.active_count, num_chains=ev.num_chains, ldc=ev.ldc)
+            if ev.active_idx:
+                b = EvalBatch(z=ptr(self.zb), grad=ptr(self.gb), pe=ptr(self.pe_p), phase=None,
+                              active_idx=ptr(self.ident), active_count=ev.active_count, num_chains=ev.num_chains,
+                              ldc=ev.ldc)
+            else:
+                b = EvalBatch(z=ptr(self.zb), grad=ptr(self.gb), pe=ev.pe, phase=ev.phase, active_idx=None,
+                              active_count=None, num_chains=ev.num_chains, ldc=ev.ldc)
             self._batches[key] = b
         return b
 
     def evaluate(self, ev, stream):
         wt = self.whitening
-        C, ldc = ev.num_chains, ev.ldc
-        check(lib().nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, self.dim, ev.z, ptr(self.zb), ptr(wt.mu), ldc,
-                                    ev.phase, C, stream), "nmx_gemm_chains")
+        L = lib()
+        C, ldc, D = ev.num_chains, ev.ldc, self.dim
+        if ev.active_idx:
+            # compacted list: the products run on packed columns of the listed chains only
+            check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
+                  "nmx_pack_columns")
+            check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ptr(self.wp), ptr(self.zb), ptr(wt.mu), UPPER, ldc,
+                                    None, ev.active_count, C, stream), "nmx_gemm_chains")
+            self.base.evaluate(self._base_batch(ev), stream)
+            check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ptr(self.wp), None, LOWER, ldc,
+                                    None, ev.active_count, C, stream), "nmx_gemm_chains")
+            check(L.nmx_unpack_columns(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
+                                       ptr(self.pe_p), ev.pe, stream), "nmx_unpack_columns")
+            return
+        check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ev.z, ptr(self.zb), ptr(wt.mu), UPPER, ldc,
+                                ev.phase, None, C, stream), "nmx_gemm_chains")
         self.base.evaluate(self._base_batch(ev), stream)
-        check(lib().nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, self.dim, ptr(self.gb), ev.grad, None, ldc,
-                                    ev.phase, C, stream), "nmx_gemm_chains")
+        check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ev.grad, None, LOWER, ldc,
+                                ev.phase, None, C, stream), "nmx_gemm_chains")
 
     def flops_per_eval(self, num_chains):
-        return 4.0 * self.dim * self.dim * num_chains
+        """Algorithmic FLOPs of the two triangular products (D^2 each per chain) -- the
+        dense-matrix count 4 D^2 of SURVEY.md §8d halves because T is triangular."""
+        return 2.0 * self.dim * self.dim * num_chains
 
 
 class PooledCovariance:

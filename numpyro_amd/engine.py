@@ -397,8 +397,7 @@ class Engine:
         zb = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
         wt.to_model(self.view("z"), zb, stream=stream_ptr())
         # g_w = T^T g_z  ->  g_z = T^-T g_w
-        gz = torch.linalg.solve_triangular(wt.T.t(), g.t().to(torch.float64), upper=False)
-        return zb[:, :self.C].t().clone(), gz.t().to(torch.float32)
+        return zb[:, :self.C].t().clone(), wt.grad_to_model(g.t()).t().contiguous()
 
     def mass_state(self):
         """(inverse_mass_matrix, mass_matrix_sqrt, mass_matrix_sqrt_inv) as HMCAdaptState holds

@@ -186,6 +186,34 @@ class Funnel(Potential):
         return 2 * 4 * self.dim
 
 
+class BNN(Potential):
+    """examples/bnn.py:43-74: w1 [Dx,H], w2 [H,H], w3 [H,1] ~ N(0,1), prec_obs ~ Gamma(3,1),
+    Y ~ N(tanh(tanh(X w1) w2) w3, 1/sqrt(prec_obs)); sites in ravel_pytree (sorted) order."""
+
+    def __init__(self, X, Y, D_H, D_Y=1):
+        if D_Y != 1:
+            raise NotImplementedError("the fused BNN kernel supports D_Y = 1 (examples/bnn.py)")
+        self.X_in, self.Y_in = X, Y
+        shape = tuple(X.shape)
+        self.N, self.Dx = int(shape[0]), int(shape[1])
+        self.H = int(D_H)
+        self.dim = 1 + self.Dx * self.H + self.H * self.H + self.H
+        self.sites = [("prec_obs", (), POSITIVE), ("w1", (self.Dx, self.H), REAL), ("w2", (self.H, self.H), REAL),
+                      ("w3", (self.H, 1), REAL)]
+
+    def _bind(self, C, ldc, device):
+        self.X = _dev(self.X_in, device)
+        self.Y = _dev(self.Y_in, device).reshape(-1)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_bnn(ptr(self.X), ptr(self.Y), self.N, self.Dx, self.H, ctypes.byref(ev), stream),
+              "nmx_pe_bnn")
+
+    def flops_per_eval(self, num_chains):
+        """Forward + adjoint: ~6 N H^2 + 6 N Dx H FLOPs per chain."""
+        return (6.0 * self.N * self.H * self.H + 6.0 * self.N * self.Dx * self.H) * num_chains
+
+
 class MultivariateNormal(Potential):
     """U = 0.5 (z - mu)^T P (z - mu): the MultivariateNormal targets of
     test/infer/test_mcmc.py:73-100 (`test_correlated_mvn`) and :313-343 (`test_dense_mass`).
@@ -254,6 +282,8 @@ stochastic_volatility = FusedModel(
     "examples/stochastic_volatility.py:57-65 model(returns)")
 
 funnel = FusedModel("funnel", lambda dim=10: Funnel(dim), "examples/funnel.py:44-46 model(dim)")
+
+bnn = FusedModel("bnn", lambda X, Y, D_H, D_Y=1: BNN(X, Y, D_H, D_Y), "examples/bnn.py:43-74 model(X, Y, D_H)")
 
 multivariate_normal = FusedModel(
     "multivariate_normal",

@@ -28,30 +28,35 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def bench_gemm(D, C, reps=10):
+def bench_gemm(D, C, reps=10, tri=0):
     dev = torch.device("cuda:0")
     lib = native.lib()
     lda = lib.nmx_dense_padded_dim(D)
     ldc = (C + 63) // 64 * 64
+    A = torch.randn(D, D, device=dev)
+    A = {0: A, 1: torch.triu(A), 2: torch.tril(A)}[tri]
     At = torch.zeros(lda, lda, device=dev)
-    At[:D, :D] = torch.randn(D, D, device=dev)
+    At[:D, :D] = A.t()
     x = torch.randn(D, ldc, device=dev)
     y = torch.empty(D, ldc, device=dev)
     s = native.stream_ptr()
     for _ in range(2):
-        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, ldc, None, C, s))
+        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
+                                         None, C, s))
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
-        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, ldc, None, C, s))
+        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
+                                         None, C, s))
     b.record()
     b.synchronize()
     ms = a.elapsed_time(b) / reps
-    tf = 2.0 * D * D * C / (ms * 1e-3) / 1e12
+    tf = (2.0 if tri == 0 else 1.0) * D * D * C / (ms * 1e-3) / 1e12  # triangular: D^2 C useful
     ref = (At[:D, :D].t().double() @ x[:, :8].double())
     err = float((y[:, :8].double() - ref).abs().max() / ref.abs().max())
-    print(json.dumps({"kernel": "k_gemm_chains", "D": D, "C": C, "ms": round(ms, 4), "tflops": round(tf, 2),
-                      "frac": round(tf / PEAK_F32_TFLOPS, 3), "max_rel_err": err}), flush=True)
+    print(json.dumps({"kernel": "k_gemm_chains", "triangle": tri, "D": D, "C": C, "ms": round(ms, 4),
+                      "useful_tflops": round(tf, 2), "frac": round(tf / PEAK_F32_TFLOPS, 3), "max_rel_err": err}),
+          flush=True)
 
 
 class Timed:
@@ -65,7 +70,7 @@ class Timed:
     def __call__(self, ev, s):
         if not self.on:
             return self.orig(ev, s)
-        st = torch.cuda.ExternalStream(s)
+        st = torch.cuda.current_stream()  # the stream `s` belongs to (native.stream_ptr())
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
         self.orig(ev, s)
@@ -126,18 +131,28 @@ def main():
         D = int(a.rest[0]) if a.rest else 10000
         C = int(a.rest[1]) if len(a.rest) > 1 else 4096
         bench_gemm(D, C)
+        bench_gemm(D, C, tri=1)
+        bench_gemm(D, C, tri=2)
     elif a.what == "funnel":
         D = a.dim
-        # dense: two products z = T w, g = T^T g_z (2 D^2 FLOP each as executed, full T)
+        # dense: two triangular products z = T w, g = T^T g_z (D^2 FLOP each per chain)
         run_model("funnel", P.funnel, (D,), a.chains or 4096, a.warmup, a.steps,
-                  flops_per_leapfrog=4.0 * D * D if a.dense else None,
-                  bytes_per_leapfrog=None if a.dense else 3 * D * 4,
+                  flops_per_leapfrog=2.0 * D * D if a.dense else None,
+                  bytes_per_leapfrog=None if a.dense else 2 * D * 4,
                   dense_mass=bool(a.dense), max_tree_depth=a.max_tree_depth)
     elif a.what == "sv":
         r = datasets.sp500_synthetic()
         D = r.size + 2
         run_model("stochastic_volatility", P.stochastic_volatility, (r,), a.chains or 1024, a.warmup, a.steps,
                   bytes_per_leapfrog=2 * D * 4, max_tree_depth=a.max_tree_depth)
+    elif a.what == "bnn":
+        X, Y = datasets.bnn_data(N=100, D_X=3)
+        H = 69
+        D = 1 + 3 * H + H * H + H
+        model_flops = 6.0 * 100 * H * H + 6.0 * 100 * 3 * H
+        run_model("bnn", P.bnn, (X, Y, H), a.chains or 2048, a.warmup, a.steps,
+                  flops_per_leapfrog=(2.0 * D * D if a.dense else 0.0) + model_flops,
+                  dense_mass=bool(a.dense), max_tree_depth=a.max_tree_depth)
     elif a.what == "covtype":
         X, y = datasets.covtype_synthetic(seed=0)
         dev = torch.device("cuda:0")

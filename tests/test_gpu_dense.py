@@ -43,13 +43,15 @@ def _eval(pot, Z, device, phase=None, bind=True):
     return pe[:C].cpu().numpy().astype(np.float64), g[:, :C].cpu().numpy().T.astype(np.float64)
 
 
+@pytest.mark.parametrize("tri", [0, 1, 2])
 @pytest.mark.parametrize("D,C", [(3, 64), (55, 200), (130, 130), (300, 256), (1000, 70)])
-def test_gemm_chains_matches_fp64(device, D, C):
+def test_gemm_chains_matches_fp64(device, D, C, tri):
     rs = np.random.RandomState(D)
     lib = native.lib()
     lda = lib.nmx_dense_padded_dim(D)
     ldc = (C + 63) // 64 * 64
     A = rs.randn(D, D)
+    A = {0: A, 1: np.triu(A), 2: np.tril(A)}[tri]
     At = np.zeros((lda, lda), np.float32)
     At[:D, :D] = A.T
     In = rs.randn(D, ldc).astype(np.float32)
@@ -62,7 +64,7 @@ def test_gemm_chains_matches_fp64(device, D, C):
     dph = torch.from_numpy(phase).to(device)
     out = torch.full((D, ldc), float("nan"), device=device)
     native.check(lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(out), native.ptr(db),
-                                     ldc, native.ptr(dph), C, native.stream_ptr()))
+                                     tri, ldc, native.ptr(dph), None, C, native.stream_ptr()))
     torch.cuda.synchronize()
     o = out.cpu().numpy().astype(np.float64)
     A32 = At[:D, :D].T.astype(np.float64)
@@ -76,10 +78,12 @@ def test_gemm_chains_matches_fp64(device, D, C):
         else:
             assert np.all(np.isnan(o[:, cols]))
     # error paths
-    assert lib.nmx_gemm_chains(native.ptr(dAt), lda - 1, D, native.ptr(dIn), native.ptr(out), None, ldc, None, C,
-                               None) != 0
-    assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(dIn), None, ldc, None, C,
-                               None) != 0
+    assert lib.nmx_gemm_chains(native.ptr(dAt), lda - 1, D, native.ptr(dIn), native.ptr(out), None, 0, ldc, None,
+                               None, C, None) != 0
+    assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(dIn), None, 0, ldc, None, None,
+                               C, None) != 0
+    assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(out), None, 3, ldc, None, None,
+                               C, None) != 0
 
 
 def _corr_cov(D, seed=0):
@@ -244,3 +248,42 @@ def test_whitening_roundtrip(device):
     wt.to_model(wpad, zb, stream=native.stream_ptr())
     torch.cuda.synchronize()
     np.testing.assert_allclose(zb.cpu().numpy(), z.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_whitened_packed_list_matches_dense_batch(device):
+    """The compacted-list path (pack -> products on packed columns -> unpack) gives bitwise
+    the dense-batch results for the listed chains and leaves the others untouched."""
+    D, C = 150, 200
+    ldc = 256
+    cov = _corr_cov(D, 8) + 0.1 * np.eye(D)
+    wp = WhitenedPotential(P.MultivariateNormal(np.zeros(D), cov))
+    wp.bind(C, ldc, device)
+    imm = _corr_cov(D, 9) + 0.3 * np.eye(D)
+    wp.whitening.set(torch.from_numpy(imm), torch.from_numpy(np.linspace(-1, 1, D)))
+    rs = np.random.RandomState(5)
+    W = torch.zeros(D, ldc, device=device)
+    W[:, :C] = torch.from_numpy(rs.randn(D, C).astype(np.float32)).to(device)
+    s = native.stream_ptr()
+
+    def run(active_idx=None, count=None):
+        g = torch.full((D, ldc), float("nan"), device=device)
+        pe = torch.full((ldc,), float("nan"), device=device)
+        ph = torch.zeros(ldc, dtype=torch.int32, device=device)
+        ph[:C] = native.PH_LEAF
+        ev = native.EvalBatch(z=native.ptr(W), grad=native.ptr(g), pe=native.ptr(pe), phase=native.ptr(ph),
+                              active_idx=native.ptr(active_idx), active_count=native.ptr(count), num_chains=C,
+                              ldc=ldc)
+        wp.evaluate(ev, s)
+        torch.cuda.synchronize()
+        return pe.cpu().numpy(), g.cpu().numpy()
+
+    pe_d, g_d = run()
+    chosen = rs.permutation(C)[:77].astype(np.int32)
+    idx = torch.zeros(ldc, dtype=torch.int32, device=device)
+    idx[:77] = torch.from_numpy(chosen).to(device)
+    cnt = torch.tensor([77], dtype=torch.int32, device=device)
+    pe_l, g_l = run(idx, cnt)
+    np.testing.assert_array_equal(pe_l[chosen], pe_d[chosen])
+    np.testing.assert_array_equal(g_l[:, chosen], g_d[:, chosen])
+    others = np.setdiff1d(np.arange(ldc), chosen)
+    assert np.all(np.isnan(pe_l[others])) and np.all(np.isnan(g_l[:, others]))

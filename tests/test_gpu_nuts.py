@@ -278,3 +278,21 @@ def test_funnel_diag_runs(device):
     mcmc.run(0, 10, extra_fields=("diverging",))
     y = mcmc.get_samples()["y"].cpu().numpy()
     assert abs(y.mean()) < 1.5 and 1.5 < y.std() < 4.0  # y ~ N(0, 3) (centred funnel is hard)
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_bnn_fits_data(device, dense):
+    """examples/bnn.py (small H): the posterior-mean network fits the training data and
+    prec_obs is of the order of the noise level (Y is standardized, sigma_obs 0.05 before)."""
+    X, Y = datasets.bnn_data(N=60, D_X=3)
+    H = 6
+    mcmc = MCMC(NUTS(P.bnn, dense_mass=dense), num_warmup=300, num_samples=100, num_chains=64)
+    mcmc.run(0, X, Y, H)
+    s = {k: v.cpu().numpy().astype(np.float64) for k, v in mcmc.get_samples().items()}
+    assert all(np.isfinite(v).all() for v in s.values())
+    h1 = np.tanh(np.einsum("nd,sdh->snh", X.astype(np.float64), s["w1"]))
+    h2 = np.tanh(np.einsum("snh,shk->snk", h1, s["w2"]))
+    yhat = np.einsum("snk,sko->sno", h2, s["w3"])[..., 0].mean(0)
+    r2 = 1 - ((Y[:, 0] - yhat) ** 2).mean() / Y[:, 0].var()
+    assert r2 > 0.8, r2
+    assert np.median(s["prec_obs"]) > 5.0

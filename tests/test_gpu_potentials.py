@@ -203,3 +203,37 @@ def test_funnel_matches_oracle(device, dim):
         pr, gr = ref.pe_grad(Z[c].astype(np.float64))
         np.testing.assert_allclose(pe[c], pr, rtol=2e-5)
         np.testing.assert_allclose(g[c], gr, rtol=1e-4, atol=1e-3 * max(1.0, np.abs(gr).max() * 1e-2))
+
+
+@pytest.mark.parametrize("N,H", [(100, 69), (50, 5), (37, 16)])
+def test_bnn_matches_oracle(device, N, H):
+    """examples/bnn.py model (D_X = 3, D_Y = 1) at the BASELINE width H = 69 (D = 5038) and
+    small/ragged shapes.  fp32 vs float64: |dU| <= 1e-4 |U| + 1e-2; grad to 1e-3 of scale."""
+    from numpyro_amd.potentials import BNN
+
+    X, Y = datasets.bnn_data(N=N, D_X=3)
+    ref = OP.BNN(X.astype(np.float64), Y.astype(np.float64), H)
+    rs = np.random.RandomState(H)
+    C = 130
+    Z = (0.5 * rs.randn(C, ref.dim)).astype(np.float32)
+    Z[:, 0] = rs.uniform(-1.0, 2.0, C)
+    pe, g = _eval(BNN(X, Y, H), Z, device)
+    for c in range(C):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c], pr, rtol=1e-4, atol=1e-2)
+        scale = np.abs(gr).max()
+        np.testing.assert_allclose(g[c], gr, rtol=1e-3, atol=1e-3 * scale)
+
+
+def test_bnn_skips_inactive_and_list(device):
+    """Only listed/LEAF chains are evaluated (grad rows of other chains stay NaN)."""
+    from numpyro_amd.potentials import BNN
+
+    X, Y = datasets.bnn_data(N=30, D_X=3)
+    pot = BNN(X, Y, 8)
+    C = 70
+    Z = np.random.RandomState(0).randn(C, pot.dim).astype(np.float32) * 0.3
+    phase = np.zeros(C, np.int32)
+    phase[::3] = 3
+    pe, g = _eval(pot, Z, device, phase=phase)
+    assert np.all(np.isnan(pe[phase == 0])) and np.all(np.isfinite(pe[phase == 3]))
