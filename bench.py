@@ -128,6 +128,18 @@ def main():
     t1 = time.perf_counter()
     pot.evaluate = orig_eval
     elapsed = t1 - t0
+    # end-of-run exchange: cross-chain R-hat / ESS by all_reduce of per-chain
+    # statistics and the sample gather (RCCL under torch.distributed); reported, not in `value`
+    from numpyro_amd import shard
+
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    site = mcmc.get_samples(group_by_chain=True)["coefs"]
+    rhat = shard.split_gelman_rubin(site) if site.shape[1] >= 4 else None
+    ess = shard.effective_sample_size(site)
+    gathered = shard.gather_chains(site)
+    torch.cuda.synchronize()
+    end_of_run_ms = (time.perf_counter() - te0) * 1e3
     num_steps = mcmc.get_extra_fields()["num_steps"].to(torch.float64).sum()
     launches = mcmc.last_run_stats["launches"]
     pot_ms = sum(a.elapsed_time(b) for a, b in evs)
@@ -178,6 +190,10 @@ def main():
                          "unit": "TFLOP/s", "frac": achieved / MI355X_FP32_MFMA_PEAK_TFLOPS,
                          "traffic": traffic},
             "cpu_baseline": None,
+            "end_of_run": {"ms": end_of_run_ms, "gathered_chains": int(gathered.shape[0]),
+                           "max_split_rhat": float(rhat.max()) if rhat is not None else None,
+                           "min_ess": float(ess.min()),
+                           "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(X, y, args.cpu_seconds)

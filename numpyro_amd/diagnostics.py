@@ -10,7 +10,7 @@ from itertools import product
 import numpy as np
 
 __all__ = ["autocorrelation", "autocovariance", "effective_sample_size", "gelman_rubin", "hpdi",
-           "split_gelman_rubin", "summary", "print_summary"]
+           "split_gelman_rubin", "summary", "print_summary", "print_summary_table"]
 
 
 def _np(x):
@@ -135,10 +135,15 @@ def print_summary(samples, prob=0.90, group_by_chain=True):
         samples = {"Param:0": samples}
     if not group_by_chain:
         samples = {k: _np(v)[None, ...] for k, v in samples.items()}
-    table = summary(samples, prob, group_by_chain=True)
+    print_summary_table(summary(samples, prob, group_by_chain=True), prob)
+
+
+def print_summary_table(table, prob=0.90):
+    """Print a {site: OrderedDict(stat -> array)} table as numpyro's print_summary does."""
     if not table:
         return
-    width = max(max(len(k) + 2 + 3 * (_np(v).ndim - 2) for k, v in samples.items()), 10)
+    table = {k: OrderedDict((s, _np(v)) for s, v in st.items()) for k, st in table.items()}
+    width = max(max(len(k) + 2 + 3 * st["mean"].ndim for k, st in table.items()), 10)
     name_fmt = "{:>" + str(width) + "}"
     cols = [""] + list(next(iter(table.values())).keys())
     print()
@@ -147,9 +152,9 @@ def print_summary(samples, prob=0.90, group_by_chain=True):
     for name, stats in table.items():
         shape = stats["mean"].shape
         if len(shape) == 0:
-            print(row_fmt.format(name, *stats.values()))
+            print(row_fmt.format(name, *[float(v) for v in stats.values()]))
         else:
             for idx in product(*map(range, shape)):
                 label = name + "[{}]".format(",".join(map(str, idx)))
-                print(row_fmt.format(label, *[v[idx] for v in stats.values()]))
+                print(row_fmt.format(label, *[float(v[idx]) for v in stats.values()]))
     print()

@@ -7,27 +7,22 @@ chain's trajectory is a function of (key, global chain id) only, so ``chain_meth
 "parallel", "sequential" and "vectorized" give the same per-chain results (the reference
 guarantees the same up to its stream, test/infer/test_mcmc.py:553-592).  Under
 ``torch.distributed`` each rank owns a contiguous shard of the chains
-(``numpyro_amd.parallel``-free: see ``shard_chains``).
+(``numpyro_amd.shard``): no collective while sampling; ``print_summary`` and
+``gather_samples`` reduce / gather across ranks at the end (RCCL on the GPU box).
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
-from .. import diagnostics, native
+from .. import diagnostics, native, shard
 from ..random import key_to_seed
 from .hmc import HMCAdaptState, HMCState
 
 _FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
 
 
-def shard_chains(num_chains, rank, world_size):
-    """Contiguous chain shard [lo, hi) of `rank`."""
-    per = num_chains // world_size
-    rem = num_chains % world_size
-    lo = rank * per + min(rank, rem)
-    hi = lo + per + (1 if rank < rem else 0)
-    return lo, hi
+from ..shard import shard_chains  # noqa: E402  (re-exported: contiguous chain shard per rank)
 
 
 class MCMC:
@@ -221,12 +216,32 @@ class MCMC:
             out["adapt_state.step_size" if f == "step_size" else f] = v
         return out
 
+    def gather_samples(self, group_by_chain=False):
+        """get_samples over the chains of every rank (all_gather; identical to get_samples
+        with one process)."""
+        out = {k: shard.gather_chains(v) for k, v in self._site_arrays(True).items()}
+        if not group_by_chain:
+            out = {k: v.reshape(v.shape[0] * v.shape[1], *v.shape[2:]) for k, v in out.items()}
+        return out
+
     def print_summary(self, prob=0.9, exclude_deterministic=True):
-        sites = {k: v.detach().cpu().numpy() for k, v in self._site_arrays(True).items()}
-        diagnostics.print_summary(sites, prob=prob)
+        """numpyro/infer/mcmc.py:710-738.  Under torch.distributed the table covers every
+        rank's chains (moments and diagnostics by all_reduce, quantiles from the gathered
+        draws) and rank 0 prints it."""
+        rank, world = shard.dist_info()
+        if world == 1:
+            sites = {k: v.detach().cpu().numpy() for k, v in self._site_arrays(True).items()}
+            diagnostics.print_summary(sites, prob=prob)
+        else:
+            stats = shard.summary(self._site_arrays(True), prob=prob)
+            if rank == 0:
+                diagnostics.print_summary_table(stats, prob)
         ef = self.get_extra_fields()
         if "diverging" in ef:
-            print("Number of divergences: {}".format(int(ef["diverging"].sum())))
+            n = torch.tensor([float(ef["diverging"].sum())], dtype=torch.float64, device=ef["diverging"].device)
+            n = shard._all_reduce(n) if world > 1 else n
+            if rank == 0:
+                print("Number of divergences: {}".format(int(n.item())))
 
     def transfer_states_to_host(self):
         self._samples = self._samples.cpu()

@@ -1,0 +1,163 @@
+"""Chains across GPUs: one process per GPU, each owning a contiguous block of
+global chain ids; no collective during sampling.  At the end of a run the only exchanges are
+
+* cross-chain diagnostics -- split Gelman-Rubin (numpyro/diagnostics.py:64-80) and the
+  Geyer initial-monotone ESS (:101-203) -- computed from per-chain sufficient statistics
+  that are summed over ranks with one all_reduce each (O(draws x D) bytes, independent of
+  the number of chains), and
+* the sample gather (all_gather of [C_local, S, ...] blocks) when a caller wants every
+  chain's draws on every rank (summary quantiles, HPDI).
+
+`torch.distributed` with backend "nccl" is RCCL over xGMI on the GPU box; the same code
+runs on "gloo" with CPU tensors (tests).  With one process every function reduces to the
+single-process result (checked against numpyro_amd.diagnostics).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+
+def shard_chains(num_chains, rank, world_size):
+    """Contiguous chain shard [lo, hi) of `rank`."""
+    per = num_chains // world_size
+    rem = num_chains % world_size
+    lo = rank * per + min(rank, rem)
+    hi = lo + per + (1 if rank < rem else 0)
+    return lo, hi
+
+
+def dist_info():
+    d = torch.distributed
+    if d.is_available() and d.is_initialized():
+        return d.get_rank(), d.get_world_size()
+    return 0, 1
+
+
+def _all_reduce(t):
+    if dist_info()[1] > 1:
+        torch.distributed.all_reduce(t)
+    return t
+
+
+def _next_fast_len(n):
+    if n <= 2:
+        return n
+    while True:
+        m = n
+        for p in (2, 3, 5):
+            while m % p == 0:
+                m //= p
+        if m == 1:
+            return n
+        n += 1
+
+
+def _autocovariance(x):
+    """Biased autocovariance along dim 1 of x [C, N, ...] (float64), FFT based
+    (numpyro/diagnostics.py:101-147)."""
+    n = x.shape[1]
+    m2 = 2 * _next_fast_len(n)
+    y = (x - x.mean(dim=1, keepdim=True)).movedim(1, -1)
+    f = torch.fft.rfft(y, n=m2, dim=-1)
+    ac = torch.fft.irfft(f * f.conj(), n=m2, dim=-1)[..., :n] / n
+    return ac.movedim(-1, 1)
+
+
+def split_gelman_rubin(x):
+    """Split R-hat over all ranks' chains; x [C_local, N, ...] on this rank."""
+    x = torch.as_tensor(x).to(torch.float64)
+    half = x.shape[1] // 2
+    xs = torch.cat([x[:, :half], x[:, -half:]], dim=0)
+    m = xs.mean(dim=1)
+    s2 = xs.var(dim=1, unbiased=True)
+    k = torch.full_like(m[:1], float(xs.shape[0]))
+    stats = _all_reduce(torch.cat([k, m.sum(0, keepdim=True), (m * m).sum(0, keepdim=True),
+                                   s2.sum(0, keepdim=True)], dim=0))
+    K, sm, smm, ss2 = stats[0], stats[1], stats[2], stats[3]
+    w = ss2 / K
+    var_m = (smm - sm * sm / K) / (K - 1)
+    est = w * (half - 1) / half + var_m
+    return torch.sqrt(est / w)
+
+
+def effective_sample_size(x):
+    """ESS over all ranks' chains (numpyro/diagnostics.py:150-203); x [C_local, N, ...]."""
+    x = torch.as_tensor(x).to(torch.float64)
+    N = x.shape[1]
+    gamma = _autocovariance(x)  # [C, N, ...]
+    mean_c = x.mean(dim=1)
+    var_c = x.var(dim=1, unbiased=True)
+    k = torch.full_like(mean_c[:1], float(x.shape[0]))
+    head = torch.cat([k, mean_c.sum(0, keepdim=True), (mean_c * mean_c).sum(0, keepdim=True),
+                      var_c.sum(0, keepdim=True)], dim=0)
+    stats = _all_reduce(torch.cat([head, gamma.sum(0)], dim=0))
+    C, sm, smm, svar = stats[0], stats[1], stats[2], stats[3]
+    gamma_mean = stats[4:] / C
+    w = svar / C
+    est = w * (N - 1) / N
+    if float(C.flatten()[0]) > 1:
+        est = est + (smm - sm * sm / C) / (C - 1)
+    else:
+        w = est
+    rho = 1.0 - (w - gamma_mean) / est
+    rho[0] = 1.0
+    pairs = rho[:-1:2] + rho[1::2]
+    tail = torch.clamp(pairs[1:], min=0.0)
+    mono = torch.cat([pairs[:1], torch.cummin(tail, dim=0).values], dim=0) if tail.shape[0] else pairs[:1]
+    tau = -1.0 + 2.0 * mono.sum(dim=0)
+    return C * N / tau
+
+
+def gather_chains(x):
+    """all_gather of per-rank chain blocks x [C_local, ...] -> [C_total, ...] on every rank
+    (uneven shards are padded to the largest and trimmed)."""
+    rank, world = dist_info()
+    x = torch.as_tensor(x)
+    if world == 1:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    torch.distributed.all_gather(ns, n)
+    ns = [int(v.item()) for v in ns]
+    mx = max(ns)
+    pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[:x.shape[0]] = x
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    torch.distributed.all_gather(parts, pad.contiguous())
+    return torch.cat([p[:k] for p, k in zip(parts, ns)], dim=0)
+
+
+def summary(samples, prob=0.90, quantiles=True):
+    """Per-site mean / std / median / HPDI / n_eff / r_hat over every rank's chains
+    (numpyro/diagnostics.py:234-294).  samples: {site: [C_local, S, ...]}.  Moments and
+    diagnostics use reductions only; median and HPDI gather the draws (the end-of-run
+    sample gather) when `quantiles`."""
+    out = OrderedDict()
+    for name, v in samples.items():
+        x = torch.as_tensor(v).to(torch.float64)
+        C, S = x.shape[:2]
+        stats = _all_reduce(torch.cat([torch.full_like(x[0, :1], float(C * S)),
+                                       x.sum(dim=(0, 1)).unsqueeze(0),
+                                       (x * x).sum(dim=(0, 1)).unsqueeze(0)], dim=0))
+        n, s1, s2 = stats[0], stats[1], stats[2]
+        mean = s1 / n
+        std = torch.sqrt(torch.clamp((s2 - n * mean * mean) / (n - 1), min=0.0))
+        site = OrderedDict(mean=mean, std=std)
+        if quantiles:
+            flat = gather_chains(x).reshape(-1, *x.shape[2:]).cpu().numpy()
+            site["median"] = torch.as_tensor(np.median(flat, axis=0))
+            srt = np.sort(flat, axis=0)
+            m = srt.shape[0]
+            w = int(np.floor(prob * m))
+            lo = srt[:m - w]
+            hi = srt[w:]
+            i = np.argmin(hi - lo, axis=0)
+            site[f"{50 * (1 - prob):.1f}%"] = torch.as_tensor(np.take_along_axis(lo, i[None], 0)[0])
+            site[f"{50 * (1 + prob):.1f}%"] = torch.as_tensor(np.take_along_axis(hi, i[None], 0)[0])
+        site["n_eff"] = effective_sample_size(x)
+        site["r_hat"] = split_gelman_rubin(x) if S >= 4 else torch.full_like(mean, float("nan"))
+        out[name] = site
+    return out

@@ -1,0 +1,97 @@
+"""Multi-GPU end-of-run exchange (numpyro_amd/shard.py) on CPU: single-process parity with
+the host diagnostics (numpy restatement of numpyro/diagnostics.py), and world_size-2 gloo
+runs (uneven chain shards) that must reproduce the single-process values -- the same code
+path RCCL runs on the GPU box."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from numpyro_amd import diagnostics, shard
+from numpyro_amd.dense import PooledCovariance
+
+
+def _ar1(C, N, D, seed=0, phi=0.7):
+    rs = np.random.RandomState(seed)
+    x = np.zeros((C, N, D))
+    x[:, 0] = rs.randn(C, D)
+    for t in range(1, N):
+        x[:, t] = phi * x[:, t - 1] + rs.randn(C, D)
+    return x + rs.randn(C, 1, D) * 0.1
+
+
+def test_single_process_matches_host_diagnostics():
+    x = _ar1(6, 200, 3)
+    np.testing.assert_allclose(shard.split_gelman_rubin(torch.from_numpy(x)).numpy(),
+                               diagnostics.split_gelman_rubin(x), rtol=1e-10)
+    np.testing.assert_allclose(shard.effective_sample_size(torch.from_numpy(x)).numpy(),
+                               diagnostics.effective_sample_size(x), rtol=1e-8)
+    s = shard.summary({"a": torch.from_numpy(x)})["a"]
+    ref = diagnostics.summary({"a": x})["a"]
+    for k in ("mean", "std", "median", "5.0%", "95.0%", "n_eff", "r_hat"):
+        np.testing.assert_allclose(np.asarray(s[k]), np.asarray(ref[k]), rtol=1e-8, err_msg=k)
+
+
+def test_shard_chains_partition():
+    for C in (1, 7, 4096):
+        for w in (1, 2, 3, 8):
+            parts = [shard.shard_chains(C, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == C
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def _worker(rank, world, port, path, x, samples_z):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard.shard_chains(x.shape[0], rank, world)
+        xl = torch.from_numpy(x[lo:hi])
+        out = {
+            "rhat": shard.split_gelman_rubin(xl).numpy(),
+            "ess": shard.effective_sample_size(xl).numpy(),
+            "gather": shard.gather_chains(xl).numpy(),
+        }
+        s = shard.summary({"a": xl})["a"]
+        out.update({f"sum_{k}": np.asarray(v) for k, v in s.items()})
+        # pooled dense-mass covariance over ranks (dense.PooledCovariance.all_reduce)
+        lo2, hi2 = shard.shard_chains(samples_z.shape[1], rank, world)
+        pool = PooledCovariance(samples_z.shape[0], "cpu", torch.zeros(samples_z.shape[0]))
+        pool.add(torch.from_numpy(samples_z[:, lo2:hi2]))
+        pool.all_reduce()
+        cov, mean = pool.finalize(regularize=True)
+        out["cov"], out["mean"], out["n"] = cov.numpy(), mean.numpy(), pool.n
+        if rank == 0:
+            np.savez(path, **out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_reproduce_single_process():
+    x = _ar1(7, 120, 2, seed=3)  # 7 chains: uneven 4 / 3 shards
+    zs = np.random.RandomState(1).randn(5, 301)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "out.npz")
+        port = 29500 + (os.getpid() % 1000)
+        mp.spawn(_worker, args=(2, port, path, x, zs), nprocs=2, join=True)
+        r = np.load(path)
+        xt = torch.from_numpy(x)
+        np.testing.assert_allclose(r["rhat"], shard.split_gelman_rubin(xt).numpy(), rtol=1e-10)
+        np.testing.assert_allclose(r["ess"], shard.effective_sample_size(xt).numpy(), rtol=1e-10)
+        np.testing.assert_array_equal(r["gather"], x)
+        ref = shard.summary({"a": xt})["a"]
+        for k, v in ref.items():
+            np.testing.assert_allclose(r[f"sum_{k}"], np.asarray(v), rtol=1e-10, err_msg=k)
+        pool = PooledCovariance(5, "cpu", torch.zeros(5))
+        pool.add(torch.from_numpy(zs))
+        cov, mean = pool.finalize(regularize=True)
+        assert int(r["n"]) == 301
+        np.testing.assert_allclose(r["cov"], cov.numpy(), rtol=1e-10)
+        np.testing.assert_allclose(r["mean"], mean.numpy(), rtol=1e-10)
+        n = 301
+        ref_cov = np.cov(zs) * n / (n + 5.0) + 1e-3 * 5.0 / (n + 5.0) * np.eye(5)
+        np.testing.assert_allclose(r["cov"], ref_cov, rtol=1e-9)
