@@ -2,7 +2,8 @@
 regression (BASELINE.json metric), one process per GPU.
 
 A "step" is one MCMC transition of every chain (one NUTS tree each).  Protocol
-(notebooks/source/logistic_regression.ipynb:202-210): `--warmup` adaptation transitions
+(notebooks/source/logistic_regression.ipynb:202-210, NUTS cell: num_warmup=50,
+num_samples=50 -- the defaults here): `--warmup` adaptation transitions
 untimed (mcmc.warmup), then exactly `--steps` sampling transitions timed (mcmc.run),
 bracketed by barrier + synchronize on every rank; value = sum(num_steps) over all chains
 and ranks / max-over-ranks wall time (useful leapfrogs, inputs resident in HBM).
@@ -27,8 +28,10 @@ MI355X_HBM_PEAK_GBS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10, help="timed sampling transitions")
-    p.add_argument("--warmup", type=int, default=30, help="untimed warmup/adaptation transitions")
+    # the reference's NUTS timing protocol: num_warmup=50, num_samples=50
+    # (notebooks/source/logistic_regression.ipynb cell 12)
+    p.add_argument("--steps", type=int, default=50, help="timed sampling transitions")
+    p.add_argument("--warmup", type=int, default=50, help="untimed warmup/adaptation transitions")
     p.add_argument("--chains", type=int, default=4096, help="total chains over all GPUs")
     p.add_argument("--rows", type=int, default=581012)
     p.add_argument("--seed", type=int, default=0)

@@ -245,7 +245,7 @@ constexpr int RL_WAVES = 4;             // row lanes per workgroup
 constexpr int RL_ROWS = 32 * RL_WAVES;  // rows per stage (= PACK)
 static_assert(RL_ROWS == PACK, "row-lane stage must equal the packing granularity");
 
-template <int KS, int NBUF>
+template <int KS, int NBUF, bool PRIO>
 __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes(const float* __restrict__ Xp, int64_t n_rows,
                                                                       int nstages, int D, int S, int Gt,
                                                                       nmx_eval_batch ev, float* __restrict__ gpart,
@@ -316,16 +316,143 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes(const floa
     const int64_t rb = (int64_t)t * RL_ROWS + w * 32;
     f32x16 a0;
     float lin = 0.0f, lg2 = 0.0f;
+    // PRIO: waves in their MFMA chains get issue priority over waves in the VALU epilogue,
+    // so co-resident waves drift out of phase and the epilogues run under other waves' MFMAs
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     gemm1<KS>(xt, zb, l31, h, a0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (rb + 32 <= n_rows) epilogue<KS, false>(xt, h, rb, n_rows, a0, lin, lg2);
     else epilogue<KS, true>(xt, h, rb, n_rows, a0, lin, lg2);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     gemm2<KS>(xt, a0, l31, h, g0, g1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     pe += (double)lin + (double)lg2 * (double)LN2;
     __syncthreads();  // drains this stage's global_load_lds (vmcnt(0)) and frees buf
   }
   pe += __shfl_xor(pe, 32);
 
   // fixed-order combination of the 4 row lanes: lane partials staged through LDS
+  float* red = xs;                                   // [RL_WAVES][32][64] floats
+  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[(w * 32 + r) * 64 + lane] = g0[r];
+    red[(w * 32 + 16 + r) * 64 + lane] = g1[r];
+  }
+  red_pe[w * 64 + lane] = pe;
+  __syncthreads();
+  if (w == 0 && cin) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
+#pragma unroll
+      for (int ww = 1; ww < RL_WAVES; ++ww) {
+        s0 += red[(ww * 32 + r) * 64 + lane];
+        s1 += red[(ww * 32 + 16 + r) * 64 + lane];
+      }
+      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
+      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
+    }
+    if (h == 0) {
+      double sp = red_pe[lane];
+#pragma unroll
+      for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
+      pepart[(size_t)split * ldc + pos] = sp;
+    }
+  }
+}
+
+// Wave-pipelined variant: the 4 row lanes of a workgroup never synchronise inside the
+// loop.  Wave w owns the 32-row subtile w of each 128-row stage; it prefetches its next
+// subtile into registers (8 x 16 B per lane) while the MFMAs of the current one run,
+// then writes it to its private LDS slice (the operand transpose) -- so neither global
+// latency nor a workgroup barrier sits between two tiles.
+template <int KS>
+__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_wavepipe(const float* __restrict__ Xp, int64_t n_rows,
+                                                                    int nstages, int D, int S, int Gt,
+                                                                    nmx_eval_batch ev, float* __restrict__ gpart,
+                                                                    double* __restrict__ pepart) {
+  constexpr int XS = 2 * KS + 1;
+  constexpr int SUB = 32 * XS;                      // floats per wave subtile
+  constexpr int CHUNKS = SUB / 4;                   // 16-byte pieces (SUB % 4 == 0 for XS odd? see assert)
+  constexpr int NCH = (CHUNKS + 63) / 64;           // float4 per lane
+  constexpr int WBUF = (SUB + 3) / 4 * 4 + 64;      // per-wave LDS floats
+  static_assert((32 * XS) % 4 == 0, "subtile must be a whole number of float4");
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7;
+  const int q = b >> 3;
+  const int ct = q % Gt;
+  const int split = (q / Gt) * 8 + xcd;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int pos = ct * 32 + l31;
+  const bool cin = pos < ldc;
+  const int c = cin ? nmx_eval_chain(ev, pos) : -1;
+  const bool act = c >= 0;
+  if (!__any(act)) return;
+
+  const int per = (nstages + S - 1) / S;
+  const int t0 = split * per;
+  const int t1 = min(t0 + per, nstages);
+  float* const xt = xs + w * WBUF;
+
+  float zb[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    zb[s] = (k < D && act) ? ev.z[(size_t)k * ldc + c] : 0.0f;
+  }
+  f32x16 g0, g1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    g0[r] = 0.0f;
+    g1[r] = 0.0f;
+  }
+  double pe = 0.0;
+  float4 pf[NCH];
+  auto fetch = [&](int t) {
+    const float4* src = reinterpret_cast<const float4*>(Xp + ((size_t)t * RL_ROWS + w * 32) * XS);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int chunk = i * 64 + lane;
+      pf[i] = chunk < CHUNKS ? src[chunk] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int chunk = i * 64 + lane;
+      if (chunk < CHUNKS) reinterpret_cast<float4*>(xt)[chunk] = pf[i];
+    }
+  };
+  if (t0 < t1) fetch(t0);
+  for (int t = t0; t < t1; ++t) {
+    commit();                       // LDS in-order per wave: the reads below see it
+    if (t + 1 < t1) fetch(t + 1);   // in flight during this tile's MFMAs
+    const int64_t rb = (int64_t)t * RL_ROWS + w * 32;
+    f32x16 a0;
+    float lin = 0.0f, lg2 = 0.0f;
+    {
+      __builtin_amdgcn_s_setprio(1);
+      gemm1<KS>(xt, zb, l31, h, a0);
+      __builtin_amdgcn_s_setprio(0);
+      if (rb + 32 <= n_rows) epilogue<KS, false>(xt, h, rb, n_rows, a0, lin, lg2);
+      else epilogue<KS, true>(xt, h, rb, n_rows, a0, lin, lg2);
+      __builtin_amdgcn_s_setprio(1);
+      gemm2<KS>(xt, a0, l31, h, g0, g1);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    pe += (double)lin + (double)lg2 * (double)LN2;
+  }
+  pe += __shfl_xor(pe, 32);
+  __syncthreads();
+
   float* red = xs;                                   // [RL_WAVES][32][64] floats
   double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
 #pragma unroll
@@ -388,13 +515,17 @@ int check_ev(const nmx_eval_batch* ev) {
   return NMX_OK;
 }
 
-// Kernel variant: NMX_LOGREG_VARIANT=0 forces the generic kernel (A/B experiments).
+// Kernel variant (A/B experiments; all give the same sums in the same order):
+//   11 (default) row lanes, single stage buffer, s_setprio around the MFMA chains
+//    5 same without s_setprio;  4 double-buffered stages;  8 barrier-free wave pipeline
+//    0 generic tile kernel.
+// Measured at C=4096 (profiles/r01): 11: 103.9, 5: 103.0, 8: 101.6, 4: 98.2 TFLOP/s.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
-  return e ? atoi(e) : 5;
+  return e ? atoi(e) : 11;
 }
 
-template <int KS, int NBUF>
+template <int KS, int NBUF, bool PRIO>
 void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
                      double* pepart, hipStream_t s) {
   const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
@@ -404,8 +535,22 @@ void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batc
   size_t lds = (size_t)NBUF * BUF * sizeof(float);
   const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
   if (lds < red) lds = red;
-  hipLaunchKernelGGL((k_logreg_rowlanes<KS, NBUF>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages,
+  hipLaunchKernelGGL((k_logreg_rowlanes<KS, NBUF, PRIO>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages,
                      D, S, Gt, *ev, gpart, pepart);
+}
+
+template <int KS>
+void launch_wavepipe(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart, double* pepart,
+                     hipStream_t s) {
+  const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
+  const int S = num_splits(n_rows);
+  const int Gt = ev->ldc / 32;
+  constexpr int WBUF = (32 * (2 * KS + 1) + 3) / 4 * 4 + 64;
+  size_t lds = (size_t)RL_WAVES * WBUF * sizeof(float);
+  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
+  if (lds < red) lds = red;
+  hipLaunchKernelGGL((k_logreg_wavepipe<KS>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages, D, S,
+                     Gt, *ev, gpart, pepart);
 }
 
 template <int KS, bool EXACT>
@@ -464,8 +609,10 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
-  if (KS == 28 && var == 4) launch_rowlanes<28, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
-  else if (KS == 28 && var == 5) launch_rowlanes<28, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  if (KS == 28 && var == 4) launch_rowlanes<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
+  else if (KS == 28 && var == 5) launch_rowlanes<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 8) launch_wavepipe<28>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 11) launch_rowlanes<28, 1, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);

@@ -46,6 +46,7 @@ def _eval(pot, Z, device, phase=None, bind=True):
 @pytest.mark.parametrize("tri", [0, 1, 2])
 @pytest.mark.parametrize("D,C", [(3, 64), (55, 200), (130, 130), (300, 256), (1000, 70)])
 def test_gemm_chains_matches_fp64(device, D, C, tri):
+    """Default (128 x 64) kernel; the opt-in wide kernel runs in a subprocess below."""
     rs = np.random.RandomState(D)
     lib = native.lib()
     lda = lib.nmx_dense_padded_dim(D)
@@ -287,3 +288,16 @@ def test_whitened_packed_list_matches_dense_batch(device):
     np.testing.assert_array_equal(g_l[:, chosen], g_d[:, chosen])
     others = np.setdiff1d(np.arange(ldc), chosen)
     assert np.all(np.isnan(pe_l[others])) and np.all(np.isnan(g_l[:, others]))
+
+
+def test_gemm_chains_wide_variant_subprocess(device):
+    """NMX_GEMM_VARIANT=1 (128 x 128 tiles, XCD-aware order) passes the same checks; the
+    variant is latched per process, hence a child process."""
+    import subprocess
+    import sys
+
+    env = dict(__import__("os").environ, NMX_GEMM_VARIANT="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", __file__,
+                        "-k", "gemm_chains_matches_fp64 or packed_list"], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -237,3 +237,25 @@ def test_bnn_skips_inactive_and_list(device):
     phase[::3] = 3
     pe, g = _eval(pot, Z, device, phase=phase)
     assert np.all(np.isnan(pe[phase == 0])) and np.all(np.isfinite(pe[phase == 3]))
+
+
+def test_logreg_kernel_variants_agree(device, monkeypatch):
+    """A/B kernel variants of the covtype potential (NMX_LOGREG_VARIANT) compute the same
+    sums in the same order: bitwise for the row-lane forms, FMA-contraction level (1e-6)
+    for the wave-pipelined one."""
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(11)
+    N, D, C = 5000, 55, 96
+    X = rs.randn(N, D).astype(np.float32)
+    y = (rs.rand(N) < 0.3).astype(np.float32)
+    Z = (rs.randn(C, D) * 0.2).astype(np.float32)
+    out = {}
+    for v in ("11", "5", "4", "8"):
+        monkeypatch.setenv("NMX_LOGREG_VARIANT", v)
+        out[v] = _eval(LogisticRegression(X, y), Z, device)
+    for v in ("5", "4"):
+        np.testing.assert_array_equal(out[v][0], out["11"][0])
+        np.testing.assert_array_equal(out[v][1], out["11"][1])
+    np.testing.assert_allclose(out["8"][0], out["11"][0], rtol=1e-6)
+    np.testing.assert_allclose(out["8"][1], out["11"][1], rtol=1e-5, atol=1e-3)
