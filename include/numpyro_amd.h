@@ -88,6 +88,8 @@ enum nmx_field {
   /* wide (D-split) step only: per-slice partial dot products f32 [NS][2*MAXD+2][ldc] and
    * momentum kinetic-energy partials [NS][ldc]; NS = nmx_nuts_num_slices(dim) (0: fused) */
   NMX_F_PART, NMX_F_PART0,
+  /* wide step only: slice-reduced totals f32 [2*MAXD+3 + 1][ldc] */
+  NMX_F_TOT,
   NMX_NUM_FIELDS
 };
 

@@ -46,6 +46,7 @@ size_t field_bytes(int field, int ldc, int D, int MD, int iter_cap) {
   if (field == NMX_F_FINISHED) return (size_t)(iter_cap > 0 ? iter_cap : 1) * 4;
   if (field == NMX_F_PART) return (size_t)num_slices(D) * NPART * ldc * 4;
   if (field == NMX_F_PART0) return (size_t)num_slices(D) * ldc * 4;
+  if (field == NMX_F_TOT) return num_slices(D) > 0 ? (size_t)(NPART + 1) * ldc * 4 : 0;
   return 0;
 }
 
@@ -67,6 +68,7 @@ struct Arena {
   int32_t* finished;
   float* part;
   float* part0;
+  float* tot;
 };
 
 #define AI(f) a.is[(f) - NMX_F_PHASE]
@@ -89,6 +91,7 @@ Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
   a.finished = (int32_t*)(b + field_offset(NMX_F_FINISHED, ldc, D, MD, iter_cap));
   a.part = (float*)(b + field_offset(NMX_F_PART, ldc, D, MD, iter_cap));
   a.part0 = (float*)(b + field_offset(NMX_F_PART0, ldc, D, MD, iter_cap));
+  a.tot = (float*)(b + field_offset(NMX_F_TOT, ldc, D, MD, iter_cap));
   return a;
 }
 
@@ -904,15 +907,59 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   }
 }
 
-__global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_s(WideArgs W) {
-  __shared__ float lds[(NPART + 1) * WIDE_SWAVES * 64];
+// Which slice-partial entries chain c needs this step (0: KE, 1..2MAXD: checkpoint pairs,
+// 2MAXD+1..+2: tree pair, NPART: momentum KE of a just-started transition).
+__device__ __forceinline__ bool entry_needed(const nmx_nuts_config& cfg, const Arena& a, int c, int e) {
+  const int ph = AI(NMX_F_PHASE)[c];
+  if (e == NPART) return (AI(NMX_F_ACTION)[c] & ACT_KE0_PENDING) != 0;
+  if (ph != NMX_PH_LEAF) return false;
+  if (e == 0) return true;
+  if (cfg.algo != NMX_ALGO_NUTS) return false;
+  if (e >= 1 + 2 * MAXD) return true;
+  int imin, imax;
+  nmx_leaf_idx_to_ckpt_idxs(AI(NMX_F_SUB_N)[c], imin, imax);
+  const int i = (e - 1) >> 1;
+  return i >= imin && i <= imax;
+}
+
+// Fixed-order slice reduction, one block per (64 chains, entry): wave w sums slices w,
+// w+4, ... in order, then the waves are added in order.
+__global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_r(WideArgs W) {
+  __shared__ float lds[WIDE_SWAVES * 64];
   const nmx_nuts_config& cfg = W.p.cfg;
   const Arena& a = W.p.a;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  const int e = blockIdx.y;
+  const int ldc = cfg.ldc;
+  const bool need = c < cfg.num_chains && entry_needed(cfg, a, c, e);
+  if (!__syncthreads_or(need)) return;
+  float s = 0.0f;
+  if (need) {
+    if (e == NPART) {
+      for (int sl = wv; sl < W.ns; sl += WIDE_SWAVES) s += a.part0[(size_t)sl * ldc + c];
+    } else {
+      for (int sl = wv; sl < W.ns; sl += WIDE_SWAVES) s += *(part_ptr(a, ldc, sl, e) + c);
+    }
+  }
+  lds[wv * 64 + lane] = s;
+  __syncthreads();
+  if (wv == 0 && need) {
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < WIDE_SWAVES; ++w) t += lds[w * 64 + lane];
+    a.tot[(size_t)e * ldc + c] = t;
+  }
+}
+
+// Scalar logic of the wide step, one wave per 64 chains, on the reduced totals.
+__global__ __launch_bounds__(64) void k_wide_s(WideArgs W) {
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x;
+  const int c = blockIdx.x * 64 + lane;
   const int ldc = cfg.ldc;
   const bool valid = c < cfg.num_chains;
-  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   const uint64_t seed = cfg.seed;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
@@ -922,45 +969,15 @@ __global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_s(WideArgs W) {
   const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
   begin_step(cfg, a, c, valid, S, A);
   const bool ke0_pending = valid && (AI(NMX_F_ACTION)[c] & ACT_KE0_PENDING);
-  // fixed-order reduction of the slice partials: wave w sums slices w, w+4, ... in order,
-  // then wave 0 sums the waves in order.
-  float red[NPART + 1];
-#pragma unroll
-  for (int i = 0; i < NPART + 1; ++i) red[i] = 0.0f;
-  for (int s = wv; s < W.ns; s += WIDE_SWAVES) {
-    if (A.leaf) {
-      red[0] += *(part_ptr(a, ldc, s, 0) + c);
-      if (is_nuts) {
-#pragma unroll
-        for (int i = 0; i < MAXD; ++i)
-          if (i >= A.imin && i <= A.imax) {
-            red[1 + 2 * i] += *(part_ptr(a, ldc, s, 1 + 2 * i) + c);
-            red[2 + 2 * i] += *(part_ptr(a, ldc, s, 2 + 2 * i) + c);
-          }
-        red[1 + 2 * MAXD] += *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c);
-        red[2 + 2 * MAXD] += *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c);
-      }
-    }
-    if (ke0_pending) red[NPART] += a.part0[(size_t)s * ldc + c];
-  }
-#pragma unroll
-  for (int i = 0; i < NPART + 1; ++i) lds[(i * WIDE_SWAVES + wv) * 64 + lane] = red[i];
-  __syncthreads();
-  if (wv != 0) return;
-#pragma unroll
-  for (int i = 0; i < NPART + 1; ++i) {
-    float t = 0.0f;
-    for (int w = 0; w < WIDE_SWAVES; ++w) t += lds[(i * WIDE_SWAVES + w) * 64 + lane];
-    red[i] = t;
-  }
+  const float* T = a.tot + c;
   if (ke0_pending) {
-    S.E0 = S.pe + 0.5f * red[NPART];  // build_tree :1130 (momentum KE from the last V2)
+    S.E0 = S.pe + 0.5f * T[(size_t)NPART * ldc];  // build_tree :1130 (momentum KE from the last V2)
     S.energy = S.E0;
   }
-  leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
+  leaf_phase(cfg, S, A, A.leaf ? 0.5f * T[0] : 0.0f, seed, gch);
   tree_phase(
-      cfg, S, A, [&](int i, int side) { return red[1 + 2 * i + side]; },
-      [&](int side) { return red[1 + 2 * MAXD + side]; }, seed, gch, W.p.fields, c, true);
+      cfg, S, A, [&](int i, int side) { return T[(size_t)(1 + 2 * i + side) * ldc]; },
+      [&](int side) { return T[(size_t)(1 + 2 * MAXD + side) * ldc]; }, seed, gch, W.p.fields, c, true);
   if (valid) {
     AI(NMX_F_ACTION)[c] = pack_act(A);
     AI(NMX_F_SLOT)[c] = A.slot;
@@ -1227,7 +1244,8 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   if (ns > 0) {
     WideArgs w{args, ns, slice_width(cfg->dim)};
     hipLaunchKernelGGL(k_wide_v1, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
-    hipLaunchKernelGGL(k_wide_s, dim3(grid), dim3(64 * WIDE_SWAVES), 0, s, w);
+    hipLaunchKernelGGL(k_wide_r, dim3(grid, NPART + 1), dim3(64 * WIDE_SWAVES), 0, s, w);
+    hipLaunchKernelGGL(k_wide_s, dim3(grid), dim3(64), 0, s, w);
     hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
     return nmx_check_launch("k_nuts_step (wide)");
   }

@@ -94,15 +94,29 @@ __global__ __launch_bounds__(64 * WAVES) void k_sv_part(const float* __restrict_
   }
 }
 
-__global__ __launch_bounds__(64) void k_sv_fin(int T, nmx_eval_batch ev, const float* __restrict__ part) {
-  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + threadIdx.x);
-  if (c < 0) return;
-  const int ldc = ev.ldc;
-  float sums[NSUM] = {0.f, 0.f, 0.f, 0.f};
-  const int ns = num_slices(T);
-  for (int sl = 0; sl < ns; ++sl)
+// Slice sums in a fixed order: wave w adds slices w, w+WAVES, ..., then wave 0 adds the
+// waves in order.
+template <int N>
+__device__ __forceinline__ bool slice_sums(const float* __restrict__ part, int ns, int ldc, int c, float (&v)[N],
+                                           float* lds) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NSUM; ++i) sums[i] += part[((size_t)sl * NSUM + i) * ldc + c];
+  for (int i = 0; i < N; ++i) v[i] = 0.0f;
+  if (c >= 0)
+    for (int sl = wv; sl < ns; sl += WAVES)
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] += part[((size_t)sl * N + i) * ldc + c];
+  wave_block_sum<N>(v, lds);
+  return wv == 0 && c >= 0;
+}
+
+__global__ __launch_bounds__(64 * WAVES) void k_sv_fin(int T, nmx_eval_batch ev, const float* __restrict__ part) {
+  __shared__ float lds[NSUM * WAVES * 64];
+  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + (threadIdx.x & 63));
+  if (!__syncthreads_or(c >= 0)) return;
+  const int ldc = ev.ldc;
+  float sums[NSUM];
+  if (!slice_sums<NSUM>(part, num_slices(T), ldc, c, sums, lds)) return;
   const float a = ev.z[c];
   const float b = ev.z[(size_t)(T + 1) * ldc + c];
   const float nu = expf(a);
@@ -151,14 +165,15 @@ __global__ __launch_bounds__(64 * WAVES) void k_funnel_part(int D, nmx_eval_batc
   if (act && wv == 0) part[(size_t)blockIdx.y * ldc + c] = sx[0];
 }
 
-__global__ __launch_bounds__(64) void k_funnel_fin(int D, nmx_eval_batch ev, const float* __restrict__ part) {
-  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + threadIdx.x);
-  if (c < 0) return;
+__global__ __launch_bounds__(64 * WAVES) void k_funnel_fin(int D, nmx_eval_batch ev, const float* __restrict__ part) {
+  __shared__ float lds[WAVES * 64];
+  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + (threadIdx.x & 63));
+  if (!__syncthreads_or(c >= 0)) return;
   const int ldc = ev.ldc;
   const int K = D - 1;
-  float sx = 0.0f;
-  const int ns = num_slices(K);
-  for (int sl = 0; sl < ns; ++sl) sx += part[(size_t)sl * ldc + c];
+  float sv[1];
+  if (!slice_sums<1>(part, num_slices(K), ldc, c, sv, lds)) return;
+  const float sx = sv[0];
   const float y = ev.z[(size_t)K * ldc + c];
   const float e = expf(-y);
   const float Kf = (float)K;
@@ -188,7 +203,7 @@ extern "C" int nmx_pe_stochastic_volatility(const float* returns, int T, const n
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
   hipLaunchKernelGGL(k_sv_part, dim3(ev->ldc / 64, num_slices(T)), dim3(64 * WAVES), 0, s, returns, T, *ev, part);
-  hipLaunchKernelGGL(k_sv_fin, dim3(ev->ldc / 64), dim3(64), 0, s, T, *ev, part);
+  hipLaunchKernelGGL(k_sv_fin, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, s, T, *ev, part);
   return nmx_check_launch("k_sv");
 }
 
@@ -198,6 +213,6 @@ extern "C" int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* workspace,
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
   hipLaunchKernelGGL(k_funnel_part, dim3(ev->ldc / 64, num_slices(dim - 1)), dim3(64 * WAVES), 0, s, dim, *ev, part);
-  hipLaunchKernelGGL(k_funnel_fin, dim3(ev->ldc / 64), dim3(64), 0, s, dim, *ev, part);
+  hipLaunchKernelGGL(k_funnel_fin, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, s, dim, *ev, part);
   return nmx_check_launch("k_funnel");
 }

@@ -42,7 +42,7 @@ FIELDS = [
     "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "pe_eval",
     "z", "zgrad", "zl", "rl", "gl", "zr", "rr", "gr", "zsub", "gsub", "rsum", "rsum_sub",
     "inv_mass", "mass_sqrt", "wf_mean", "wf_m2", "z_eval", "g_eval",
-    "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished", "part", "part0",
+    "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished", "part", "part0", "tot",
 ]
 FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 INT_FIELDS = set(FIELDS[:FIELDS.index("step_size")]) | {"counters", "finished", "active_idx"}
