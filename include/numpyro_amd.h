@@ -243,7 +243,10 @@ int nmx_logreg_num_splits(int64_t n_rows);
 int nmx_dense_padded_dim(int dim);
 int nmx_gemm_chains(const float* At, int lda, int dim, const float* In, float* Out, const float* bias,
                     int triangle, int ldc, const int32_t* phase, const int32_t* active_count, int num_chains,
-                    void* stream);
+                    void* workspace, void* stream);
+/* Workspace for split-K (K split in a number of parts that depends on dim only; partials
+ * summed in a fixed order).  0 = no split; a NULL workspace also disables it. */
+size_t nmx_gemm_chains_workspace_bytes(int dim, int ldc);
 /* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
  * (p < *count, device-side count, grid sized for ldo / ldi positions). */
 int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,

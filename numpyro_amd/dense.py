@@ -45,7 +45,15 @@ class Whitening:
         self.fwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T^T
         self.bwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T
         self.mu = torch.zeros(self.D, dtype=torch.float32, device=self.device)
+        self._ws = {}
         self.set(torch.eye(self.D, dtype=torch.float64, device=self.device), None)
+
+    def workspace(self, ldc):
+        """Split-K workspace of nmx_gemm_chains for [D][ldc] operands (None if no split)."""
+        if ldc not in self._ws:
+            nb = lib().nmx_gemm_chains_workspace_bytes(self.D, ldc)
+            self._ws[ldc] = torch.empty(nb, dtype=torch.uint8, device=self.device) if nb else None
+        return self._ws[ldc]
 
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
@@ -86,13 +94,15 @@ class Whitening:
         """out[:, c] = mu + T w[:, c] for [D, ldc] buffers."""
         ldc = w.shape[-1]
         check(lib().nmx_gemm_chains(ptr(self.fwd_t), self.lda, self.D, ptr(w), ptr(out), ptr(self.mu), UPPER, ldc,
-                                    ptr(phase), None, int(num_chains or ldc), stream), "nmx_gemm_chains")
+                                    ptr(phase), None, int(num_chains or ldc), ptr(self.workspace(ldc)), stream),
+              "nmx_gemm_chains")
 
     def grad_to_w(self, g, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = T^T g[:, c]."""
         ldc = g.shape[-1]
         check(lib().nmx_gemm_chains(ptr(self.bwd_t), self.lda, self.D, ptr(g), ptr(out), None, LOWER, ldc,
-                                    ptr(phase), None, int(num_chains or ldc), stream), "nmx_gemm_chains")
+                                    ptr(phase), None, int(num_chains or ldc), ptr(self.workspace(ldc)), stream),
+              "nmx_gemm_chains")
 
     def to_whitened(self, z):
         """w = T^-1 (z - mu) for z [D, n] (host-side re-expression at window ends)."""
@@ -148,19 +158,21 @@ class WhitenedPotential(Potential):
             # compacted list: the products run on packed columns of the listed chains only
             check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
                   "nmx_pack_columns")
+            ws = ptr(wt.workspace(ldc))
             check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ptr(self.wp), ptr(self.zb), ptr(wt.mu), UPPER, ldc,
-                                    None, ev.active_count, C, stream), "nmx_gemm_chains")
+                                    None, ev.active_count, C, ws, stream), "nmx_gemm_chains")
             self.base.evaluate(self._base_batch(ev), stream)
             check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ptr(self.wp), None, LOWER, ldc,
-                                    None, ev.active_count, C, stream), "nmx_gemm_chains")
+                                    None, ev.active_count, C, ws, stream), "nmx_gemm_chains")
             check(L.nmx_unpack_columns(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
                                        ptr(self.pe_p), ev.pe, stream), "nmx_unpack_columns")
             return
+        ws = ptr(wt.workspace(ldc))
         check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ev.z, ptr(self.zb), ptr(wt.mu), UPPER, ldc,
-                                ev.phase, None, C, stream), "nmx_gemm_chains")
+                                ev.phase, None, C, ws, stream), "nmx_gemm_chains")
         self.base.evaluate(self._base_batch(ev), stream)
         check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ev.grad, None, LOWER, ldc,
-                                ev.phase, None, C, stream), "nmx_gemm_chains")
+                                ev.phase, None, C, ws, stream), "nmx_gemm_chains")
 
     def flops_per_eval(self, num_chains):
         """Algorithmic FLOPs of the two triangular products (D^2 each per chain) -- the

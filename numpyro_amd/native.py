@@ -114,7 +114,8 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_logreg_pe_grad": (c_int, [c_vp, c_i64, c_int, _evp, c_vp, c_vp]),
     "nmx_logreg_num_splits": (c_int, [c_i64]),
     "nmx_dense_padded_dim": (c_int, [c_int]),
-    "nmx_gemm_chains": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "nmx_gemm_chains": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "nmx_gemm_chains_workspace_bytes": (c_size, [c_int, c_int]),
     "nmx_pack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_unpack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "nmx_pe_mvn": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, _evp, c_vp]),

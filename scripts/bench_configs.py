@@ -40,14 +40,16 @@ def bench_gemm(D, C, reps=10, tri=0):
     x = torch.randn(D, ldc, device=dev)
     y = torch.empty(D, ldc, device=dev)
     s = native.stream_ptr()
+    nws = lib.nmx_gemm_chains_workspace_bytes(D, ldc)
+    ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws else None
     for _ in range(2):
         native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
-                                         None, C, s))
+                                         None, C, native.ptr(ws), s))
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
         native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
-                                         None, C, s))
+                                         None, C, native.ptr(ws), s))
     b.record()
     b.synchronize()
     ms = a.elapsed_time(b) / reps

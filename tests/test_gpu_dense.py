@@ -44,8 +44,9 @@ def _eval(pot, Z, device, phase=None, bind=True):
 
 
 @pytest.mark.parametrize("tri", [0, 1, 2])
-@pytest.mark.parametrize("D,C", [(3, 64), (55, 200), (130, 130), (300, 256), (1000, 70)])
-def test_gemm_chains_matches_fp64(device, D, C, tri):
+@pytest.mark.parametrize("D,C,split", [(3, 64, False), (55, 200, False), (130, 130, False), (300, 256, False),
+                                       (1000, 70, False), (3000, 130, True), (5038, 64, True)])
+def test_gemm_chains_matches_fp64(device, D, C, tri, split):
     """Default (128 x 64) kernel; the opt-in wide kernel runs in a subprocess below."""
     rs = np.random.RandomState(D)
     lib = native.lib()
@@ -64,8 +65,11 @@ def test_gemm_chains_matches_fp64(device, D, C, tri):
     dAt, dIn, db = (torch.from_numpy(x).to(device) for x in (At, In, bias))
     dph = torch.from_numpy(phase).to(device)
     out = torch.full((D, ldc), float("nan"), device=device)
+    nws = lib.nmx_gemm_chains_workspace_bytes(D, ldc)
+    ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=device) if split else None
     native.check(lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(out), native.ptr(db),
-                                     tri, ldc, native.ptr(dph), None, C, native.stream_ptr()))
+                                     tri, ldc, native.ptr(dph), None, C, native.ptr(ws) if nws else None,
+                                     native.stream_ptr()))
     torch.cuda.synchronize()
     o = out.cpu().numpy().astype(np.float64)
     A32 = At[:D, :D].T.astype(np.float64)
@@ -80,11 +84,11 @@ def test_gemm_chains_matches_fp64(device, D, C, tri):
             assert np.all(np.isnan(o[:, cols]))
     # error paths
     assert lib.nmx_gemm_chains(native.ptr(dAt), lda - 1, D, native.ptr(dIn), native.ptr(out), None, 0, ldc, None,
-                               None, C, None) != 0
+                               None, C, None, None) != 0
     assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(dIn), None, 0, ldc, None, None,
-                               C, None) != 0
+                               C, None, None) != 0
     assert lib.nmx_gemm_chains(native.ptr(dAt), lda, D, native.ptr(dIn), native.ptr(out), None, 3, ldc, None, None,
-                               C, None) != 0
+                               C, None, None) != 0
 
 
 def _corr_cov(D, seed=0):
