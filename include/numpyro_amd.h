@@ -113,8 +113,11 @@ typedef struct nmx_nuts_config {
   int32_t adapt_step_size;       /* hmc_util.py:518-707 flags */
   int32_t adapt_mass_matrix;
   int32_t regularize_mass_matrix;
-  int32_t dense_mass;            /* must be 0: dense mass runs as identity mass on whitened
-                                    coordinates around the potential (nmx_gemm_chains) */
+  int32_t unit_mass;             /* 1: the inverse mass matrix is the identity for every chain
+                                    and is not adapted (dense mass runs as identity mass on
+                                    whitened coordinates around the potential, nmx_gemm_chains;
+                                    or no adaptation and no user matrix): the step skips the
+                                    inv_mass / mass_sqrt loads */
   int32_t sync_chains;           /* 1: reference vmap lockstep per transition */
   float target_accept_prob;
   float max_delta_energy;        /* hmc.py:188 */
@@ -210,7 +213,10 @@ size_t nmx_pe_wide_workspace_bytes(int dim, int num_chains);
  * units, tanh; z = (log prec_obs, w1[Dx][H], w2[H][H], w3[H]).  One workgroup per evaluated
  * chain with weights and activations in LDS (needs 4 (Dx H + H^2 + H + N Dx + 2N + 2 N H + 256)
  * bytes <= 160 KiB). */
-int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev, void* stream);
+int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev, void* workspace,
+               void* stream);
+/* Workspace of nmx_pe_bnn: the evaluated chains' z and gradient transposed to rows. */
+size_t nmx_pe_bnn_workspace_bytes(int Dx, int H, int num_chains);
 
 /* Logistic regression (examples/covtype.py:66-71): coefs ~ N(0,1)^D,
  * obs ~ BernoulliLogits(X @ coefs).  X is first packed (row tiles with the label in a pad

@@ -515,6 +515,7 @@ struct VecCtx {
   const Arena* a;
   int ldc, D;
   size_t ck_stride;
+  bool unit;  // cfg.unit_mass: inv_mass == mass_sqrt == 1, not loaded
 };
 
 // L1 + L2 minus the proposal copy: finish the pending leapfrog (hmc_util.py:306-308),
@@ -532,7 +533,7 @@ __device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t 
   const Arena& a = *v.a;
   x.g = AV(NMX_F_G_EVAL)[idx];
   x.rf = (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
-  x.im = AV(NMX_F_INV_MASS)[idx];
+  x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
   x.ze = AV(NMX_F_Z_EVAL)[idx];
   if constexpr (NUTS) {
     x.rs_old = A.k == 0 ? 0.0f : AV(NMX_F_RSUM_SUB)[idx];
@@ -656,8 +657,8 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t
     x.wm = AV(NMX_F_WF_MEAN)[idx];
     x.w2 = AV(NMX_F_WF_M2)[idx];
   }
-  if (A.start_iter) x.ms = AV(NMX_F_MASS_SQRT)[idx];
-  if (A.start_iter || A.prep_leaf) x.im = AV(NMX_F_INV_MASS)[idx];
+  if (A.start_iter) x.ms = v.unit ? 1.0f : AV(NMX_F_MASS_SQRT)[idx];
+  if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
   if (A.prep_leaf) {
     const int nd = A.new_dir;
     x.zfn = (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
   Act A;
   const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
   begin_step(cfg, a, c, valid, S, A);
-  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   const float seff = valid ? S.step_eff : 0.0f;
 
   float red[NPART];
@@ -882,7 +883,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   A.imax = 0;
   if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);
   const float seff = A.leaf ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
-  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   float red[NPART];
 #pragma unroll
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
@@ -1018,7 +1019,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   const int it = valid ? AI(NMX_F_ITER)[c] : 0;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   float* const samp = (A.iter_done && A.slot >= 0) ? W.p.samples + (size_t)A.slot * D * ldc : nullptr;
-  const VecCtx v{&a, ldc, D, (size_t)D * ldc};
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   float ke0[1] = {0.0f};
   if (act & VEC) {
     const int b0 = (s * W.sw) / 4, b1 = (min(D, (s + 1) * W.sw) + 3) / 4;
@@ -1127,7 +1128,8 @@ int validate(const nmx_nuts_config* cfg) {
   if (cfg->num_chains <= 0 || cfg->dim <= 0) return nmx_fail(NMX_ERR_INVALID, "num_chains and dim must be positive");
   if (cfg->algo != NMX_ALGO_NUTS && cfg->algo != NMX_ALGO_HMC)
     return nmx_fail(NMX_ERR_INVALID, "algo must be NUTS(0) or HMC(1)");
-  if (cfg->dense_mass) return nmx_fail(NMX_ERR_UNSUPPORTED, "dense_mass is not supported by this engine build");
+  if (cfg->unit_mass && cfg->adapt_mass_matrix)
+    return nmx_fail(NMX_ERR_INVALID, "unit_mass excludes adapt_mass_matrix");
   const int md = cfg->max_tree_depth > cfg->max_tree_depth_warmup ? cfg->max_tree_depth : cfg->max_tree_depth_warmup;
   if (cfg->algo == NMX_ALGO_NUTS) {
     if (cfg->max_tree_depth < 1 || cfg->max_tree_depth_warmup < 1)
@@ -1209,7 +1211,8 @@ extern "C" int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void
   int st = validate(cfg);
   if (st) return st;
   Arena a = arena_of(cfg, arena);
-  hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream);
+  if (hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
   hipLaunchKernelGGL(k_nuts_init_check, dim3((cfg->num_chains + 63) / 64), dim3(64), 0,
                      (hipStream_t)stream, a, *cfg);
   return nmx_check_launch("k_nuts_init_check");

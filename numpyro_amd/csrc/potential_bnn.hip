@@ -8,9 +8,10 @@
 // activation layers and the adjoints live in LDS (N=100, H=69: 78 KB), the three
 // N x H x H products run as 4x4 register-blocked FMA loops.  The model is ~3 MFLOP per
 // chain-leapfrog -- ~3% of the dense-mass products it runs between (dense.hip), so it is
-// written for clarity and LDS residency rather than MFMA.  Blocks are mapped so that
-// consecutive list positions run on one XCD (blockIdx % 8): the strided per-chain column
-// gathers of neighbouring chains then share L2 lines.
+// written for clarity and LDS residency rather than MFMA.  The chain-major columns of the
+// evaluated chains are first transposed to rows (k_cols_to_rows, 64x64 LDS tiles, both
+// sides coalesced) so each workgroup reads its chain's 20 KB parameter vector and writes
+// its gradient contiguously; k_rows_to_cols scatters the gradients back.
 #include <math.h>
 
 #include "nmx_api_internal.h"
@@ -18,7 +19,10 @@
 
 namespace {
 
-constexpr int THREADS = 256;
+#ifndef NMX_BNN_THREADS
+#define NMX_BNN_THREADS 512
+#endif
+constexpr int THREADS = NMX_BNN_THREADS;
 
 struct BnnDims {
   int N, Dx, H;
@@ -31,7 +35,7 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   if (threadIdx.x < 64) {
     float s = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s += red[w * 64 + threadIdx.x];
+    for (int w = 0; w < THREADS / 64; ++w) s += red[w * 64 + threadIdx.x];
     red[threadIdx.x] = s;
   }
   __syncthreads();
@@ -46,8 +50,49 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return t;
 }
 
+// Column <-> row transposes of the listed chains: rows[p][d] = cols[d][chain(p)] (and back),
+// 64 x 64 tiles through LDS so both sides are coalesced.  They let k_bnn read and write
+// each chain's D-vector contiguously instead of one cache line per coordinate.
+__global__ __launch_bounds__(256) void k_cols_to_rows(const float* __restrict__ cols, int D, nmx_eval_batch ev,
+                                                      float* __restrict__ rows) {
+  __shared__ float tile[64][65];
+  const int p0 = blockIdx.y * 64, d0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = nmx_eval_chain(ev, p0 + lane);
+  if (!__syncthreads_or(c >= 0)) return;
+  for (int dd = wv; dd < 64; dd += 4) {
+    const int d = d0 + dd;
+    tile[dd][lane] = (c >= 0 && d < D) ? cols[(size_t)d * ev.ldc + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int pp = wv; pp < 64; pp += 4) {
+    const int d = d0 + lane;
+    if (d < D && nmx_eval_chain(ev, p0 + pp) >= 0) rows[(size_t)(p0 + pp) * D + d] = tile[lane][pp];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rows_to_cols(const float* __restrict__ rows, int D, nmx_eval_batch ev,
+                                                      float* __restrict__ cols) {
+  __shared__ float tile[64][65];
+  const int p0 = blockIdx.y * 64, d0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = nmx_eval_chain(ev, p0 + lane);
+  if (!__syncthreads_or(c >= 0)) return;
+  for (int pp = wv; pp < 64; pp += 4) {
+    const int d = d0 + lane;
+    tile[pp][lane] = (d < D && p0 + pp < ev.ldc) ? rows[(size_t)(p0 + pp) * D + d] : 0.0f;
+  }
+  __syncthreads();
+  for (int dd = wv; dd < 64; dd += 4) {
+    const int d = d0 + dd;
+    if (c >= 0 && d < D) cols[(size_t)d * ev.ldc + c] = tile[lane][dd];
+  }
+}
+
+// zr / gr: the evaluated chains' positions and gradients as rows [position][D].
 __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, const float* __restrict__ Y, BnnDims dm,
-                                               nmx_eval_batch ev) {
+                                               nmx_eval_batch ev, const float* __restrict__ zr,
+                                               float* __restrict__ gr, int D) {
   extern __shared__ float sm[];
   const int N = dm.N, Dx = dm.Dx, H = dm.H;
   // XCD-aware position: blocks b, b+8, b+16, ... (one XCD) take consecutive positions
@@ -71,23 +116,23 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   float* gy = h2 + N * H;          // N     dU/dyhat
   float* red = gy + N;             // THREADS
 
-  const float* z = ev.z;
-  float* g = ev.grad;
-  const float u = z[c];
+  const float* z = zr + (size_t)pos * D;  // this chain's row
+  float* g = gr + (size_t)pos * D;
+  const float u = z[0];
   const float p = expf(u);
   float wsq = 0.0f;
   for (int i = t; i < Dx * H; i += THREADS) {
-    const float v = z[(size_t)(dm.o_w1 + i) * ldc + c];
+    const float v = z[dm.o_w1 + i];
     W1[i] = v;
     wsq += v * v;
   }
   for (int i = t; i < H * H; i += THREADS) {
-    const float v = z[(size_t)(dm.o_w2 + i) * ldc + c];
+    const float v = z[dm.o_w2 + i];
     W2[i] = v;
     wsq += v * v;
   }
   for (int i = t; i < H; i += THREADS) {
-    const float v = z[(size_t)(dm.o_w3 + i) * ldc + c];
+    const float v = z[dm.o_w3 + i];
     w3[i] = v;
     wsq += v * v;
   }
@@ -144,7 +189,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int j = t; j < H; j += THREADS) {
     float s = 0.0f;
     for (int n = 0; n < N; ++n) s += h2[n * H + j] * gy[n];
-    g[(size_t)(dm.o_w3 + j) * ldc + c] = w3[j] + s;
+    g[dm.o_w3 + j] = w3[j] + s;
   }
   __syncthreads();
   // ga2 = (gy w3^T) * (1 - h2^2)   (in place of h2)
@@ -177,7 +222,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
       for (int y = 0; y < 4; ++y)
         if (i0 + x < H && j0 + y < H) {
           const int ij = (i0 + x) * H + j0 + y;
-          g[(size_t)(dm.o_w2 + ij) * ldc + c] = W2[ij] + acc[x][y];
+          g[dm.o_w2 + ij] = W2[ij] + acc[x][y];
         }
   }
   __syncthreads();
@@ -216,7 +261,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     const int k = e / H, j = e % H;
     float s = 0.0f;
     for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[n * H + j];
-    g[(size_t)(dm.o_w1 + e) * ldc + c] = W1[e] + s;
+    g[dm.o_w1 + e] = W1[e] + s;
   }
 
   const float esq_t = block_sum256(esq, red);
@@ -229,7 +274,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     lp += 2.0f * u - p - 0.6931471805599453f + u;              // Gamma(3,1) at p (lgamma(3)=log 2) + log|J|
     lp += Nf * (0.5f * u - 0.5f * LOG_2PI) - 0.5f * p * esq_t;  // Normal(yhat, p^-1/2)
     ev.pe[c] = -lp;
-    g[c] = -(3.0f - p + 0.5f * Nf - 0.5f * p * esq_t);
+    g[0] = -(3.0f - p + 0.5f * Nf - 0.5f * p * esq_t);
   }
 }
 
@@ -239,10 +284,17 @@ size_t lds_bytes(int N, int Dx, int H) {
 
 }  // namespace
 
+extern "C" size_t nmx_pe_bnn_workspace_bytes(int Dx, int H, int num_chains) {
+  const size_t D = 1 + (size_t)Dx * H + (size_t)H * H + H;
+  const size_t ldc = (size_t)(num_chains + 63) / 64 * 64;
+  return 2 * ldc * D * sizeof(float);
+}
+
 extern "C" int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev,
-                          void* stream) {
+                          void* workspace, void* stream) {
   if (!ev || !ev->z || !ev->grad || !ev->pe || !X || !Y) return nmx_fail(NMX_ERR_INVALID, "bnn: NULL operand");
   if (N <= 0 || Dx <= 0 || H <= 0) return nmx_fail(NMX_ERR_INVALID, "bnn: bad sizes");
+  if (!workspace) return nmx_fail(NMX_ERR_INVALID, "bnn: NULL workspace (nmx_pe_bnn_workspace_bytes)");
   if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
     return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
   const size_t lds = lds_bytes(N, Dx, H);
@@ -253,6 +305,13 @@ extern "C" int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, 
     const hipError_t e = hipFuncSetAttribute((const void*)k_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "bnn: hipFuncSetAttribute: %s", hipGetErrorString(e));
   }
-  hipLaunchKernelGGL(k_bnn, dim3(ev->ldc), dim3(THREADS), lds, (hipStream_t)stream, X, Y, dm, *ev);
+  const int D = 1 + Dx * H + H * H + H;
+  float* zr = (float*)workspace;
+  float* gr = zr + (size_t)ev->ldc * D;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 tgrid((D + 63) / 64, ev->ldc / 64);
+  hipLaunchKernelGGL(k_cols_to_rows, tgrid, dim3(256), 0, s, ev->z, D, *ev, zr);
+  hipLaunchKernelGGL(k_bnn, dim3(ev->ldc), dim3(THREADS), lds, s, X, Y, dm, *ev, zr, gr, D);
+  hipLaunchKernelGGL(k_rows_to_cols, tgrid, dim3(256), 0, s, gr, D, *ev, ev->grad);
   return nmx_check_launch("k_bnn");
 }

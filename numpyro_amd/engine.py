@@ -144,7 +144,7 @@ class Engine:
         # dense mass: identity on the device (whitened coordinates), pooled on the host side
         c.adapt_mass_matrix = int(bool(o.adapt_mass_matrix) and not self.dense)
         c.regularize_mass_matrix = int(bool(o.regularize_mass_matrix))
-        c.dense_mass = 0
+        c.unit_mass = int(self.dense or (not o.adapt_mass_matrix and o.inverse_mass_matrix is None))
         c.sync_chains = int(self.sync_chains)
         c.target_accept_prob = float(o.target_accept_prob)
         c.max_delta_energy = float(o.max_delta_energy)

@@ -64,7 +64,7 @@ class NutsConfig(ctypes.Structure):
         ("iter_end", ctypes.c_int32), ("iter_begin", ctypes.c_int32),
         ("iter_capacity", ctypes.c_int32), ("adapt_step_size", ctypes.c_int32),
         ("adapt_mass_matrix", ctypes.c_int32), ("regularize_mass_matrix", ctypes.c_int32),
-        ("dense_mass", ctypes.c_int32), ("sync_chains", ctypes.c_int32),
+        ("unit_mass", ctypes.c_int32), ("sync_chains", ctypes.c_int32),
         ("target_accept_prob", ctypes.c_float), ("max_delta_energy", ctypes.c_float),
         ("trajectory_length", ctypes.c_float), ("num_steps", ctypes.c_int32),
         ("num_windows", ctypes.c_int32), ("window_end", ctypes.c_int32 * MAX_WINDOWS),
@@ -107,7 +107,8 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_pe_stochastic_volatility": (c_int, [c_vp, c_int, _evp, c_vp, c_vp]),
     "nmx_pe_funnel": (c_int, [c_int, _evp, c_vp, c_vp]),
     "nmx_pe_wide_workspace_bytes": (c_size, [c_int, c_int]),
-    "nmx_pe_bnn": (c_int, [c_vp, c_vp, c_int, c_int, c_int, _evp, c_vp]),
+    "nmx_pe_bnn": (c_int, [c_vp, c_vp, c_int, c_int, c_int, _evp, c_vp, c_vp]),
+    "nmx_pe_bnn_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "nmx_logreg_packed_bytes": (c_size, [c_i64, c_int]),
     "nmx_logreg_pack": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
     "nmx_logreg_workspace_bytes": (c_size, [c_i64, c_int, c_int]),

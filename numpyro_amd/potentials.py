@@ -204,10 +204,12 @@ class BNN(Potential):
     def _bind(self, C, ldc, device):
         self.X = _dev(self.X_in, device)
         self.Y = _dev(self.Y_in, device).reshape(-1)
+        self.workspace = torch.empty(lib().nmx_pe_bnn_workspace_bytes(self.Dx, self.H, C), dtype=torch.uint8,
+                                     device=device)
 
     def evaluate(self, ev, stream):
-        check(lib().nmx_pe_bnn(ptr(self.X), ptr(self.Y), self.N, self.Dx, self.H, ctypes.byref(ev), stream),
-              "nmx_pe_bnn")
+        check(lib().nmx_pe_bnn(ptr(self.X), ptr(self.Y), self.N, self.Dx, self.H, ctypes.byref(ev),
+                               ptr(self.workspace), stream), "nmx_pe_bnn")
 
     def flops_per_eval(self, num_chains):
         """Forward + adjoint: ~6 N H^2 + 6 N Dx H FLOPs per chain."""
