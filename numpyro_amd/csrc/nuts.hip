@@ -225,6 +225,7 @@ __device__ __forceinline__ void store_scalars(const Arena& a, int c, const Chain
 // Decisions of one step for one chain.
 struct Act {
   bool leaf, take_leaf, done_sub, take_biased, hmc_accept, iter_done, wf_update, finalize;
+  bool tree_chk;  // this leaf completes its subtree by size: the whole-tree U-turn dots are needed
   bool start_iter, prep_leaf, fin_done, fin_wait, div_new;
   int dirR, new_dir, k, j, imin, imax, slot, fin_t, wfn;
   float pe_eval, E_new, acc_new, w_new;
@@ -270,6 +271,7 @@ __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Aren
   A.k = (A.leaf && is_nuts) ? S.sub_n : 0;
   A.j = (A.leaf && is_nuts) ? S.depth : 0;
   if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);  // :1036
+  A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
   return ph;
 }
 
@@ -326,7 +328,10 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
     A.done_sub = (S.sub_n >= (1 << A.j)) || turning_sub || A.div_new;  // loop exit (:992-997)
     if (A.done_sub) {
       // _double_tree -> _combine_tree(..., biased_transition=True) (:936-938, :756-764)
-      const bool turning_tree = turning_sub || (tree(0) <= 0.0f) || (tree(1) <= 0.0f);
+      // the whole-tree check is only decisive when the subtree completed by size; a subtree
+      // stopped by a U-turn or a divergence ends the transition either way (tree.turning is
+      // internal state, not an output)
+      const bool turning_tree = turning_sub || (A.tree_chk && ((tree(0) <= 0.0f) || (tree(1) <= 0.0f)));
       float pb = expf(S.sub_w - S.tree_w);
       pb = isnan(pb) ? pb : fminf(pb, 1.0f);  // jnp.clip keeps NaN
       if (turning_sub || A.div_new) pb = 0.0f;
@@ -537,8 +542,10 @@ __device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t 
   x.ze = AV(NMX_F_Z_EVAL)[idx];
   if constexpr (NUTS) {
     x.rs_old = A.k == 0 ? 0.0f : AV(NMX_F_RSUM_SUB)[idx];
-    x.rst = AV(NMX_F_RSUM)[idx];
-    x.ro = (A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx];  // the other end's momentum
+    if (A.tree_chk) {
+      x.rst = AV(NMX_F_RSUM)[idx];
+      x.ro = (A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx];  // the other end's momentum
+    }
     // checkpoints read by the U-turn check; the range is empty for even leaves, whose
     // checkpoint write below therefore never feeds this step's check (:1036-1047)
 #pragma unroll
@@ -582,13 +589,15 @@ __device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float 
         red[2 + 2 * i] += (im * r) * rss;
       }
     }
-    // tentative whole-tree turning check with the tree's outer momenta (:795-799)
-    const float rst = x.rst + rs;
-    const float rlv = A.dirR ? x.ro : r;
-    const float rrv = A.dirR ? r : x.ro;
-    const float rss2 = rst - (rlv + rrv) / 2.0f;
-    red[1 + 2 * MAXD] += (im * rlv) * rss2;
-    red[2 + 2 * MAXD] += (im * rrv) * rss2;
+    // whole-tree turning check with the tree's outer momenta (:795-799), at subtree completion
+    if (A.tree_chk) {
+      const float rst = x.rst + rs;
+      const float rlv = A.dirR ? x.ro : r;
+      const float rrv = A.dirR ? r : x.ro;
+      const float rss2 = rst - (rlv + rrv) / 2.0f;
+      red[1 + 2 * MAXD] += (im * rlv) * rss2;
+      red[2 + 2 * MAXD] += (im * rrv) * rss2;
+    }
   }
 }
 
@@ -879,9 +888,11 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   A.leaf = ph == NMX_PH_LEAF;
   A.dirR = A.leaf ? AI(NMX_F_DIR)[c] : 0;
   A.k = (A.leaf && is_nuts) ? AI(NMX_F_SUB_N)[c] : 0;
+  A.j = (A.leaf && is_nuts) ? AI(NMX_F_DEPTH)[c] : 0;
   A.imin = 1;
   A.imax = 0;
   if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);
+  A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
   const float seff = A.leaf ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   float red[NPART];
@@ -902,8 +913,10 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
           *(part_ptr(a, ldc, s, 1 + 2 * i) + c) = red[1 + 2 * i];
           *(part_ptr(a, ldc, s, 2 + 2 * i) + c) = red[2 + 2 * i];
         }
-      *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c) = red[1 + 2 * MAXD];
-      *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c) = red[2 + 2 * MAXD];
+      if (A.tree_chk) {
+        *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c) = red[1 + 2 * MAXD];
+        *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c) = red[2 + 2 * MAXD];
+      }
     }
   }
 }
@@ -916,7 +929,7 @@ __device__ __forceinline__ bool entry_needed(const nmx_nuts_config& cfg, const A
   if (ph != NMX_PH_LEAF) return false;
   if (e == 0) return true;
   if (cfg.algo != NMX_ALGO_NUTS) return false;
-  if (e >= 1 + 2 * MAXD) return true;
+  if (e >= 1 + 2 * MAXD) return AI(NMX_F_SUB_N)[c] + 1 == (1 << AI(NMX_F_DEPTH)[c]);  // tree_chk
   int imin, imax;
   nmx_leaf_idx_to_ckpt_idxs(AI(NMX_F_SUB_N)[c], imin, imax);
   const int i = (e - 1) >> 1;
