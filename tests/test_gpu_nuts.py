@@ -20,11 +20,12 @@ from oracle import potentials as OP
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS", **kw):
+def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS", z0=None, **kw):
     o = H.NUTSOracle(lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)
                                      for v in pe_grad(z)),
                      dim, num_warmup, algo=algo, **kw)
-    z0 = philox.init_uniform(seed, chain, 0, dim)
+    if z0 is None:
+        z0 = philox.init_uniform(seed, chain, 0, dim)
     s = o.init(z0, seed, chain)
     out = []
     for _ in range(num_iters):
@@ -34,7 +35,7 @@ def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS",
 
 
 def _run_engine(model_args, model, num_chains, num_warmup, num_samples, seed, kernel_cls=NUTS,
-                sync=False, chain_offset=None, **kw):
+                sync=False, chain_offset=None, init_params=None, **kw):
     kernel = kernel_cls(model, **kw)
     mcmc = MCMC(kernel, num_warmup=num_warmup, num_samples=num_samples, num_chains=num_chains,
                 chain_method="vectorized", progress_bar=False, sync_chains=sync,
@@ -45,7 +46,7 @@ def _run_engine(model_args, model, num_chains, num_warmup, num_samples, seed, ke
         warm = mcmc.get_samples(group_by_chain=True), mcmc.get_extra_fields(group_by_chain=True)
     else:
         warm = ({}, {"num_steps": torch.zeros(num_chains, 0, dtype=torch.int32)})
-    mcmc.run(seed, *model_args,
+    mcmc.run(seed, *model_args, init_params=init_params,
              extra_fields=("num_steps", "accept_prob", "potential_energy", "adapt_state.step_size"))
     return mcmc, warm
 
@@ -86,46 +87,76 @@ def test_engine_matches_oracle_eight_schools(device, algo):
     assert match >= int(0.9 * C), f"only {match}/{C} chains reproduced the oracle path"
 
 
-@pytest.mark.parametrize("algo", ["NUTS", "HMC"])
-@pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300),
-                                       ("diag_normal", 1500)])
-def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
-    """No adaptation, fixed step size: every transition is a deterministic function of
-    the Philox stream; device and oracle must take the same discrete path.  dim 40 runs the
-    fused multi-wave step kernel (8 waves per 64 chains), dim 300 / 1500 the wide D-split
-    schedule (nmx_nuts_num_slices > 0; slice widths 32)."""
-    seed, C, T = 77, 64, 3
-    rs = np.random.RandomState(dim)
+def _fixed_step_case(model, dim, rs):
+    """(model args, fused model, oracle, checked site, oracle-z extractor, step, min match,
+    shared initial points or None for init_to_uniform)."""
     if model == "logreg":
         X = rs.randn(300, dim).astype(np.float32)
         beta = rs.randn(dim) * 0.5 / np.sqrt(dim)
         y = (rs.rand(300) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
-        args, fm = (X, y), P.logistic_regression
-        ref = OP.LogisticRegression(X, y, dtype=np.float32)
-        site = "coefs"
-        step = 0.02
-    else:
+        return (X, y), P.logistic_regression, OP.LogisticRegression(X, y, dtype=np.float32), "coefs", \
+            (lambda z: z), 0.02, 0.95, None
+    if model == "diag_normal":
         mu = rs.randn(dim).astype(np.float32)
         sd = (0.5 + rs.rand(dim)).astype(np.float32)
-        args, fm = (mu, sd), P.diag_normal
-        ref = OP.IsoNormal(mu, sd, dtype=np.float32)
-        site = "x"
-        step = 0.05
+        return (mu, sd), P.diag_normal, OP.IsoNormal(mu, sd, dtype=np.float32), "x", (lambda z: z), 0.05, 0.95, None
+    if model == "funnel":
+        return (dim,), P.funnel, OP.Funnel(dim, dtype=np.float32), "x", (lambda z: z[..., :-1]), 0.05, 0.9, None
+    if model == "sv":
+        r = datasets.sp500_synthetic(T=dim - 2)
+        return (r,), P.stochastic_volatility, OP.StochasticVolatility(r, dtype=np.float32), "s", \
+            (lambda z: z[..., 1:-1]), 0.005, 0.9, None
+    if model == "bnn":
+        H = {46: 5, 321: 16}[dim]
+        X, Y = datasets.bnn_data(N=30, D_X=3)
+        o = 1 + 3 * H
+        # shared well-conditioned start (small weights, prec ~ e): from U(-2, 2) the tanh
+        # layers saturate and |U| ~ 1e3, where fp32 energy rounding flips leaf choices
+        z0 = (0.3 * rs.randn(64, dim)).astype(np.float32)
+        z0[:, 0] = 1.0
+        return (X, Y, H), P.bnn, OP.BNN(X, Y, H, dtype=np.float32), "w2", \
+            (lambda z: z[..., o:o + H * H]), 0.01, 0.9, z0
+    raise ValueError(model)
+
+
+@pytest.mark.parametrize("algo", ["NUTS", "HMC"])
+@pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300),
+                                       ("diag_normal", 1500), ("funnel", 600), ("sv", 302),
+                                       ("bnn", 46), ("bnn", 321)])
+def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
+    """No adaptation, fixed step size: every transition is a deterministic function of
+    the Philox stream; device and oracle must take the same discrete path.  D < 257 runs the
+    fused step kernel (dim 40, 46: 8 waves per 64 chains), D >= 257 the wide D-split
+    schedule.  Funnel, SV and BNN check the fused potentials inside full trajectories; their
+    stiffer geometry lets fp32 rounding flip a few more decisions (>= 90% of chains)."""
+    seed, C, T = 77, 64, 3
+    rs = np.random.RandomState(dim)
+    args, fm, ref, site, extract, step, frac, z0 = _fixed_step_case(model, dim, rs)
+    if model == "bnn":
+        # BNN trees run 255-511 leapfrogs: tree sizes agree for every chain over 3
+        # transitions, but fp32 rounding grows along ~1000 chaotic leapfrogs, so the draws
+        # are compared over the first two (scripts/debug_bnn_parity.py prints the growth)
+        T = 2
     kcls = NUTS if algo == "NUTS" else HMC
     kw = dict(step_size=step, adapt_step_size=False, adapt_mass_matrix=False)
     if algo == "HMC":
         kw["trajectory_length"] = 15 * step
-    mcmc, warm = _run_engine(args, fm, C, 0, T, seed, kernel_cls=kcls, **kw)
+    mcmc, warm = _run_engine(args, fm, C, 0, T, seed, kernel_cls=kcls,
+                             init_params=None if z0 is None else torch.from_numpy(z0), **kw)
     ns_dev, sites = _dev_paths(mcmc, warm)
     match = 0
+    tol = dict(rtol=1e-3, atol=1e-3 if frac < 0.95 else 1e-4)
     for c in range(C):
-        states = _oracle_chain(ref.pe_grad, dim, seed, c, 0, T, algo=algo, **kw)
+        states = _oracle_chain(ref.pe_grad, dim, seed, c, 0, T, algo=algo,
+                               z0=None if z0 is None else z0[c], **kw)
         ns = np.array([s.num_steps for s in states])
-        if np.array_equal(ns, ns_dev[c]):
+        z = extract(np.stack([s.z for s in states]))
+        got = sites[site][c].reshape(z.shape)
+        # a chain is reproduced when its discrete path (tree sizes) AND its draws agree
+        # (a rounding flip in a leaf weight can change the proposal inside an equal-size tree)
+        if np.array_equal(ns, ns_dev[c]) and np.allclose(got, z, **tol):
             match += 1
-            z = np.stack([s.z for s in states])
-            np.testing.assert_allclose(sites[site][c], z, rtol=1e-3, atol=1e-4)
-    assert match >= int(0.95 * C), f"only {match}/{C} chains reproduced the oracle path"
+    assert match >= int(frac * C), f"only {match}/{C} chains reproduced the oracle path and draws"
 
 
 @pytest.mark.parametrize("model", ["logreg", "wide"])
