@@ -1,0 +1,133 @@
+"""Host-side API behaviour (no GPU): the numpyro-shaped constructors validate arguments like
+the reference (numpyro/infer/hmc.py:541-948, mcmc.py:224-330), fused models refuse direct
+calls, and the engine's host logic (adaptation schedule, fori_collect slot indexing,
+dense-mass window segmentation) follows numpyro."""
+import math
+
+import numpy as np
+import pytest
+
+from numpyro_amd import diagnostics
+from numpyro_amd import potentials as P
+from numpyro_amd.engine import Engine, build_adaptation_schedule
+from numpyro_amd.infer import HMC, MCMC, NUTS
+from oracle import hmc_ref as H
+
+
+def test_kernel_argument_validation():
+    with pytest.raises(ValueError):
+        NUTS()  # neither model nor potential_fn (hmc.py:570-571)
+    with pytest.raises(ValueError):
+        NUTS(P.eight_schools, potential_fn=P.DiagNormal([0.0], [1.0]))
+    with pytest.raises(ValueError):
+        HMC(P.eight_schools, num_steps=None, trajectory_length=None)
+    with pytest.raises(TypeError):
+        NUTS(lambda: None)  # arbitrary Python models cannot run on the device engine
+    with pytest.raises(TypeError):
+        NUTS(potential_fn=lambda z: z)
+    with pytest.raises(NotImplementedError):
+        NUTS(P.eight_schools, dense_mass=[("mu", "tau")])
+    with pytest.raises(NotImplementedError):
+        NUTS(P.eight_schools, kinetic_fn=lambda m, r: 0.0)
+    with pytest.warns(UserWarning):
+        HMC(P.eight_schools, num_steps=5, trajectory_length=1.0)  # hmc.py:595-599
+    k = NUTS(P.eight_schools, dense_mass=True, max_tree_depth=(8, 10), target_accept_prob=0.9)
+    o = k.options()
+    assert o.dense_mass and o.max_tree_depth == (8, 10) and o.target_accept_prob == 0.9
+    assert k.sample_field == "z" and "diverging" in k.default_fields
+
+
+def test_mcmc_argument_validation():
+    k = NUTS(P.eight_schools)
+    with pytest.raises(ValueError):
+        MCMC(k, num_warmup=10, num_samples=10, thinning=0)
+    with pytest.raises(ValueError):
+        MCMC(k, num_warmup=10, num_samples=10, chain_method="pmap")
+    m = MCMC(k, num_warmup=10, num_samples=10, num_chains=7, chain_method="vectorized")
+    assert (m.chain_lo, m.chain_hi, m.local_chains) == (0, 7, 7)
+    m = MCMC(k, num_warmup=10, num_samples=10, num_chains=5, chain_offset=40)
+    assert (m.chain_lo, m.chain_hi) == (40, 45)
+
+
+def test_fused_model_is_not_callable():
+    with pytest.raises(TypeError):
+        P.eight_schools(8, np.ones(8), np.zeros(8))
+    pot = P.eight_schools.potential(8, np.ones(8), np.zeros(8))
+    assert pot.dim == 10 and [n for n, _, _ in pot.sites] == ["mu", "tau", "theta"]
+
+
+def test_potential_site_metadata_follows_ravel_order():
+    sv = P.StochasticVolatility(np.ones(20, np.float32))
+    assert [n for n, _, _ in sv.sites] == ["nu", "s", "sigma"] and sv.dim == 22
+    bnn = P.BNN(np.ones((10, 3), np.float32), np.ones((10, 1), np.float32), 4)
+    assert [n for n, _, _ in bnn.sites] == ["prec_obs", "w1", "w2", "w3"]
+    assert bnn.dim == 1 + 12 + 16 + 4
+    f = P.Funnel(7)
+    flat = np.arange(2 * 7, dtype=np.float32).reshape(2, 7)
+    out = f.unflatten(flat)
+    assert out["x"].shape == (2, 6) and out["y"].shape == (2,)
+    np.testing.assert_array_equal(out["y"], flat[:, -1])
+
+
+@pytest.mark.parametrize("n", [0, 1, 10, 19, 20, 30, 149, 150, 500, 1000, 2345])
+def test_adaptation_schedule_matches_oracle(n):
+    if n == 0:
+        return
+    assert build_adaptation_schedule(n) == H.build_adaptation_schedule(n)
+
+
+def test_fori_collect_slots():
+    """numpyro/util.py:330-346: slot (i - start) // thinning, the last write wins."""
+    N, lower, thin = 23, 5, 4
+    start = lower + (N - lower) % thin
+    S = (N - lower) // thin
+    slots = {}
+    for i in range(N):
+        k = Engine._slot_of(i, start, thin, S)
+        if k >= 0:
+            slots[k] = i
+    ref = {}
+    for i in range(N):  # the reference loop: every i >= start writes its slot
+        if i >= start:
+            ref[(i - start) // thin] = i
+    assert slots == {k: v for k, v in ref.items() if k < S}
+
+
+def test_dense_segments_split_at_middle_window_ends():
+    class Fake:
+        num_warmup = 1000
+
+        class opts:
+            adapt_mass_matrix = True
+
+    segs = Engine._dense_segments(Fake(), 0, 2000)
+    sched = build_adaptation_schedule(1000)
+    middle = [(a, b + 1) for a, b in sched[1:-1]]
+    assert [(a, b) for a, b, m in segs if m] == middle
+    assert segs[0] == (0, 75, False) and segs[-1] == (950, 2000, False)
+    # contiguous cover
+    assert all(segs[i][1] == segs[i + 1][0] for i in range(len(segs) - 1))
+    Fake.opts.adapt_mass_matrix = False
+    assert Engine._dense_segments(Fake(), 0, 2000) == [(0, 2000, False)]
+
+
+def test_host_diagnostics_known_values():
+    rs = np.random.RandomState(0)
+    iid = rs.randn(4, 4000)
+    ess = diagnostics.effective_sample_size(iid)
+    assert 0.8 * 16000 < ess < 1.25 * 16000
+    assert abs(diagnostics.split_gelman_rubin(iid) - 1.0) < 0.01
+    phi = 0.9
+    x = np.zeros((4, 20000))
+    x[:, 0] = rs.randn(4)
+    e = rs.randn(4, 20000)
+    for t in range(1, 20000):
+        x[:, t] = phi * x[:, t - 1] + e[:, t]
+    ess_ar = diagnostics.effective_sample_size(x)
+    expected = 80000 * (1 - phi) / (1 + phi)  # AR(1) integrated autocorrelation time
+    assert 0.7 * expected < ess_ar < 1.3 * expected
+    shifted = np.concatenate([iid[:2], iid[2:] + 3.0])
+    assert diagnostics.split_gelman_rubin(shifted) > 1.5
+    lo, hi = diagnostics.hpdi(rs.randn(100000), prob=0.9)
+    np.testing.assert_allclose([lo, hi], [-1.645, 1.645], atol=0.05)
+    assert math.isclose(float(diagnostics.autocorrelation(np.arange(10.0))[0]), 1.0)
