@@ -529,7 +529,7 @@ struct VecCtx {
 // Split into a load stage and a compute/store stage so that several rows' loads are in
 // flight before the (possibly aliasing, from the compiler's view) stores.
 struct LeafIn {
-  float g, rf, im, ze, rs_old, rst, ro;
+  float g, rf, im, rs_old, rst, ro;
   float ckr[MAXD], ckrs[MAXD];
 };
 
@@ -539,7 +539,6 @@ __device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t 
   x.g = AV(NMX_F_G_EVAL)[idx];
   x.rf = (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
   x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
-  x.ze = AV(NMX_F_Z_EVAL)[idx];
   if constexpr (NUTS) {
     x.rs_old = A.k == 0 ? 0.0f : AV(NMX_F_RSUM_SUB)[idx];
     if (A.tree_chk) {
@@ -566,8 +565,8 @@ __device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float 
   const float half = 0.5f * es;
   const float r = x.rf - half * x.g;
   (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = r;
-  (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = x.ze;
-  (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = x.g;
+  // the moving end's z / grad stay in Z_EVAL / G_EVAL (the frontier); apply_store saves
+  // them into the side arrays only when the next doubling turns around
   const float im = x.im;
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
@@ -628,22 +627,27 @@ __device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float s
 // (L3/L4), then the momentum draw + tree init or the next half step and z_eval (L5/L6,
 // velocity_verlet first half, hmc_util.py:297-301).  Load stage first (values the
 // stores below would otherwise serialise behind), then compute/store.
+// Frontier layout: Z_EVAL / G_EVAL hold the moving end of the trajectory (the leaf just
+// evaluated); the side arrays Z{L,R} / G{L,R} hold only the end the tree is NOT growing
+// from.  R{L,R} hold both ends' momenta.  A turn-around (new doubling direction differs from
+// the last leaf's) parks the frontier in its side arrays and loads the other end.
 struct ApplyIn {
-  float zf, gf;     // old frontier (take_leaf)
+  float ze, ge;     // frontier = the leaf just evaluated (take_leaf, hmc_accept, prep_leaf)
   float rst, rss;   // tree / subtree r_sum (done_sub)
   float zs, gs;     // subtree proposal (take_biased)
-  float zr, gr;     // HMC end point
   float zp, gp;     // state
   float wm, w2;     // Welford
   float ms, im;     // mass
-  float zfn, rfn, gfn;  // new frontier (prep_leaf)
+  float zfn, rfn, gfn;  // the end the next leaf grows from (prep_leaf)
 };
+
+__device__ __forceinline__ bool turn_around(const Act& A) { return A.prep_leaf && A.new_dir != A.dirR; }
 
 __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t idx, ApplyIn& x) {
   const Arena& a = *v.a;
-  if (A.take_leaf) {
-    x.zf = (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
-    x.gf = (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+  if (A.take_leaf || A.hmc_accept || A.prep_leaf) {
+    x.ze = AV(NMX_F_Z_EVAL)[idx];
+    x.ge = AV(NMX_F_G_EVAL)[idx];
   }
   if (A.done_sub) {
     x.rst = AV(NMX_F_RSUM)[idx];
@@ -652,10 +656,6 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t
   if (A.take_biased && !A.take_leaf) {
     x.zs = AV(NMX_F_ZSUB)[idx];
     x.gs = AV(NMX_F_GSUB)[idx];
-  }
-  if (A.hmc_accept) {
-    x.zr = AV(NMX_F_ZR)[idx];
-    x.gr = AV(NMX_F_GR)[idx];
   }
   const bool need_state = (A.iter_done || A.start_iter) && !A.take_biased && !A.hmc_accept;
   if (need_state) {
@@ -670,9 +670,14 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t
   if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
   if (A.prep_leaf) {
     const int nd = A.new_dir;
-    x.zfn = (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
     x.rfn = (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
-    x.gfn = (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+    if (turn_around(A)) {
+      x.zfn = (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
+      x.gfn = (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+    } else {
+      x.zfn = x.ze;
+      x.gfn = x.ge;
+    }
   }
 }
 
@@ -682,10 +687,10 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
                                              const nmx_nuts_config& cfg) {
   const Arena& a = *v.a;
   if (A.take_leaf) {
-    AV(NMX_F_ZSUB)[idx] = x.zf;
-    AV(NMX_F_GSUB)[idx] = x.gf;
-    x.zs = x.zf;
-    x.gs = x.gf;
+    AV(NMX_F_ZSUB)[idx] = x.ze;
+    AV(NMX_F_GSUB)[idx] = x.ge;
+    x.zs = x.ze;
+    x.gs = x.ge;
   }
   if (A.done_sub) AV(NMX_F_RSUM)[idx] = x.rst + x.rss;
   if (A.take_biased) {
@@ -695,10 +700,10 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
     x.gp = x.gs;
   }
   if (A.hmc_accept) {
-    AV(NMX_F_Z)[idx] = x.zr;
-    AV(NMX_F_ZGRAD)[idx] = x.gr;
-    x.zp = x.zr;
-    x.gp = x.gr;
+    AV(NMX_F_Z)[idx] = x.ze;
+    AV(NMX_F_ZGRAD)[idx] = x.ge;
+    x.zp = x.ze;
+    x.gp = x.ge;
   }
   float im = x.im;
   if (A.iter_done) {
@@ -741,15 +746,18 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       const float g = x.gp;
       ke0 = (im * r) * r;
       AV(NMX_F_RSUM)[idx] = r;
+      // both ends start at z; only the fixed end goes to the side arrays
       (nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR))[idx] = z;
       (nd ? AV(NMX_F_GL) : AV(NMX_F_GR))[idx] = g;
       (nd ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx] = r;
-      (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = z;
-      (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = g;
       const float rh = r - half * g;
       (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
       ZE[idx] = z + es * (im * rh);
     } else {
+      if (turn_around(A)) {
+        (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = x.ze;
+        (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = x.ge;
+      }
       const float rh = x.rfn - half * x.gfn;
       (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
       ZE[idx] = x.zfn + es * (im * rh);
