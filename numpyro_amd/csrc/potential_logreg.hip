@@ -23,6 +23,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "nmx_api_internal.h"
 #include "nmx_common.h"
 
@@ -64,6 +66,33 @@ __global__ void k_logreg_pack(const float* X, const float* y, int64_t n, int D, 
     else if (k == XS - 1) v = y[row];
   }
   out[i] = v;
+}
+
+// w[d] = sum_n X[n,d] / 2 - sum_n y_n X[n,d] in float64 (the per-chain linear part of U used
+// by epilogue_abs).  One workgroup per column, fixed thread count and a fixed-order tree, so
+// the value does not depend on anything but the data.
+constexpr int CS_THREADS = 256;
+__global__ __launch_bounds__(CS_THREADS) void k_logreg_colsums(const float* X, const float* y, int64_t n, int D,
+                                                              double* w) {
+  __shared__ double red[CS_THREADS];
+  const int d = blockIdx.x;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += CS_THREADS) {
+    const double x = X[i * D + d];
+    acc += 0.5 * x - (double)y[i] * x;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = CS_THREADS / 2; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) w[d] = red[0];
+}
+
+// byte offset of the float64 column terms behind the packed rows
+inline size_t colterm_offset(int64_t n_rows, int dim) {
+  return ((size_t)npad_of(n_rows) * xs_of(dim) * sizeof(float) + 255) / 256 * 256;
 }
 
 // KS = K/2 MFMA k-steps.  EXACT: the dim's KS equals the template (compile-time strides);
@@ -215,8 +244,10 @@ __device__ __forceinline__ void epilogue(const float* xt, int h, int64_t rowbase
     const float ope = 1.0f + e;
     const float inv = __builtin_amdgcn_rcpf(ope);
     const float num = l >= 0.0f ? 1.0f : e;
-    float res = num * inv - y;
-    float li = fmaxf(l, 0.0f) - l * y;
+    // explicit fmas: the rounding must not depend on how the compiler contracts (kernel
+    // variants compute bitwise the same values)
+    float res = __builtin_fmaf(num, inv, -y);
+    float li = __builtin_fmaf(-l, y, fmaxf(l, 0.0f));
     float lo = __builtin_amdgcn_logf(ope);
     if (MASK) {
       const bool ok = rowbase + rr < n_rows;
@@ -228,6 +259,75 @@ __device__ __forceinline__ void epilogue(const float* xt, int h, int64_t rowbase
     lg2 += lo;
     acc[r] = res;
   }
+}
+
+// Same as epilogue(), with sum(log2(1+e)) taken as log2 of the product of the 16 factors
+// (each in [1, 2], so the product stays below 2^16): one v_log per 16 rows instead of 16.
+// The product rounds 16 times (<= ~1e-6 relative, ~1e-6 absolute after the log) -- far below
+// the f32 rounding of U itself (|U| ~ 1e5); the gradient path is unchanged.
+template <int KS, bool MASK>
+__device__ __forceinline__ void epilogue_prod(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
+                                              float& lin, float& lg2) {
+  constexpr int XS = 2 * KS + 1;
+  float prod = 1.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float y = xt[rr * XS + (XS - 1)];
+    const float l = acc[r];
+    const float e = __builtin_amdgcn_exp2f(-fabsf(l) * LOG2E);
+    float ope = 1.0f + e;
+    const float inv = __builtin_amdgcn_rcpf(ope);
+    const float num = l >= 0.0f ? 1.0f : e;
+    // explicit fmas: the rounding must not depend on how the compiler contracts (kernel
+    // variants compute bitwise the same values)
+    float res = __builtin_fmaf(num, inv, -y);
+    float li = __builtin_fmaf(-l, y, fmaxf(l, 0.0f));
+    if (MASK) {
+      const bool ok = rowbase + rr < n_rows;
+      res = ok ? res : 0.0f;
+      li = ok ? li : 0.0f;
+      ope = ok ? ope : 1.0f;
+    }
+    lin += li;
+    prod *= ope;
+    acc[r] = res;
+  }
+  lg2 += __builtin_amdgcn_logf(prod);
+}
+
+// epilogue_prod plus the linear part taken out of the row loop: with
+//   max(l,0) - l y = (|l| + l)/2 - l y,   sum_n l_n = (sum_n x_n) . b,   sum_n l_n y_n = (X^T y) . b,
+// the rows only accumulate |l| and the chain adds w . b once, w = sum_n x_n / 2 - X^T y
+// (k_logreg_colsums, float64).  4 VALU ops per row fewer; the gradient path is unchanged.
+template <int KS, bool MASK>
+__device__ __forceinline__ void epilogue_abs(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
+                                             float& lin, float& lg2) {
+  constexpr int XS = 2 * KS + 1;
+  float prod = 1.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float y = xt[rr * XS + (XS - 1)];
+    const float l = acc[r];
+    float al = fabsf(l);
+    const float e = __builtin_amdgcn_exp2f(-al * LOG2E);
+    float ope = 1.0f + e;
+    const float inv = __builtin_amdgcn_rcpf(ope);
+    const float num = l >= 0.0f ? 1.0f : e;
+    float res = __builtin_fmaf(num, inv, -y);
+    if (MASK) {
+      const bool ok = rowbase + rr < n_rows;
+      res = ok ? res : 0.0f;
+      al = ok ? al : 0.0f;
+      ope = ok ? ope : 1.0f;
+    }
+    lin += al;
+    prod *= ope;
+    acc[r] = res;
+  }
+  lin *= 0.5f;
+  lg2 += __builtin_amdgcn_logf(prod);
 }
 
 template <int KS>
@@ -484,8 +584,203 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_wavepipe(const floa
   }
 }
 
+// Row lanes with CT chain tiles per wave: every X operand read from LDS feeds CT MFMAs, and
+// each stage's load + barrier is amortised over CT x the matrix work.  Per chain the MFMA
+// sequence (rows, k order, lanes) is the one of k_logreg_rowlanes, so the sums are bitwise
+// the same; only the grouping of chains into workgroups differs (ct = 64-chain group).
+template <int KS, int CT, bool PRIO, bool ILP, int EPI>
+__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const float* __restrict__ Xp,
+                                                                         int64_t n_rows, int nstages, int D, int S,
+                                                                         int Gt, nmx_eval_batch ev,
+                                                                         float* __restrict__ gpart,
+                                                                         double* __restrict__ pepart) {
+  constexpr int XS = 2 * KS + 1;
+  constexpr int STAGE = RL_ROWS * XS;
+  constexpr int CHUNKS = STAGE / 4;
+  constexpr int NINST = (CHUNKS + 63) / 64;
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7;
+  const int q = b >> 3;
+  const int ct = q % Gt;
+  const int split = (q / Gt) * 8 + xcd;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  int cc[CT];
+  bool any = false;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int pos = (ct * CT + t) * 32 + l31;
+    cc[t] = pos < ldc ? nmx_eval_chain(ev, pos) : -1;
+    any |= cc[t] >= 0;
+  }
+  if (!__any(any)) return;  // identical in all waves of the workgroup
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Xp, 0, nstages * STAGE * 4, 0x00020000);
+
+  const int per = (nstages + S - 1) / S;
+  const int t0 = split * per;
+  const int t1 = min(t0 + per, nstages);
+
+  float zb[CT][KS];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 2 * s + h;
+      zb[t][s] = (k < D && cc[t] >= 0) ? ev.z[(size_t)k * ldc + cc[t]] : 0.0f;
+    }
+  f32x16 g0[CT], g1[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      g0[t][r] = 0.0f;
+      g1[t][r] = 0.0f;
+    }
+  double pe[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) pe[t] = 0.0;
+  // TAIL: the stage holds rows >= n_rows (only the last one can): masked epilogue
+  auto stage = [&](int st, auto tailc) {
+    constexpr bool TAIL = decltype(tailc)::value;
+    {
+      // buffer LDS-DMA: scalar descriptor + stage offset, one 32-bit lane offset; the last
+      // piece's lanes past the stage read the next stage (or 0 past the end, range check)
+      // into the LDS slack
+#pragma unroll
+      for (int j = 0; j < (NINST + RL_WAVES - 1) / RL_WAVES; ++j) {
+        const int i = wu + j * RL_WAVES;
+        if (i < NINST)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              xrs, (__attribute__((address_space(3))) void*)(xs + i * 256), 16, lane * 16,
+              (unsigned)(st * STAGE * 4 + i * 1024), 0, 0);
+      }
+    }
+    __syncthreads();
+    const float* xt = xs + w * 32 * XS;
+    const int64_t rb = (int64_t)st * RL_ROWS + w * 32;
+    f32x16 a[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[t][r] = 0.0f;
+    auto epi = [&](int t) {
+      float lin = 0.0f, lg2 = 0.0f;
+      // per wave, as in k_logreg_rowlanes: only the waves holding rows >= n_rows mask
+      if constexpr (EPI == 2) {
+        if (TAIL && rb + 32 > n_rows) epilogue_abs<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
+        else epilogue_abs<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
+      } else if constexpr (EPI == 1) {
+        if (TAIL && rb + 32 > n_rows) epilogue_prod<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
+        else epilogue_prod<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
+      } else {
+        if (TAIL && rb + 32 > n_rows) epilogue<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
+        else epilogue<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
+      }
+      pe[t] += (double)lin + (double)lg2 * (double)LN2;
+    };
+    auto g1_tile = [&](int t) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        a[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[t][s], a[t], 0, 0, 0);
+    };
+    auto g2_tile = [&](int t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        g0[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], a[t][r], g0[t], 0, 0, 0);
+        if (KS > 16) g1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], a[t][r], g1[t], 0, 0, 0);
+      }
+    };
+    if constexpr (ILP) {
+      // tile t's epilogue (VALU) is independent of tile t+1's GEMM1 and of tile t-1's GEMM2:
+      // issue them side by side so the vector work runs in the MFMAs' shadow
+      static_assert(CT == 2, "ILP schedule pairs two chain tiles");
+      g1_tile(0);
+      g1_tile(1);
+      epi(0);
+      g2_tile(0);
+      epi(1);
+      g2_tile(1);
+    } else {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float x = xt[l31 * XS + 2 * s + h];
+#pragma unroll
+        for (int t = 0; t < CT; ++t) a[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, zb[t][s], a[t], 0, 0, 0);
+      }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+      for (int t = 0; t < CT; ++t) epi(t);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float x0 = xt[rr * XS + l31];
+        const float x1 = xt[rr * XS + 32 + l31];
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+          g0[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, a[t][r], g0[t], 0, 0, 0);
+          if (KS > 16) g1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, a[t][r], g1[t], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
+  };
+  const int t_full = (int)min((int64_t)t1, n_rows / RL_ROWS);  // stages with all 128 rows < n_rows
+  int st = t0;
+  for (; st < t_full; ++st) stage(st, std::false_type{});
+  for (; st < t1; ++st) stage(st, std::true_type{});
+
+  // fixed-order combination of the 4 row lanes, one chain tile at a time
+  float* red = xs;                                                      // [RL_WAVES][32][64]
+  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const double p = pe[t] + __shfl_xor(pe[t], 32);
+    const int pos = (ct * CT + t) * 32 + l31;
+    if (t > 0) __syncthreads();  // the previous tile's reads are done
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      red[(w * 32 + r) * 64 + lane] = g0[t][r];
+      red[(w * 32 + 16 + r) * 64 + lane] = g1[t][r];
+    }
+    red_pe[w * 64 + lane] = p;
+    __syncthreads();
+    if (w == 0 && pos < ldc) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
+#pragma unroll
+        for (int ww = 1; ww < RL_WAVES; ++ww) {
+          s0 += red[(ww * 32 + r) * 64 + lane];
+          s1 += red[(ww * 32 + 16 + r) * 64 + lane];
+        }
+        const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
+        if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
+      }
+      if (h == 0) {
+        double sp = red_pe[lane];
+#pragma unroll
+        for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
+        pepart[(size_t)split * ldc + pos] = sp;
+      }
+    }
+  }
+}
+
+// wcol (epilogue_abs variants): U gains the per-chain linear term w . b
 __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
-                                  int D, nmx_eval_batch ev) {
+                                  int D, nmx_eval_batch ev, const double* __restrict__ wcol) {
   const int pos = blockIdx.x * blockDim.x + threadIdx.x;
   const int d = blockIdx.y;
   const int c = nmx_eval_chain(ev, pos);
@@ -499,12 +794,13 @@ __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double*
   } else {
     double s = 0.0;
     for (int sp = 0; sp < S; ++sp) s += pepart[(size_t)sp * ldc + pos];
-    double zz = 0.0;
+    double zz = 0.0, wz = 0.0;
     for (int k = 0; k < D; ++k) {
       const double z = ev.z[(size_t)k * ldc + c];
       zz += z * z;
+      if (wcol) wz += wcol[k] * z;
     }
-    ev.pe[c] = (float)(s + 0.5 * zz + 0.9189385332046727 * D);
+    ev.pe[c] = (float)(s + wz + 0.5 * zz + 0.9189385332046727 * D);
   }
 }
 
@@ -515,14 +811,23 @@ int check_ev(const nmx_eval_batch* ev) {
   return NMX_OK;
 }
 
-// Kernel variant (A/B experiments; all give the same sums in the same order):
-//   11 (default) row lanes, single stage buffer, s_setprio around the MFMA chains
-//    5 same without s_setprio;  4 double-buffered stages;  8 barrier-free wave pipeline
-//    0 generic tile kernel.
-// Measured at C=4096 (profiles/r01): 11: 103.9, 5: 103.0, 8: 101.6, 4: 98.2 TFLOP/s.
+// Kernel variant (A/B experiments).  The gradient is bitwise the same in all row-lane forms
+// (same MFMA sequence per chain, explicit fmas in the epilogue); 17-19 round U differently
+// (product-of-factors log, |l| sums + w.b) at ~1e-7 relative.
+//   19 (default) k_logreg_rowlanes_ct, 1 chain tile, buffer LDS-DMA, peeled tail stage
+//      (124 VGPRs -> 4 waves/SIMD), s_setprio, epilogue_abs
+//   17 / 18  same with epilogue_prod, with / without s_setprio
+//   14 / 16  same with the plain epilogue, with / without s_setprio
+//   12 / 13  two chain tiles per wave (256 / 248 VGPRs, 2 waves/SIMD), 15 = 13 with the two
+//            tiles' epilogues scheduled beside the other tile's MFMAs
+//   11 k_logreg_rowlanes (global_load_lds, 177 VGPRs, 2 waves/SIMD), 5 without s_setprio,
+//    4 double-buffered stages, 8 barrier-free wave pipeline, 0 generic tile kernel.
+// Measured at C=4096 (scripts/bench_potential.py, MI355X): 19: 116.5, 17: 112.9,
+// 14: 109.8, 16: 109.4, 11: 103.5, 13: 103.0, 15: 102.9, 12: 97.0 TFLOP/s; earlier: 5: 103.0,
+// 8: 101.6, 4: 98.2.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
-  return e ? atoi(e) : 11;
+  return e ? atoi(e) : 19;
 }
 
 template <int KS, int NBUF, bool PRIO>
@@ -537,6 +842,20 @@ void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batc
   if (lds < red) lds = red;
   hipLaunchKernelGGL((k_logreg_rowlanes<KS, NBUF, PRIO>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages,
                      D, S, Gt, *ev, gpart, pepart);
+}
+
+template <int KS, int CT, bool PRIO, bool ILP = false, int EPI = 0>
+void launch_rowlanes_ct(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
+                        double* pepart, hipStream_t s) {
+  const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
+  const int S = num_splits(n_rows);
+  const int Gt = ev->ldc / (32 * CT);  // ldc % 64 == 0 (check_ev)
+  constexpr int BUF = (RL_ROWS * (2 * KS + 1) + LDS_SLACK + 255) / 256 * 256;
+  size_t lds = (size_t)BUF * sizeof(float);
+  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
+  if (lds < red) lds = red;
+  hipLaunchKernelGGL((k_logreg_rowlanes_ct<KS, CT, PRIO, ILP, EPI>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows,
+                     nstages, D, S, Gt, *ev, gpart, pepart);
 }
 
 template <int KS>
@@ -570,7 +889,7 @@ extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return num_splits(n_rows)
 
 extern "C" size_t nmx_logreg_packed_bytes(int64_t n_rows, int dim) {
   if (n_rows <= 0 || dim <= 0) return 0;
-  return (size_t)npad_of(n_rows) * xs_of(dim) * sizeof(float);
+  return colterm_offset(n_rows, dim) + 64 * sizeof(double);  // rows, then w[64] (k_logreg_colsums)
 }
 
 extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, int dim, void* packed,
@@ -584,7 +903,10 @@ extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, i
   const int64_t total = npad * XS;
   hipLaunchKernelGGL(k_logreg_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      X, y, n_rows, dim, XS, npad, (float*)packed);
-  return nmx_check_launch("k_logreg_pack");
+  if (int st = nmx_check_launch("k_logreg_pack")) return st;
+  hipLaunchKernelGGL(k_logreg_colsums, dim3(dim), dim3(CS_THREADS), 0, (hipStream_t)stream, X, y, n_rows, dim,
+                     (double*)((char*)packed + colterm_offset(n_rows, dim)));
+  return nmx_check_launch("k_logreg_colsums");
 }
 
 extern "C" size_t nmx_logreg_workspace_bytes(int64_t n_rows, int dim, int num_chains) {
@@ -609,16 +931,27 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
+  const bool epi_abs = KS == 28 && var == 19;
   if (KS == 28 && var == 4) launch_rowlanes<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
   else if (KS == 28 && var == 5) launch_rowlanes<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28 && var == 8) launch_wavepipe<28>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28 && var == 11) launch_rowlanes<28, 1, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 12) launch_rowlanes_ct<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 13) launch_rowlanes_ct<28, 2, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 14) launch_rowlanes_ct<28, 1, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 15) launch_rowlanes_ct<28, 2, false, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 16) launch_rowlanes_ct<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 17) launch_rowlanes_ct<28, 1, true, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 18) launch_rowlanes_ct<28, 1, false, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 19) launch_rowlanes_ct<28, 1, true, false, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 16) launch_tiles<16, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else launch_tiles<32, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   if (int st = nmx_check_launch("k_logreg_tiles")) return st;
-  hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S, dim, *ev);
+  const double* wcol = epi_abs ? (const double*)((const char*)packed + colterm_offset(n_rows, dim)) : nullptr;
+  hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S, dim, *ev,
+                     wcol);
   return nmx_check_launch("k_logreg_finalize");
 }

@@ -251,11 +251,14 @@ def test_logreg_kernel_variants_agree(device, monkeypatch):
     y = (rs.rand(N) < 0.3).astype(np.float32)
     Z = (rs.randn(C, D) * 0.2).astype(np.float32)
     out = {}
-    for v in ("11", "5", "4", "8"):
+    for v in ("11", "5", "4", "8", "12", "13", "14", "15", "16", "17", "18", "19"):
         monkeypatch.setenv("NMX_LOGREG_VARIANT", v)
         out[v] = _eval(LogisticRegression(X, y), Z, device)
-    for v in ("5", "4"):
-        np.testing.assert_array_equal(out[v][0], out["11"][0])
-        np.testing.assert_array_equal(out[v][1], out["11"][1])
+    for v in ("5", "4", "12", "13", "14", "15", "16"):
+        np.testing.assert_array_equal(out[v][0], out["11"][0], err_msg=v)
+        np.testing.assert_array_equal(out[v][1], out["11"][1], err_msg=v)
+    for v in ("17", "18", "19"):  # product-of-factors log / |l| sums: U to ~1e-6 relative, grad bitwise
+        np.testing.assert_allclose(out[v][0], out["11"][0], rtol=1e-6, err_msg=v)
+        np.testing.assert_array_equal(out[v][1], out["11"][1], err_msg=v)
     np.testing.assert_allclose(out["8"][0], out["11"][0], rtol=1e-6)
     np.testing.assert_allclose(out["8"][1], out["11"][1], rtol=1e-5, atol=1e-3)
