@@ -330,6 +330,38 @@ __device__ __forceinline__ void epilogue_abs(const float* xt, int h, int64_t row
   lg2 += __builtin_amdgcn_logf(prod);
 }
 
+// epilogue_abs on m = -l log2(e) (z pre-scaled in GEMM1): e = 2^-|m| straight from the
+// accumulator (no multiply); lin collects |m| / 2 (the caller scales by ln 2).
+template <int KS, bool MASK>
+__device__ __forceinline__ void epilogue_log2(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
+                                              float& lin, float& lg2) {
+  constexpr int XS = 2 * KS + 1;
+  float prod = 1.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float y = xt[rr * XS + (XS - 1)];
+    const float m = acc[r];
+    float am = fabsf(m);
+    const float e = __builtin_amdgcn_exp2f(-am);
+    float ope = 1.0f + e;
+    const float inv = __builtin_amdgcn_rcpf(ope);
+    const float num = m <= 0.0f ? 1.0f : e;
+    float res = __builtin_fmaf(num, inv, -y);
+    if (MASK) {
+      const bool ok = rowbase + rr < n_rows;
+      res = ok ? res : 0.0f;
+      am = ok ? am : 0.0f;
+      ope = ok ? ope : 1.0f;
+    }
+    lin += am;
+    prod *= ope;
+    acc[r] = res;
+  }
+  lin *= 0.5f;
+  lg2 += __builtin_amdgcn_logf(prod);
+}
+
 template <int KS>
 __device__ __forceinline__ void gemm2(const float* xt, const f32x16& res, int l31, int h, f32x16& g0, f32x16& g1) {
   constexpr int XS = 2 * KS + 1;
@@ -588,8 +620,8 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_wavepipe(const floa
 // each stage's load + barrier is amortised over CT x the matrix work.  Per chain the MFMA
 // sequence (rows, k order, lanes) is the one of k_logreg_rowlanes, so the sums are bitwise
 // the same; only the grouping of chains into workgroups differs (ct = 64-chain group).
-template <int KS, int CT, bool PRIO, bool ILP, int EPI>
-__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const float* __restrict__ Xp,
+template <int KS, int CT, bool PRIO, bool ILP, int EPI, bool WAVE, int MINB>
+__global__ __launch_bounds__(RL_WAVES * 64, MINB) void k_logreg_rowlanes_ct(const float* __restrict__ Xp,
                                                                          int64_t n_rows, int nstages, int D, int S,
                                                                          int Gt, nmx_eval_batch ev,
                                                                          float* __restrict__ gpart,
@@ -598,6 +630,8 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
   constexpr int STAGE = RL_ROWS * XS;
   constexpr int CHUNKS = STAGE / 4;
   constexpr int NINST = (CHUNKS + 63) / 64;
+  constexpr int WPIECES = (32 * XS + 255) / 256;  // 1 KB DMA pieces per wave subtile
+  constexpr int WSLICE = WPIECES * 256;           // floats per wave slice
   extern __shared__ __attribute__((aligned(16))) float xs[];
   const int b = blockIdx.x;
   const int xcd = b & 7;
@@ -634,6 +668,7 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
     for (int s = 0; s < KS; ++s) {
       const int k = 2 * s + h;
       zb[t][s] = (k < D && cc[t] >= 0) ? ev.z[(size_t)k * ldc + cc[t]] : 0.0f;
+      if constexpr (EPI == 3) zb[t][s] *= -LOG2E;  // GEMM1 yields -l log2(e) (epilogue_log2)
     }
   f32x16 g0[CT], g1[CT];
 #pragma unroll
@@ -649,7 +684,22 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
   // TAIL: the stage holds rows >= n_rows (only the last one can): masked epilogue
   auto stage = [&](int st, auto tailc) {
     constexpr bool TAIL = decltype(tailc)::value;
-    {
+    const float* xt;
+    if constexpr (WAVE) {
+      // wave-private pipeline: each wave DMAs only its own 32-row subtile into its own LDS
+      // slice and waits for its own loads -- no workgroup barrier couples the 4 SIMDs.  Its
+      // previous reads of the slice were consumed (MFMA/VALU operands) before this point.
+      static_assert(CT == 1, "wave-private staging is written for one chain tile");
+      float* xw = xs + wu * WSLICE;
+      const unsigned base = (unsigned)(((int64_t)st * RL_ROWS + wu * 32) * XS * 4);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < WPIECES; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(xw + i * 256), 16,
+                                                 lane * 16, base + i * 1024, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      xt = xw;
+    } else {
       // buffer LDS-DMA: scalar descriptor + stage offset, one 32-bit lane offset; the last
       // piece's lanes past the stage read the next stage (or 0 past the end, range check)
       // into the LDS slack
@@ -661,9 +711,9 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
               xrs, (__attribute__((address_space(3))) void*)(xs + i * 256), 16, lane * 16,
               (unsigned)(st * STAGE * 4 + i * 1024), 0, 0);
       }
+      __syncthreads();
+      xt = xs + w * 32 * XS;
     }
-    __syncthreads();
-    const float* xt = xs + w * 32 * XS;
     const int64_t rb = (int64_t)st * RL_ROWS + w * 32;
     f32x16 a[CT];
 #pragma unroll
@@ -673,7 +723,10 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
     auto epi = [&](int t) {
       float lin = 0.0f, lg2 = 0.0f;
       // per wave, as in k_logreg_rowlanes: only the waves holding rows >= n_rows mask
-      if constexpr (EPI == 2) {
+      if constexpr (EPI == 3) {
+        if (TAIL && rb + 32 > n_rows) epilogue_log2<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
+        else epilogue_log2<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
+      } else if constexpr (EPI == 2) {
         if (TAIL && rb + 32 > n_rows) epilogue_abs<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
         else epilogue_abs<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
       } else if constexpr (EPI == 1) {
@@ -683,7 +736,7 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
         if (TAIL && rb + 32 > n_rows) epilogue<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
         else epilogue<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
       }
-      pe[t] += (double)lin + (double)lg2 * (double)LN2;
+      pe[t] += (EPI == 3 ? (double)LN2 : 1.0) * (double)lin + (double)lg2 * (double)LN2;
     };
     auto g1_tile = [&](int t) {
 #pragma unroll
@@ -733,45 +786,49 @@ __global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes_ct(const f
       }
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    __syncthreads();
+    if constexpr (!WAVE) __syncthreads();
   };
   const int t_full = (int)min((int64_t)t1, n_rows / RL_ROWS);  // stages with all 128 rows < n_rows
   int st = t0;
   for (; st < t_full; ++st) stage(st, std::false_type{});
   for (; st < t1; ++st) stage(st, std::true_type{});
 
-  // fixed-order combination of the 4 row lanes, one chain tile at a time
-  float* red = xs;                                                      // [RL_WAVES][32][64]
-  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
+  if constexpr (WAVE) __syncthreads();  // every wave is done with its slice
+  // fixed-order combination of the 4 row lanes, one chain tile at a time: waves 1-3 park
+  // their partials in LDS, wave 0 adds them to its registers in wave order
+  float* red = xs;                                                            // [RL_WAVES-1][32][64]
+  double* red_pe = reinterpret_cast<double*>(xs + (RL_WAVES - 1) * 32 * 64);  // [RL_WAVES-1][64]
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const double p = pe[t] + __shfl_xor(pe[t], 32);
     const int pos = (ct * CT + t) * 32 + l31;
     if (t > 0) __syncthreads();  // the previous tile's reads are done
+    if (w > 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      red[(w * 32 + r) * 64 + lane] = g0[t][r];
-      red[(w * 32 + 16 + r) * 64 + lane] = g1[t][r];
+      for (int r = 0; r < 16; ++r) {
+        red[((w - 1) * 32 + r) * 64 + lane] = g0[t][r];
+        red[((w - 1) * 32 + 16 + r) * 64 + lane] = g1[t][r];
+      }
+      red_pe[(w - 1) * 64 + lane] = p;
     }
-    red_pe[w * 64 + lane] = p;
     __syncthreads();
     if (w == 0 && pos < ldc) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
+        float s0 = g0[t][r], s1 = g1[t][r];
 #pragma unroll
         for (int ww = 1; ww < RL_WAVES; ++ww) {
-          s0 += red[(ww * 32 + r) * 64 + lane];
-          s1 += red[(ww * 32 + 16 + r) * 64 + lane];
+          s0 += red[((ww - 1) * 32 + r) * 64 + lane];
+          s1 += red[((ww - 1) * 32 + 16 + r) * 64 + lane];
         }
         const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
         if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
         if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
       }
       if (h == 0) {
-        double sp = red_pe[lane];
+        double sp = p;
 #pragma unroll
-        for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
+        for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[(ww - 1) * 64 + lane];
         pepart[(size_t)split * ldc + pos] = sp;
       }
     }
@@ -812,22 +869,28 @@ int check_ev(const nmx_eval_batch* ev) {
 }
 
 // Kernel variant (A/B experiments).  The gradient is bitwise the same in all row-lane forms
-// (same MFMA sequence per chain, explicit fmas in the epilogue); 17-19 round U differently
-// (product-of-factors log, |l| sums + w.b) at ~1e-7 relative.
-//   19 (default) k_logreg_rowlanes_ct, 1 chain tile, buffer LDS-DMA, peeled tail stage
-//      (124 VGPRs -> 4 waves/SIMD), s_setprio, epilogue_abs
-//   17 / 18  same with epilogue_prod, with / without s_setprio
-//   14 / 16  same with the plain epilogue, with / without s_setprio
+// (same MFMA sequence per chain, explicit fmas in the epilogue); 17-25 round U differently
+// (product-of-factors log, |l| sums + w.b) at ~1e-7 relative; 21 also rounds the logits
+// differently (z pre-scaled by -log2 e).
+//   22 (default) k_logreg_rowlanes_ct, 1 chain tile, wave-private LDS-DMA staging (no
+//      workgroup barrier in the row loop), peeled tail stage (124 VGPRs -> 4 waves/SIMD),
+//      s_setprio, epilogue_abs;  23 = 22 without s_setprio;  24 = 22 at >= 5 workgroups/CU
+//      (96 VGPRs, spills)
+//   19 same as 22 with workgroup-shared stages + barrier;  20 without s_setprio;  25 at 5/CU;
+//      21 = 19 on pre-scaled z
+//   17 / 18  19 with epilogue_prod, with / without s_setprio
+//   14 / 16  19 with the plain epilogue, with / without s_setprio
 //   12 / 13  two chain tiles per wave (256 / 248 VGPRs, 2 waves/SIMD), 15 = 13 with the two
 //            tiles' epilogues scheduled beside the other tile's MFMAs
 //   11 k_logreg_rowlanes (global_load_lds, 177 VGPRs, 2 waves/SIMD), 5 without s_setprio,
 //    4 double-buffered stages, 8 barrier-free wave pipeline, 0 generic tile kernel.
-// Measured at C=4096 (scripts/bench_potential.py, MI355X): 19: 116.5, 17: 112.9,
-// 14: 109.8, 16: 109.4, 11: 103.5, 13: 103.0, 15: 102.9, 12: 97.0 TFLOP/s; earlier: 5: 103.0,
-// 8: 101.6, 4: 98.2.
+// Measured at C=4096 (scripts/bench_potential.py, MI355X), TFLOP/s: 22: 117.2, 21: 117.4,
+// 19: 116.4, 23: 115.5, 25: 114.8, 20: 114.6, 24: 113.3, 17: 112.9, 14: 109.8, 16: 109.4,
+// 11: 103.5, 13: 103.0, 15: 102.9, 12: 97.0; earlier: 5: 103.0, 8: 101.6, 4: 98.2.
+// PMC (scripts/pmc_kernel.sh): MFMA pipe busy 82.5% (19) vs 72.4% (11) of SIMD cycles.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
-  return e ? atoi(e) : 19;
+  return e ? atoi(e) : 22;
 }
 
 template <int KS, int NBUF, bool PRIO>
@@ -844,17 +907,18 @@ void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batc
                      D, S, Gt, *ev, gpart, pepart);
 }
 
-template <int KS, int CT, bool PRIO, bool ILP = false, int EPI = 0>
+template <int KS, int CT, bool PRIO, bool ILP = false, int EPI = 0, bool WAVE = false, int MINB = 2>
 void launch_rowlanes_ct(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
                         double* pepart, hipStream_t s) {
   const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
   const int S = num_splits(n_rows);
   const int Gt = ev->ldc / (32 * CT);  // ldc % 64 == 0 (check_ev)
   constexpr int BUF = (RL_ROWS * (2 * KS + 1) + LDS_SLACK + 255) / 256 * 256;
-  size_t lds = (size_t)BUF * sizeof(float);
-  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
+  constexpr int WBUF = RL_WAVES * ((32 * (2 * KS + 1) + 255) / 256 * 256);
+  size_t lds = (size_t)(WAVE ? WBUF : BUF) * sizeof(float);
+  const size_t red = (size_t)(RL_WAVES - 1) * 32 * 64 * sizeof(float) + (RL_WAVES - 1) * 64 * sizeof(double);
   if (lds < red) lds = red;
-  hipLaunchKernelGGL((k_logreg_rowlanes_ct<KS, CT, PRIO, ILP, EPI>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows,
+  hipLaunchKernelGGL((k_logreg_rowlanes_ct<KS, CT, PRIO, ILP, EPI, WAVE, MINB>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows,
                      nstages, D, S, Gt, *ev, gpart, pepart);
 }
 
@@ -931,7 +995,7 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
-  const bool epi_abs = KS == 28 && var == 19;
+  const bool epi_abs = KS == 28 && var >= 19 && var <= 25;
   if (KS == 28 && var == 4) launch_rowlanes<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
   else if (KS == 28 && var == 5) launch_rowlanes<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28 && var == 8) launch_wavepipe<28>(Xp, n_rows, dim, ev, gpart, pepart, s);
@@ -944,6 +1008,12 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   else if (KS == 28 && var == 17) launch_rowlanes_ct<28, 1, true, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28 && var == 18) launch_rowlanes_ct<28, 1, false, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28 && var == 19) launch_rowlanes_ct<28, 1, true, false, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 20) launch_rowlanes_ct<28, 1, false, false, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 21) launch_rowlanes_ct<28, 1, true, false, 3>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 22) launch_rowlanes_ct<28, 1, true, false, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 23) launch_rowlanes_ct<28, 1, false, false, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 24) launch_rowlanes_ct<28, 1, true, false, 2, true, 5>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  else if (KS == 28 && var == 25) launch_rowlanes_ct<28, 1, true, false, 2, false, 5>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);

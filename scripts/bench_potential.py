@@ -5,7 +5,8 @@ import numpy as np, torch
 from numpyro_amd import datasets, native
 from numpyro_amd.potentials import LogisticRegression
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2,3,4,5").split(",")]
+# variant "d": the library default (NMX_LOGREG_VARIANT unset)
+variants = [v for v in (sys.argv[1] if len(sys.argv) > 1 else "d").split(",")]
 chains = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "4096,1024").split(",")]
 X, y = datasets.covtype_synthetic(seed=0)
 N, D = X.shape
@@ -22,7 +23,10 @@ for C in chains:
     ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), num_chains=C, ldc=ldc)
     ref = None
     for v in variants:
-        os.environ["NMX_LOGREG_VARIANT"] = str(v)
+        if v == "d":
+            os.environ.pop("NMX_LOGREG_VARIANT", None)
+        else:
+            os.environ["NMX_LOGREG_VARIANT"] = str(v)
         s = native.stream_ptr()
         for _ in range(3):
             pot.evaluate(ev, s)

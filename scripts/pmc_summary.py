@@ -1,0 +1,33 @@
+"""Average rocprofv3 counter values per dispatch of the logreg potential kernel.
+usage: python scripts/pmc_summary.py <dir with a/ b/ pass outputs>"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+tot = defaultdict(float)
+cnt = defaultdict(set)
+for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if "logreg_rowlanes" not in row.get("Kernel_Name", ""):
+                continue
+            name = row["Counter_Name"]
+            tot[name] += float(row["Counter_Value"])
+            cnt[name].add((path, row.get("Dispatch_Id", row.get("Correlation_Id", ""))))
+avg = {k: tot[k] / max(1, len(cnt[k])) for k in tot}
+for k in sorted(avg):
+    print(f"{k:32s} {avg[k]:.6g}  (dispatches {len(cnt[k])})")
+w = avg.get("SQ_WAVE_CYCLES")
+if w:
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+              "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_MISC"):
+        if k in avg:
+            print(f"{k} / WAVE_CYCLES = {avg[k] / w:.3f}")
+if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg and "SQ_BUSY_CU_CYCLES" in avg:
+    pass
+if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "SQ_BUSY_CYCLES" in avg:
+    print(f"MFMA_BUSY / (BUSY_CYCLES x 256 CU x 4 SIMD / 8 XCD?) raw ratio = "
+          f"{avg['SQ_VALU_MFMA_BUSY_CYCLES'] / avg['SQ_BUSY_CYCLES']:.3f}")

@@ -11,8 +11,10 @@ mkdir -p "$O"
 step() { echo "== $1" >> "$O/steps.log"; shift; "$@"; rc=$?; echo "rc=$rc" >> "$O/steps.log"; [ $rc -eq 0 ] || exit $rc; }
 step bench timeout -k 10 600 bash -c "python bench.py > $O/bench_line.json 2> $O/bench.err"
 step ktrace timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace" -o bench -- python3 bench.py --no-cpu-baseline
-step fetch timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o p -- python3 scripts/bench_potential.py 5 4096
-step write timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o p -- python3 scripts/bench_potential.py 5 4096
+step fetch timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o p -- python3 scripts/bench_potential.py d 4096
+step write timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o p -- python3 scripts/bench_potential.py d 4096
+step traffic python3 scripts/traffic_json.py "$O/pmc_fetch" "$O/pmc_write" "$O/traffic.json" "k_logreg_rowlanes_ct (NMX_LOGREG_VARIANT default), C=4096 all active"
+step sqpmc bash scripts/pmc_kernel.sh d "$tag"
 step configs timeout -k 10 900 bash -c "python scripts/bench_configs.py gemm 10000 4096 > $O/configs.jsonl && \
   python scripts/bench_configs.py covtype --chains 1024 --warmup 30 --steps 10 >> $O/configs.jsonl && \
   python scripts/bench_configs.py funnel --dense 0 --warmup 10 --steps 3 >> $O/configs.jsonl && \

@@ -251,14 +251,17 @@ def test_logreg_kernel_variants_agree(device, monkeypatch):
     y = (rs.rand(N) < 0.3).astype(np.float32)
     Z = (rs.randn(C, D) * 0.2).astype(np.float32)
     out = {}
-    for v in ("11", "5", "4", "8", "12", "13", "14", "15", "16", "17", "18", "19"):
+    for v in ("11", "5", "4", "8", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "22", "23", "24", "25"):
         monkeypatch.setenv("NMX_LOGREG_VARIANT", v)
         out[v] = _eval(LogisticRegression(X, y), Z, device)
     for v in ("5", "4", "12", "13", "14", "15", "16"):
         np.testing.assert_array_equal(out[v][0], out["11"][0], err_msg=v)
         np.testing.assert_array_equal(out[v][1], out["11"][1], err_msg=v)
-    for v in ("17", "18", "19"):  # product-of-factors log / |l| sums: U to ~1e-6 relative, grad bitwise
+    for v in ("17", "18", "19", "20", "22", "23", "24", "25"):  # product-of-factors log / |l| sums: U to ~1e-6 relative, grad bitwise
         np.testing.assert_allclose(out[v][0], out["11"][0], rtol=1e-6, err_msg=v)
         np.testing.assert_array_equal(out[v][1], out["11"][1], err_msg=v)
+    # GEMM1 on the pre-scaled z (-log2(e) z): logits round differently, grad to f32 accumulation level
+    np.testing.assert_allclose(out["21"][0], out["11"][0], rtol=1e-6)
+    np.testing.assert_allclose(out["21"][1], out["11"][1], rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(out["8"][0], out["11"][0], rtol=1e-6)
     np.testing.assert_allclose(out["8"][1], out["11"][1], rtol=1e-5, atol=1e-3)
