@@ -137,6 +137,114 @@ __global__ __launch_bounds__(256, 2) void k_gemm_chains(const float* __restrict_
   }
 }
 
+// Same products, tiles and MFMA order as k_gemm_chains (bitwise equal results), with both
+// operand tiles staged by buffer LDS-DMA through scalar descriptors (no register staging of
+// B: fewer VGPRs, no VALU copies), BK-deep double-buffered stages in dynamic LDS, and one
+// barrier per stage.  B rows >= D come back as zeros from the descriptor's range check
+// (every B offset is in voffset, which the check covers).
+template <int BKV>
+__global__ __launch_bounds__(256, 2) void k_gemm_chains2(const float* __restrict__ At, int lda, int D,
+                                                         const float* __restrict__ In, float* __restrict__ Out,
+                                                         const float* __restrict__ bias, int triangle, int ldc,
+                                                         const int32_t* __restrict__ phase,
+                                                         const int32_t* __restrict__ count, int C,
+                                                         float* __restrict__ part, int ksplit, int order, int n_rt,
+                                                         int n_ct) {
+  constexpr int A_PIECES = BKV * TM / 256;  // 1 KB pieces (2 rows of 128 floats)
+  constexpr int B_PIECES = BKV * TN / 256;  // 1 KB pieces (4 rows of 64 floats)
+  constexpr int STAGE = BKV * (TM + TN);    // floats per stage
+  constexpr int PER_WAVE = (A_PIECES + B_PIECES) / 4;
+  static_assert((A_PIECES + B_PIECES) % 4 == 0, "pieces split evenly over 4 waves");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int rt_i = blockIdx.x, ct_i = blockIdx.y;
+  if (order) {
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    rt_i = (q / n_ct) * 8 + xcd;
+    ct_i = q % n_ct;
+    if (rt_i >= n_rt) return;
+  }
+  const int i0 = rt_i * TM;
+  const int c0 = ct_i * TN;
+  if (count) {
+    if (c0 >= *count) return;
+  } else {
+    const int c = c0 + lane;
+    const bool act = c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+    if (!__any(act)) return;
+  }
+  // K range and split-K boundaries in units of BK = 32 (those of k_gemm_chains), then in
+  // BKV-tiles: every variant adds the same products in the same order
+  constexpr int R = BK / BKV;
+  static_assert(BK % BKV == 0, "BKV divides BK");
+  const int kt_lo = triangle == 1 ? i0 / BK : 0;
+  const int kt_hi = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
+  const int z = blockIdx.z;
+  const int kt_begin = R * (kt_lo + (int)((int64_t)(kt_hi - kt_lo) * z / ksplit));
+  const int nk = R * (kt_lo + (int)((int64_t)(kt_hi - kt_lo) * (z + 1) / ksplit));
+
+  const __amdgpu_buffer_rsrc_t ars =
+      __builtin_amdgcn_make_buffer_rsrc((void*)At, 0, (int)min((int64_t)lda * lda * 4, (int64_t)0x7fffffff),
+                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t brs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)In, 0, (int)min((int64_t)D * ldc * 4, (int64_t)0x7fffffff),
+                                        0x00020000);
+  const unsigned a_lane = (unsigned)(((lane >> 5) * lda + (lane & 31) * 4) * 4);
+  const unsigned b_lane = (unsigned)(((lane >> 4) * ldc + (lane & 15) * 4) * 4);
+  auto issue = [&](int kt, int buf) {
+    float* st = lds + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j) {
+      const int p = wu * PER_WAVE + j;  // wave-uniform piece index
+      if (p < A_PIECES) {
+        const unsigned so = (unsigned)(((size_t)(kt * BKV + 2 * p) * lda + i0) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(st + p * 256), 16,
+                                                 a_lane, so, 0, 0);
+      } else {
+        const int pb = p - A_PIECES;
+        const unsigned vo = b_lane + (unsigned)(((size_t)(kt * BKV + 4 * pb) * ldc + c0) * 4);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            brs, (__attribute__((address_space(3))) void*)(st + BKV * TM + pb * 256), 16, vo, 0, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = 0.0f;
+    acc1[r] = 0.0f;
+  }
+  if (kt_begin < nk) issue(kt_begin, 0);
+  for (int kt = kt_begin; kt < nk; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage kt landed for every wave; every wave is done with stage kt-1
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const float* as = lds + buf * STAGE;
+    const float* bs = as + BKV * TM;
+#pragma unroll
+    for (int s = 0; s < BKV / 2; ++s) {
+      const int k = 2 * s + h;
+      const float a = as[k * TM + w * 32 + l31];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bs[k * TN + l31], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bs[k * TN + 32 + l31], acc1, 0, 0, 0);
+    }
+  }
+  float* const dst = ksplit > 1 ? part + (size_t)z * D * ldc : Out;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = i0 + w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (i < D) {
+      const float bi = (bias && ksplit == 1) ? bias[i] : 0.0f;
+      const int ca = c0 + l31, cb = c0 + 32 + l31;
+      if (ca < ldc) dst[(size_t)i * ldc + ca] = acc0[r] + bi;
+      if (cb < ldc) dst[(size_t)i * ldc + cb] = acc1[r] + bi;
+    }
+  }
+}
+
 // Out = sum_z part[z] (+ bias), z in order; same tile selection as k_gemm_chains.
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ part, int ksplit, int D, int ldc,
                                                      float* __restrict__ Out, const float* __restrict__ bias,
@@ -363,11 +471,13 @@ extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In,
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains: lda must be a multiple of %d >= padded D", TM);
   if (In == Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: In and Out must not alias");
   if (triangle < 0 || triangle > 2) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: triangle must be 0, 1 or 2");
+  // 2 (default): k_gemm_chains2<32>; 3: k_gemm_chains2<16>; 0: k_gemm_chains (register-
+  // staged B); 1: k_gemm_chains_w (128-chain tiles).  0, 2, 3 give bitwise equal products.
   static const int wide = [] {
     const char* e = getenv("NMX_GEMM_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
-  if (wide && ldc >= TN2) {
+  if (wide == 1 && ldc >= TN2) {
     const int n_rt = lda / TM, n_ct = (ldc + TN2 - 1) / TN2;
     const int nb = (n_rt + 7) / 8 * 8 * n_ct;
     hipLaunchKernelGGL(k_gemm_chains_w, dim3(nb), dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias,
@@ -384,8 +494,20 @@ extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In,
   const int n_rt = lda / TM, n_ct = ldc / TN;
   const int order = forced_order >= 0 ? forced_order : (n_rt <= 48 ? 1 : 0);
   dim3 grid = order ? dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks) : dim3(n_rt, n_ct, ks);
-  hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, triangle,
-                     ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
+  const bool fits32 = (int64_t)lda * lda * 4 < 0x7fffffff && (int64_t)D * ldc * 4 < 0x7fffffff;
+  if (wide >= 2 && fits32) {
+    const int bk = wide == 3 ? 16 : 32;
+    const size_t lds = 2 * (size_t)bk * (TM + TN) * sizeof(float);
+    if (bk == 16)
+      hipLaunchKernelGGL(k_gemm_chains2<16>, grid, dim3(256), lds, (hipStream_t)stream, At, lda, D, In, Out, bias,
+                         triangle, ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
+    else
+      hipLaunchKernelGGL(k_gemm_chains2<32>, grid, dim3(256), lds, (hipStream_t)stream, At, lda, D, In, Out, bias,
+                         triangle, ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
+  } else {
+    hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, triangle,
+                       ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
+  }
   if (ks > 1)
     hipLaunchKernelGGL(k_gemm_reduce, dim3((D + 15) / 16, ldc / TN), dim3(256), 0, (hipStream_t)stream,
                        (const float*)workspace, ks, D, ldc, Out, bias, phase, active_count, num_chains);
