@@ -23,6 +23,7 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "nmx_api_internal.h"
@@ -835,9 +836,357 @@ __global__ __launch_bounds__(RL_WAVES * 64, MINB) void k_logreg_rowlanes_ct(cons
   }
 }
 
-// wcol (epilogue_abs variants): U gains the per-chain linear term w . b
+// ---------------------------------------------------------------------------------------
+// Split-bf16 kernel (variant 30): f32-accurate products on the bf16 matrix cores.
+//
+// Every f32 operand v is split into three bf16 terms, v1 = bf16(v), v2 = bf16(v - v1),
+// v3 = bf16(v - v1 - v2) (round to nearest; the remainders are exact in f32), which
+// represents v to within 2^-24 |v| -- the f32 rounding unit.  A product a.b keeps the six
+// terms with i + j <= 4 (a3b1 + a2b2 + a1b3 + a2b1 + a1b2 + a1b1, small terms first); the
+// three dropped ones are each below 2^-24 |ab|.  A bf16 x bf16 product is exact in f32 and
+// v_mfma_f32_32x32x16_bf16 accumulates in f32, so each output carries f32-level accuracy
+// (tests/test_gpu_potentials.py compares its error against the f32-MFMA kernel's, both
+// vs float64) for 6 bf16 MFMAs per 16-deep k-step, against 8 f32 MFMAs (32x32x2) at 2x the
+// cycles each: 32 vs 64 cycles per MFMA, 6 x 32 = 192 vs 8 x 64 = 512 cycles per k-step.
+//
+// Packed layout (nmx_logreg_pack, behind the f32 rows): per 32-row tile NP = 3 KB + 6 DT + 1
+// pieces of 1 KB, each a 64-lane x 16-byte MFMA operand fragment in lane order, so a wave
+// reads an operand with one conflict-free ds_read_b128 and the LDS-DMA copy is linear:
+//   piece p*KB + kb                 GEMM1 A = X[32 rows][16 cols], plane p, k-block kb:
+//                                   lane (r, h) holds X[r][16 kb + 8 h + j]
+//   piece 3KB + p*2DT + 2 dt + s    GEMM2 A = X^T[32 cols][16 rows], plane p, col tile dt,
+//                                   k-step s: lane (r, h) element j holds
+//                                   X[16 s + 8 (j>>2) + 4 h + (j&3)][32 dt + r] -- the k order
+//                                   of the GEMM1 accumulator used as the B operand
+//   piece NP-1                      labels y[h][i] of row (i&3) + 8 (i>>2) + 4 h, then zeros
+// Rows >= n_rows are zero (l = 0: no gradient, an exact log(2) each in U, removed in the
+// finalize), columns >= D are zero.  KB = ceil(D/16), DT = ceil(D/32).
+//
+// Workgroup = 4 waves = 4 chain tiles of 32 sharing each X tile; X tiles stream through a
+// 3-slot LDS ring by buffer LDS-DMA, one workgroup barrier per tile.  Grid = chain groups x
+// S2 row splits, S2 a function of n_rows only (fixed summation order, as for the f32
+// kernels); the partials go through the same slabs and finalize.
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int X3_ROWS = 32;
+constexpr int X3_MAX_S = 256;
+
+inline int x3_kb(int D) { return (D + 15) / 16; }
+inline int x3_dt(int D) { return (D + 31) / 32; }
+inline int x3_np(int D) { return 3 * x3_kb(D) + 6 * x3_dt(D) + 1; }
+inline int64_t x3_ntiles(int64_t n) { return (n + X3_ROWS - 1) / X3_ROWS; }
+
+int x3_num_splits(int64_t n_rows) {
+  static const int max_s = [] {
+    const char* e = getenv("NMX_X3_MAX_SPLITS");  // experiments only; must not change between bind and use
+    return e ? atoi(e) : X3_MAX_S;
+  }();
+  int64_t s = x3_ntiles(n_rows) / 16;
+  s = s / 8 * 8;
+  if (s < 8) s = 8;
+  if (s > max_s) s = max_s;
+  return (int)s;
+}
+
+// three-term bf16 split of 8 floats (round to nearest even at every step)
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h1 = (__bf16)v[j];
+    const float e1 = v[j] - (float)h1;
+    const __bf16 h2 = (__bf16)e1;
+    const float e2 = e1 - (float)h2;
+    b1[j] = h1;
+    b2[j] = h2;
+    b3[j] = (__bf16)e2;
+  }
+}
+
+// one thread per (tile, piece, lane): 16 bytes of one operand fragment
+__global__ void k_logreg_pack_x3(const float* __restrict__ X, const float* __restrict__ y, int64_t n, int D,
+                                 int KB, int DT, int64_t ntiles, bf16x8* __restrict__ out) {
+  const int NP = 3 * KB + 6 * DT + 1;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ntiles * NP * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t q = i >> 6;
+  const int piece = (int)(q % NP);
+  const int64_t t = q / NP;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t r0 = t * X3_ROWS;
+  float v[8];
+  int plane = 0;
+  if (piece < 3 * KB) {
+    plane = piece / KB;
+    const int kb = piece % KB;
+    const int64_t row = r0 + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * kb + 8 * h + j;
+      v[j] = (row < n && d < D) ? X[row * D + d] : 0.0f;
+    }
+  } else if (piece < NP - 1) {
+    const int qq = piece - 3 * KB;
+    plane = qq / (2 * DT);
+    const int rem = qq % (2 * DT);
+    const int dt = rem >> 1, s = rem & 1;
+    const int d = 32 * dt + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = r0 + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+      v[j] = (row < n && d < D) ? X[row * D + d] : 0.0f;
+    }
+  } else {
+    // labels as floats: lane L < 8 holds y[h = L/4][i = 4 (L%4) .. +3] (bytes 16 L .. 16 L + 15)
+    float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (lane < 8) {
+      const int hh = lane >> 2;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ii = 4 * (lane & 3) + k;
+        const int64_t row = r0 + (ii & 3) + 8 * (ii >> 2) + 4 * hh;
+        f[k] = row < n ? y[row] : 0.0f;
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(out + i);
+    *o = make_float4(f[0], f[1], f[2], f[3]);
+    return;
+  }
+  bf16x8 b1, b2, b3;
+  split3(v, b1, b2, b3);
+  out[i] = plane == 0 ? b1 : (plane == 1 ? b2 : b3);
+}
+
+template <int N>
+__device__ __forceinline__ void x3_wait_vm() {
+  // s_waitcnt vmcnt(N), other counters untouched (gfx9 encoding: vmcnt[3:0] | expcnt 7 << 4
+  // | lgkmcnt 15 << 8 | vmcnt[5:4] << 14)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// GEMM1 of one tile: L = X . Z (32 rows x 32 chains), six split products per k-block
+template <int KB>
+__device__ __forceinline__ f32x16 x3_gemm1(const bf16x8* fr, const bf16x8 (&z1)[KB], const bf16x8 (&z2)[KB],
+                                           const bf16x8 (&z3)[KB]) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const bf16x8 a1 = fr[(0 * KB + kb) * 64], a2 = fr[(1 * KB + kb) * 64], a3 = fr[(2 * KB + kb) * 64];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// Labels of a tile (16 per lane, rows of the accumulator layout), read by inline asm: a
+// compiler-visible LDS read here gets an s_waitcnt vmcnt(0) (the wait tracking cannot tell
+// it from the ring slots still being filled), which would drain the prefetch.  x3_labels_wait
+// must run before the values are used.
+__device__ __forceinline__ void x3_labels(const char* ybase, int h, f32x4 (&y4)[4]) {
+  const unsigned ya = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)ybase) + 64 * h;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:16\n\t"
+      "ds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b128 %3, %4 offset:48"
+      : "=&v"(y4[0]), "=&v"(y4[1]), "=&v"(y4[2]), "=&v"(y4[3])
+      : "v"(ya));
+}
+__device__ __forceinline__ void x3_labels_wait(f32x4 (&y4)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y4[0]), "+v"(y4[1]), "+v"(y4[2]), "+v"(y4[3]));
+}
+
+// Bernoulli-logits epilogue (epilogue_abs arithmetic; no row mask: padded rows have l = 0):
+// acc -> sigmoid(l) - y, U terms into pe
+__device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&y4)[4], float (&res)[16], double& pe) {
+  float lin = 0.0f, prod = 1.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = 4 * q + u;
+      const float l = acc[r];
+      const float al = fabsf(l);
+      const float e = __builtin_amdgcn_exp2f(-al * LOG2E);
+      const float ope = 1.0f + e;
+      const float inv = __builtin_amdgcn_rcpf(ope);
+      const float num = l >= 0.0f ? 1.0f : e;
+      res[r] = __builtin_fmaf(num, inv, -y4[q][u]);
+      lin += al;
+      prod *= ope;
+    }
+  }
+  pe += (double)(0.5f * lin) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+}
+
+// GEMM2 of one tile: G += X^T . R, R split into three bf16 terms (k-step s = registers 8s..8s+7)
+template <int KB, int DT>
+__device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16], f32x16 (&g)[DT]) {
+  constexpr int G2 = 3 * KB;  // first GEMM2 piece
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = res[8 * s + j];
+    bf16x8 r1, r2, r3;
+    split3(v, r1, r2, r3);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16x8 b1 = fr[(G2 + 0 * 2 * DT + 2 * dt + s) * 64];
+      const bf16x8 b2 = fr[(G2 + 1 * 2 * DT + 2 * dt + s) * 64];
+      const bf16x8 b3 = fr[(G2 + 2 * 2 * DT + 2 * dt + s) * 64];
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
+    }
+  }
+}
+
+// PIPE: software-pipelined -- GEMM1 of tile k+1 is issued beside the epilogue of tile k (they
+// are independent), then GEMM2 of tile k; needs RING = 3 (slots k, k+1 read, k+2 filling).
+// The per-chain arithmetic and its order are the same in both forms (bitwise equal results).
+template <int KB, int DT, int RING, int MINB, bool PIPE>
+__global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
+                                                     int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
+                                                     double* __restrict__ pepart) {
+  constexpr int NP = 3 * KB + 6 * DT + 1;
+  constexpr int PPW = (NP + 3) / 4;     // DMA pieces per wave per tile (max)
+  static_assert(!PIPE || RING == 3, "the pipelined loop reads two slots while a third fills");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7;
+  const int qb = b >> 3;
+  const int ct = qb % Gt;
+  const int split = (qb / Gt) * 8 + xcd;
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int pos = (ct * 4 + wu) * 32 + l31;
+  const int c = pos < ldc ? nmx_eval_chain(ev, pos) : -1;
+  const bool active = __any(c >= 0);  // wave-uniform
+  if (!__syncthreads_or(active)) return;  // workgroup-uniform
+
+  const int64_t per = (ntiles + S - 1) / S;
+  const int64_t t0 = min((int64_t)split * per, ntiles);
+  const int64_t t1 = min(t0 + per, ntiles);
+  const int nt = (int)(t1 - t0);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
+  // pieces of this wave: wu, wu + 4, ... (PPW of them, or PPW - 1)
+  const bool full = wu < NP - 4 * (PPW - 1);
+
+  bf16x8 z1[KB], z2[KB], z3[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * kb + 8 * h + j;
+      v[j] = (c >= 0 && d < D) ? ev.z[(size_t)d * ldc + c] : 0.0f;
+    }
+    split3(v, z1[kb], z2[kb], z3[kb]);
+  }
+  f32x16 g[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) g[dt][r] = 0.0f;
+  double pe = 0.0;
+
+  auto issue = [&](int k) {  // tile t0 + k into ring slot k % RING
+    char* dst = lds + (k % RING) * NP * 1024;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int i = wu + 4 * j;
+      if (i < NP)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                                 lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
+    }
+  };
+  auto slot = [&](int k) { return lds + (k % RING) * NP * 1024; };
+  if constexpr (PIPE) {
+    if (nt > 0) {
+      issue(0);
+      if (nt > 1) issue(1);
+      if (nt > 1) {
+        if (full) x3_wait_vm<PPW>();
+        else x3_wait_vm<PPW - 1>();
+      } else {
+        x3_wait_vm<0>();
+      }
+      asm volatile("s_barrier" ::: "memory");  // tile 0 is in
+      f32x16 acc;
+      if (active) acc = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(slot(0)) + lane, z1, z2, z3);
+      for (int k = 0; k < nt; ++k) {
+        // tile k+1 has landed (in every wave); slot (k+2) % 3 was last read by GEMM2(k-1)
+        x3_wait_vm<0>();
+        asm volatile("s_barrier" ::: "memory");
+        if (k + 2 < nt) issue(k + 2);
+        if (!active) continue;
+        const bf16x8* frk = reinterpret_cast<const bf16x8*>(slot(k)) + lane;
+        f32x4 y4[4];
+        x3_labels(slot(k) + (NP - 1) * 1024, h, y4);
+        x3_labels_wait(y4);
+        // GEMM1 of tile k+1 (junk slot past the last tile: computed, never used) beside the
+        // epilogue of tile k
+        const f32x16 nxt = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(slot(k + 1)) + lane, z1, z2, z3);
+        float res[16];
+        x3_epilogue(acc, y4, res, pe);
+        x3_gemm2<KB, DT>(frk, res, g);
+        acc = nxt;
+      }
+    }
+  } else {
+    // RING slots, RING - 1 tiles in flight ahead of the one being computed
+    for (int k = 0; k < RING - 1 && k < nt; ++k) issue(k);
+    for (int k = 0; k < nt; ++k) {
+      // this wave's pieces of tile k have landed (those of tile k + 1 may still fly)
+      if (RING == 2 || k + 1 >= nt) x3_wait_vm<0>();
+      else if (full) x3_wait_vm<PPW>();
+      else x3_wait_vm<PPW - 1>();
+      asm volatile("s_barrier" ::: "memory");  // ... and every wave's; slot (k-1) % RING is free
+      if (k + RING - 1 < nt) issue(k + RING - 1);
+      if (!active) continue;
+      const bf16x8* fr = reinterpret_cast<const bf16x8*>(slot(k)) + lane;
+      f32x4 y4[4];
+      x3_labels(slot(k) + (NP - 1) * 1024, h, y4);
+      const f32x16 acc = x3_gemm1<KB>(fr, z1, z2, z3);
+      x3_labels_wait(y4);
+      float res[16];
+      x3_epilogue(acc, y4, res, pe);
+      x3_gemm2<KB, DT>(fr, res, g);
+    }
+  }
+  if (!active || pos >= ldc) return;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = 32 * dt + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = g[dt][r];
+    }
+  const double p = pe + __shfl_xor(pe, 32);
+  if (h == 0) pepart[(size_t)split * ldc + pos] = p;
+}
+
+// wcol (epilogue_abs variants): U gains the per-chain linear term w . b; pe_shift removes the
+// log(2) terms of the zero rows that pad the split-bf16 tiles
 __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
-                                  int D, nmx_eval_batch ev, const double* __restrict__ wcol) {
+                                  int D, nmx_eval_batch ev, const double* __restrict__ wcol, double pe_shift) {
   const int pos = blockIdx.x * blockDim.x + threadIdx.x;
   const int d = blockIdx.y;
   const int c = nmx_eval_chain(ev, pos);
@@ -857,7 +1206,7 @@ __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double*
       zz += z * z;
       if (wcol) wz += wcol[k] * z;
     }
-    ev.pe[c] = (float)(s + wz + 0.5 * zz + 0.9189385332046727 * D);
+    ev.pe[c] = (float)(s + pe_shift + wz + 0.5 * zz + 0.9189385332046727 * D);
   }
 }
 
@@ -951,9 +1300,14 @@ void launch_tiles(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* 
 
 extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return num_splits(n_rows); }
 
+// packed buffer: f32 rows | w[64] (k_logreg_colsums) | split-bf16 tiles (k_logreg_pack_x3)
+inline size_t x3_offset(int64_t n_rows, int dim) {
+  return (colterm_offset(n_rows, dim) + 64 * sizeof(double) + 255) / 256 * 256;
+}
+
 extern "C" size_t nmx_logreg_packed_bytes(int64_t n_rows, int dim) {
   if (n_rows <= 0 || dim <= 0) return 0;
-  return colterm_offset(n_rows, dim) + 64 * sizeof(double);  // rows, then w[64] (k_logreg_colsums)
+  return x3_offset(n_rows, dim) + (size_t)x3_ntiles(n_rows) * x3_np(dim) * 1024;
 }
 
 extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, int dim, void* packed,
@@ -970,12 +1324,17 @@ extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, i
   if (int st = nmx_check_launch("k_logreg_pack")) return st;
   hipLaunchKernelGGL(k_logreg_colsums, dim3(dim), dim3(CS_THREADS), 0, (hipStream_t)stream, X, y, n_rows, dim,
                      (double*)((char*)packed + colterm_offset(n_rows, dim)));
-  return nmx_check_launch("k_logreg_colsums");
+  if (int st = nmx_check_launch("k_logreg_colsums")) return st;
+  const int64_t nt = x3_ntiles(n_rows);
+  const int64_t nthreads = nt * x3_np(dim) * 64;
+  hipLaunchKernelGGL(k_logreg_pack_x3, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, X,
+                     y, n_rows, dim, x3_kb(dim), x3_dt(dim), nt, (bf16x8*)((char*)packed + x3_offset(n_rows, dim)));
+  return nmx_check_launch("k_logreg_pack_x3");
 }
 
 extern "C" size_t nmx_logreg_workspace_bytes(int64_t n_rows, int dim, int num_chains) {
   const size_t ldc = (size_t)(num_chains + 63) / 64 * 64;
-  const size_t S = num_splits(n_rows);
+  const size_t S = std::max(num_splits(n_rows), x3_num_splits(n_rows));
   const size_t g = S * dim * ldc * sizeof(float);
   const size_t p = S * ldc * sizeof(double);
   return (g + 255) / 256 * 256 + p;
@@ -995,6 +1354,32 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
+  if (var >= 30 && var <= 32) {
+    const int S2 = x3_num_splits(n_rows);
+    pepart = (double*)((char*)workspace + ((size_t)S2 * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
+    const int64_t nt = x3_ntiles(n_rows);
+    const int Gt = (ev->ldc + 127) / 128;
+    const int KB = x3_kb(dim), DT = x3_dt(dim);
+    const int ring = var == 30 ? 2 : 3;
+    const size_t lds = (size_t)ring * x3_np(dim) * 1024;
+    const char* Xq = (const char*)packed + x3_offset(n_rows, dim);
+    const dim3 grid(Gt * S2), blk(256);
+#define NMX_X3(kb, dt)                                                                                           \
+  if (var == 30) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 2, 3, false>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else if (var == 31) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, false>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
+    if (KB == 4) { NMX_X3(4, 2) }
+    else if (KB == 3) { NMX_X3(3, 2) }
+    else if (KB == 2) { NMX_X3(2, 1) }
+    else { NMX_X3(1, 1) }
+#undef NMX_X3
+    if (int st = nmx_check_launch("k_logreg_x3")) return st;
+    const double* wcol = (const double*)((const char*)packed + colterm_offset(n_rows, dim));
+    const double shift = -(double)(nt * X3_ROWS - n_rows) * 0.6931471805599453;
+    hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S2, dim, *ev,
+                       wcol, shift);
+    return nmx_check_launch("k_logreg_finalize");
+  }
   const bool epi_abs = KS == 28 && var >= 19 && var <= 25;
   if (KS == 28 && var == 4) launch_rowlanes<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
   else if (KS == 28 && var == 5) launch_rowlanes<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
@@ -1022,6 +1407,6 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   if (int st = nmx_check_launch("k_logreg_tiles")) return st;
   const double* wcol = epi_abs ? (const double*)((const char*)packed + colterm_offset(n_rows, dim)) : nullptr;
   hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S, dim, *ev,
-                     wcol);
+                     wcol, 0.0);
   return nmx_check_launch("k_logreg_finalize");
 }
