@@ -186,7 +186,9 @@ typedef struct nmx_eval_batch {
                                   when set, only chains active_idx[0 .. *active_count) are
                                   evaluated and `phase` is ignored */
   const int32_t* active_count;
-  int32_t num_chains;
+  int32_t num_chains;      /* without a list: positions >= num_chains hold no chain; with a
+                              list: an upper bound on *active_count that kernels may size their
+                              grids by (the engine lowers it as chains finish) */
   int32_t ldc;
 } nmx_eval_batch;
 

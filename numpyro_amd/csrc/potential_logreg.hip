@@ -1057,19 +1057,15 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 // PIPE: software-pipelined -- GEMM1 of tile k+1 is issued beside the epilogue of tile k (they
 // are independent), then GEMM2 of tile k; needs RING = 3 (slots k, k+1 read, k+2 filling).
 // The per-chain arithmetic and its order are the same in both forms (bitwise equal results).
-template <int KB, int DT, int RING, int MINB, bool PIPE>
-__global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
-                                                     int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
-                                                     double* __restrict__ pepart) {
+//
+template <int KB, int DT, int RING, bool PIPE>
+__device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
+                                        nmx_eval_batch ev, float* __restrict__ gpart,
+                                        double* __restrict__ pepart) {
   constexpr int NP = 3 * KB + 6 * DT + 1;
   constexpr int PPW = (NP + 3) / 4;     // DMA pieces per wave per tile (max)
   static_assert(!PIPE || RING == 3, "the pipelined loop reads two slots while a third fills");
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x;
-  const int xcd = b & 7;
-  const int qb = b >> 3;
-  const int ct = qb % Gt;
-  const int split = (qb / Gt) * 8 + xcd;
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5;
@@ -1089,15 +1085,19 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   // pieces of this wave: wu, wu + 4, ... (PPW of them, or PPW - 1)
   const bool full = wu < NP - 4 * (PPW - 1);
 
+  // Z through a buffer descriptor: coordinates >= D and inactive lanes (c = -1) fall outside
+  // its range and read 0, so the loads need no per-element conditions (conditions and 64-bit
+  // addresses hoisted out of the item loop spilled)
+  const __amdgpu_buffer_rsrc_t zrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)ev.z, 0, D * ldc * 4, 0x00020000);
+  const unsigned zoff = c >= 0 ? (unsigned)((8 * h * ldc + c) * 4) : 0xFFFFFFF0u;
   bf16x8 z1[KB], z2[KB], z3[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = 16 * kb + 8 * h + j;
-      v[j] = (c >= 0 && d < D) ? ev.z[(size_t)d * ldc + c] : 0.0f;
-    }
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zoff, (16 * kb + j) * ldc * 4, 0));
     split3(v, z1[kb], z2[kb], z3[kb]);
   }
   f32x16 g[DT];
@@ -1183,6 +1183,22 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   if (h == 0) pepart[(size_t)split * ldc + pos] = p;
 }
 
+// Grid = chain groups (128 batch positions) x S row splits.  Splits sp = x (mod 8) run on XCD x
+// (workgroup b = x mod 8), the chain groups of a split on consecutive workgroups of that XCD, so
+// they share X tiles in its L2.  A workgroup whose chain group lies past the compacted list's
+// count leaves after one scalar load: the tail of a NUTS run launches thousands of them.
+template <int KB, int DT, int RING, int MINB, bool PIPE>
+__global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
+                                                     int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
+                                                     double* __restrict__ pepart) {
+  const int b = blockIdx.x;
+  const int qb = b >> 3;
+  const int ct = qb % Gt;
+  const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
+  if (ct * 128 >= npos) return;
+  x3_item<KB, DT, RING, PIPE>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
+}
+
 // wcol (epilogue_abs variants): U gains the per-chain linear term w . b; pe_shift removes the
 // log(2) terms of the zero rows that pad the split-bf16 tiles
 __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
@@ -1239,7 +1255,7 @@ int check_ev(const nmx_eval_batch* ev) {
 // PMC (scripts/pmc_kernel.sh): MFMA pipe busy 82.5% (19) vs 72.4% (11) of SIMD cycles.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
-  return e ? atoi(e) : 22;
+  return e ? atoi(e) : 30;
 }
 
 template <int KS, int NBUF, bool PRIO>
@@ -1358,11 +1374,13 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
     const int S2 = x3_num_splits(n_rows);
     pepart = (double*)((char*)workspace + ((size_t)S2 * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
     const int64_t nt = x3_ntiles(n_rows);
-    const int Gt = (ev->ldc + 127) / 128;
     const int KB = x3_kb(dim), DT = x3_dt(dim);
     const int ring = var == 30 ? 2 : 3;
     const size_t lds = (size_t)ring * x3_np(dim) * 1024;
     const char* Xq = (const char*)packed + x3_offset(n_rows, dim);
+    // fixed grid: workgroups per XCD = 32 CUs x workgroups per CU (3 for the 2-slot ring)
+    const int nb = std::min(ev->num_chains, ev->ldc);  // batch positions that can hold a chain
+    const int Gt = (nb + 127) / 128;
     const dim3 grid(Gt * S2), blk(256);
 #define NMX_X3(kb, dt)                                                                                           \
   if (var == 30) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 2, 3, false>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
@@ -1376,8 +1394,8 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
     if (int st = nmx_check_launch("k_logreg_x3")) return st;
     const double* wcol = (const double*)((const char*)packed + colterm_offset(n_rows, dim));
     const double shift = -(double)(nt * X3_ROWS - n_rows) * 0.6931471805599453;
-    hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S2, dim, *ev,
-                       wcol, shift);
+    hipLaunchKernelGGL(k_logreg_finalize, dim3((nb + 63) / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S2, dim,
+                       *ev, wcol, shift);
     return nmx_check_launch("k_logreg_finalize");
   }
   const bool epi_abs = KS == 28 && var >= 19 && var <= 25;

@@ -360,6 +360,8 @@ class Engine:
         check(step(cfgp, arena, sp, fp, tp, s), "nmx_nuts_step")
         evaluate = self.potential.evaluate
         lists = self.eval_lists
+        for b in lists:
+            b.num_chains = self.C
         while True:
             for _ in range(poll_every):
                 evaluate(lists[parity], s)
@@ -369,8 +371,13 @@ class Engine:
             launches += poll_every
             if pending:
                 ev.synchronize()
-                if int(host[0]) >= self.C:
+                done_n = int(host[0])
+                if done_n >= self.C:
                     break
+                # finished chains never re-enter the lists: C - done bounds every later list
+                # count, and kernels size their grids by it (nmx_eval_batch.num_chains)
+                for b in lists:
+                    b.num_chains = self.C - done_n
             host.copy_(done, non_blocking=True)
             ev.record()
             pending = True
