@@ -1058,13 +1058,13 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 // are independent), then GEMM2 of tile k; needs RING = 3 (slots k, k+1 read, k+2 filling).
 // The per-chain arithmetic and its order are the same in both forms (bitwise equal results).
 //
-template <int KB, int DT, int RING, bool PIPE>
+template <int KB, int DT, int RING, bool PIPE, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
                                         nmx_eval_batch ev, float* __restrict__ gpart,
                                         double* __restrict__ pepart) {
   constexpr int NP = 3 * KB + 6 * DT + 1;
   constexpr int PPW = (NP + 3) / 4;     // DMA pieces per wave per tile (max)
-  static_assert(!PIPE || RING == 3, "the pipelined loop reads two slots while a third fills");
+  static_assert(!PIPE || RING == 3 || RING == 4, "the pipelined loop reads two slots while a third fills");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1118,7 +1118,118 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
     }
   };
   auto slot = [&](int k) { return lds + (k % RING) * NP * 1024; };
-  if constexpr (PIPE) {
+  if constexpr (PIPE && RING == 4) {
+    // Split rings: GEMM1 reads only the A part of a tile (pieces < 3 KB), GEMM2 and the labels
+    // only the B part.  Iteration k reads A(k+1) and B(k) while A(k+2) and B(k+1) fill, so two
+    // slots of each part suffice: 2 x (12 + 13) KB for covtype, three workgroups per CU.
+    constexpr int NA = 3 * KB, NBP = NP - NA;
+    char* aring = lds;
+    char* bring = lds + 2 * NA * 1024;
+    auto issue_a = [&](int k) {
+      char* dst = aring + (k & 1) * NA * 1024;
+#pragma unroll
+      for (int j = 0; j < (NA + 3) / 4; ++j) {
+        const int i = wu + 4 * j;
+        if (i < NA)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                                   lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
+      }
+    };
+    auto issue_b = [&](int k) {
+      char* dst = bring + (k & 1) * NBP * 1024;
+#pragma unroll
+      for (int j = 0; j < (NBP + 3) / 4; ++j) {
+        const int i = wu + 4 * j;
+        if (i < NBP)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                                   lane * 16, (unsigned)((k * NP + NA + i) * 1024), 0, 0);
+      }
+    };
+    if (nt > 0) {
+      issue_a(0);
+      x3_wait_vm<0>();
+      asm volatile("s_barrier" ::: "memory");  // A(0) is in
+      if (nt > 1) issue_a(1);
+      issue_b(0);
+      f32x16 acc;
+      if (active) acc = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      for (int k = 0; k < nt; ++k) {
+        // A(k+1) and B(k) have landed in every wave; A slot k&1 (GEMM1(k)) and B slot
+        // (k+1)&1 (GEMM2(k-1)) were last read in iteration k-1
+        x3_wait_vm<0>();
+        asm volatile("s_barrier" ::: "memory");
+        if (k + 2 < nt) issue_a(k + 2);
+        if (k + 1 < nt) issue_b(k + 1);
+        if (!active) continue;
+        const char* bs = bring + (k & 1) * NBP * 1024;
+        f32x4 y4[4];
+        x3_labels(bs + (NBP - 1) * 1024, h, y4);
+        x3_labels_wait(y4);
+        // GEMM1 of tile k+1 (a stale slot past the last tile: computed, never used) beside
+        // the epilogue of tile k
+        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) & 1) * NA * 1024) + lane;
+        float res[16];
+        f32x16 nxt;
+        if constexpr (SCHED && KB == 4) {
+          // Hand-interleaved (in-order issue within a wave): each GEMM1(k+1) MFMA is followed
+          // by one row's epilogue of tile k, which fills the MFMA's dependency stall; the first
+          // split half then rides on the last k-block.  sched_barrier(0) pins the order; the
+          // operations and their per-value order equal x3_gemm1 / x3_epilogue / x3_gemm2.
+#pragma unroll
+          for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
+          float lin = 0.0f, prod = 1.0f;
+          auto epi1 = [&](int r) {
+            const float l = acc[r];
+            const float al = fabsf(l);
+            const float e = __builtin_amdgcn_exp2f(-al * LOG2E);
+            const float ope = 1.0f + e;
+            const float inv = __builtin_amdgcn_rcpf(ope);
+            const float num = l >= 0.0f ? 1.0f : e;
+            res[r] = __builtin_fmaf(num, inv, -y4[r >> 2][r & 3]);
+            lin += al;
+            prod *= ope;
+          };
+          bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            bf16x8 n1, n2, n3;
+            if (kb + 1 < KB) {
+              n1 = fa[(kb + 1) * 64];
+              n2 = fa[(KB + kb + 1) * 64];
+              n3 = fa[(2 * KB + kb + 1) * 64];
+            }
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
+            epi1(4 * kb + 0);
+            __builtin_amdgcn_sched_barrier(0);
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
+            epi1(4 * kb + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
+            epi1(4 * kb + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
+            epi1(4 * kb + 3);
+            __builtin_amdgcn_sched_barrier(0);
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kb + 1 < KB) {
+              a1 = n1;
+              a2 = n2;
+              a3 = n3;
+            }
+          }
+          pe += (double)(0.5f * lin) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+        } else {
+          nxt = x3_gemm1<KB>(fa, z1, z2, z3);
+          x3_epilogue(acc, y4, res, pe);
+        }
+        x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
+        acc = nxt;
+      }
+    }
+  } else if constexpr (PIPE) {
     if (nt > 0) {
       issue(0);
       if (nt > 1) issue(1);
@@ -1187,7 +1298,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
 // (workgroup b = x mod 8), the chain groups of a split on consecutive workgroups of that XCD, so
 // they share X tiles in its L2.  A workgroup whose chain group lies past the compacted list's
 // count leaves after one scalar load: the tail of a NUTS run launches thousands of them.
-template <int KB, int DT, int RING, int MINB, bool PIPE>
+template <int KB, int DT, int RING, int MINB, bool PIPE, int SCHED = 0>
 __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
                                                      int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
                                                      double* __restrict__ pepart) {
@@ -1196,7 +1307,7 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   const int ct = qb % Gt;
   const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
   if (ct * 128 >= npos) return;
-  x3_item<KB, DT, RING, PIPE>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
+  x3_item<KB, DT, RING, PIPE, SCHED>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
 }
 
 // wcol (epilogue_abs variants): U gains the per-chain linear term w . b; pe_shift removes the
@@ -1209,13 +1320,32 @@ __global__ void k_logreg_finalize(const float* __restrict__ gpart, const double*
   if (c < 0) return;
   const int ldc = ev.ldc;
   if (d < D) {
+    // slabs summed in split order; 16 loads issued ahead of their adds
+    const float* gp = gpart + (size_t)d * ldc + pos;
+    const size_t st = (size_t)D * ldc;
     float s = 0.0f;
-    for (int sp = 0; sp < S; ++sp) s += gpart[((size_t)sp * D + d) * ldc + pos];
+    int sp = 0;
+    for (; sp + 16 <= S; sp += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(gp + (size_t)(sp + j) * st);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; sp < S; ++sp) s += gp[(size_t)sp * st];
     const size_t idx = (size_t)d * ldc + c;
     ev.grad[idx] = s + ev.z[idx];
   } else {
     double s = 0.0;
-    for (int sp = 0; sp < S; ++sp) s += pepart[(size_t)sp * ldc + pos];
+    int sp = 0;
+    for (; sp + 16 <= S; sp += 16) {
+      double v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = pepart[(size_t)(sp + j) * ldc + pos];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; sp < S; ++sp) s += pepart[(size_t)sp * ldc + pos];
     double zz = 0.0, wz = 0.0;
     for (int k = 0; k < D; ++k) {
       const double z = ev.z[(size_t)k * ldc + c];
@@ -1370,13 +1500,13 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
-  if (var >= 30 && var <= 32) {
+  if (var >= 30 && var <= 35) {
     const int S2 = x3_num_splits(n_rows);
     pepart = (double*)((char*)workspace + ((size_t)S2 * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
     const int64_t nt = x3_ntiles(n_rows);
     const int KB = x3_kb(dim), DT = x3_dt(dim);
     const int ring = var == 30 ? 2 : 3;
-    const size_t lds = (size_t)ring * x3_np(dim) * 1024;
+    const size_t lds = var >= 33 ? (size_t)2 * x3_np(dim) * 1024 : (size_t)ring * x3_np(dim) * 1024;
     const char* Xq = (const char*)packed + x3_offset(n_rows, dim);
     // fixed grid: workgroups per XCD = 32 CUs x workgroups per CU (3 for the 2-slot ring)
     const int nb = std::min(ev->num_chains, ev->ldc);  // batch positions that can hold a chain
@@ -1385,7 +1515,10 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
 #define NMX_X3(kb, dt)                                                                                           \
   if (var == 30) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 2, 3, false>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
   else if (var == 31) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, false>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
-  else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
+  else if (var == 32) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else if (var == 33) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else if (var == 34) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 2, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
     if (KB == 4) { NMX_X3(4, 2) }
     else if (KB == 3) { NMX_X3(3, 2) }
     else if (KB == 2) { NMX_X3(2, 1) }

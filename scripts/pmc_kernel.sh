@@ -14,4 +14,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_W
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_COEXEC_CYCLES \
   SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CU_CYCLES --output-format csv -d "$O/b" -o p -- \
   python3 scripts/bench_potential.py "$v" 4096 > "$O/b.log" 2>&1 || exit $?
-python3 scripts/pmc_summary.py "$O" > "$O/summary.txt"
+pat=logreg_x3; case $v in 30|31|32|d) ;; *) pat=logreg_rowlanes;; esac
+python3 scripts/pmc_summary.py "$O" $pat > "$O/summary.txt"

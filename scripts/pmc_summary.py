@@ -1,5 +1,5 @@
 """Average rocprofv3 counter values per dispatch of the logreg potential kernel.
-usage: python scripts/pmc_summary.py <dir with a/ b/ pass outputs>"""
+usage: python scripts/pmc_summary.py <dir with a/ b/ pass outputs> [kernel name pattern]"""
 import csv
 import glob
 import os
@@ -7,12 +7,13 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
+pat = sys.argv[2] if len(sys.argv) > 2 else "logreg_x3"
 tot = defaultdict(float)
 cnt = defaultdict(set)
 for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(path) as f:
         for row in csv.DictReader(f):
-            if "logreg_rowlanes" not in row.get("Kernel_Name", ""):
+            if pat not in row.get("Kernel_Name", ""):
                 continue
             name = row["Counter_Name"]
             tot[name] += float(row["Counter_Value"])
