@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 MI355X_FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (matrix), dense
 MI355X_BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
 MI355X_HBM_PEAK_GBS = 8000.0
-# The default covtype kernel (NMX_LOGREG_VARIANT 30-32, potential_logreg.hip) runs each f32
+# The default covtype kernel (NMX_LOGREG_VARIANT 30-36, potential_logreg.hip) runs each f32
 # product as six bf16 MFMA products of three-term splits: its f32-equivalent ceiling is the
 # bf16 MFMA peak / 6.  The f32-MFMA kernels (variants < 30) are bounded by the f32 matrix peak.
 SPLIT_PRODUCTS = 6
@@ -167,8 +167,8 @@ def main():
     local_useful = stats[0].item()
     flop = 4.0 * args.rows * X.shape[1] * local_useful
     achieved = flop / (pot_ms * 1e-3) / 1e12 if pot_ms > 0 else 0.0
-    variant = int(os.environ.get("NMX_LOGREG_VARIANT", "30"))
-    split = 30 <= variant <= 32
+    variant = int(os.environ.get("NMX_LOGREG_VARIANT", "36"))
+    split = 30 <= variant <= 36
     peak = MI355X_BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS if split else MI355X_FP32_MFMA_PEAK_TFLOPS
     traffic = None
     try:

@@ -1007,6 +1007,9 @@ __device__ __forceinline__ void x3_labels_wait(f32x4 (&y4)[4]) {
 
 // Bernoulli-logits epilogue (epilogue_abs arithmetic; no row mask: padded rows have l = 0):
 // acc -> sigmoid(l) - y, U terms into pe
+// L2E: the accumulator holds m = -l log2(e) (Z pre-scaled by -log2 e before its split), so
+// e = 2^-|m| needs no multiply and sum |l| = ln 2 sum |m|
+template <bool L2E = false>
 __device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&y4)[4], float (&res)[16], double& pe) {
   float lin = 0.0f, prod = 1.0f;
 #pragma unroll
@@ -1016,16 +1019,16 @@ __device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&y4)
       const int r = 4 * q + u;
       const float l = acc[r];
       const float al = fabsf(l);
-      const float e = __builtin_amdgcn_exp2f(-al * LOG2E);
+      const float e = __builtin_amdgcn_exp2f(L2E ? -al : -al * LOG2E);
       const float ope = 1.0f + e;
       const float inv = __builtin_amdgcn_rcpf(ope);
-      const float num = l >= 0.0f ? 1.0f : e;
+      const float num = (L2E ? l <= 0.0f : l >= 0.0f) ? 1.0f : e;
       res[r] = __builtin_fmaf(num, inv, -y4[q][u]);
       lin += al;
       prod *= ope;
     }
   }
-  pe += (double)(0.5f * lin) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+  pe += (double)(0.5f * lin) * (L2E ? (double)LN2 : 1.0) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
 }
 
 // GEMM2 of one tile: G += X^T . R, R split into three bf16 terms (k-step s = registers 8s..8s+7)
@@ -1058,7 +1061,7 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 // are independent), then GEMM2 of tile k; needs RING = 3 (slots k, k+1 read, k+2 filling).
 // The per-chain arithmetic and its order are the same in both forms (bitwise equal results).
 //
-template <int KB, int DT, int RING, bool PIPE, int SCHED>
+template <int KB, int DT, int RING, bool PIPE, int SCHED, bool L2E>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
                                         nmx_eval_batch ev, float* __restrict__ gpart,
                                         double* __restrict__ pepart) {
@@ -1098,6 +1101,10 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zoff, (16 * kb + j) * ldc * 4, 0));
+    if constexpr (L2E) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= -LOG2E;
+    }
     split3(v, z1[kb], z2[kb], z3[kb]);
   }
   f32x16 g[DT];
@@ -1223,7 +1230,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
           pe += (double)(0.5f * lin) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
         } else {
           nxt = x3_gemm1<KB>(fa, z1, z2, z3);
-          x3_epilogue(acc, y4, res, pe);
+          x3_epilogue<L2E>(acc, y4, res, pe);
         }
         x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
         acc = nxt;
@@ -1256,7 +1263,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         // epilogue of tile k
         const f32x16 nxt = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(slot(k + 1)) + lane, z1, z2, z3);
         float res[16];
-        x3_epilogue(acc, y4, res, pe);
+        x3_epilogue<L2E>(acc, y4, res, pe);
         x3_gemm2<KB, DT>(frk, res, g);
         acc = nxt;
       }
@@ -1278,7 +1285,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
       const f32x16 acc = x3_gemm1<KB>(fr, z1, z2, z3);
       x3_labels_wait(y4);
       float res[16];
-      x3_epilogue(acc, y4, res, pe);
+      x3_epilogue<L2E>(acc, y4, res, pe);
       x3_gemm2<KB, DT>(fr, res, g);
     }
   }
@@ -1298,7 +1305,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
 // (workgroup b = x mod 8), the chain groups of a split on consecutive workgroups of that XCD, so
 // they share X tiles in its L2.  A workgroup whose chain group lies past the compacted list's
 // count leaves after one scalar load: the tail of a NUTS run launches thousands of them.
-template <int KB, int DT, int RING, int MINB, bool PIPE, int SCHED = 0>
+template <int KB, int DT, int RING, int MINB, bool PIPE, int SCHED = 0, bool L2E = false>
 __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
                                                      int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
                                                      double* __restrict__ pepart) {
@@ -1307,7 +1314,7 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   const int ct = qb % Gt;
   const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
   if (ct * 128 >= npos) return;
-  x3_item<KB, DT, RING, PIPE, SCHED>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
+  x3_item<KB, DT, RING, PIPE, SCHED, L2E>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
 }
 
 // wcol (epilogue_abs variants): U gains the per-chain linear term w . b; pe_shift removes the
@@ -1363,7 +1370,15 @@ int check_ev(const nmx_eval_batch* ev) {
   return NMX_OK;
 }
 
-// Kernel variant (A/B experiments).  The gradient is bitwise the same in all row-lane forms
+// Kernel variant (A/B experiments).
+//   36 (default) split-bf16 k_logreg_x3: split rings (A/B parts, 2 slots each, 50 KB ->
+//      3 workgroups/CU), GEMM1 of tile k+1 issued beside the epilogue of tile k, Z pre-scaled
+//      by -log2(e) (no multiply before v_exp).  30 = 2-slot ring, unpipelined; 31 = 3-slot;
+//      32 = pipelined on one 3-slot ring; 33 = 36 without the pre-scale; 34/35 = 33 hand-
+//      interleaved with sched_barrier at 3/2 workgroups per CU.  30-35 are bitwise equal.
+//      C=4096 all-active, f32-equivalent TFLOP/s (scripts/logreg_variant_check.py, one box):
+//      36: 180.9, 33: 178.1, 30: 175.0 (others 165-175); f32-MFMA 22: 116.5.
+// f32-MFMA forms (< 30).  The gradient is bitwise the same in all row-lane forms
 // (same MFMA sequence per chain, explicit fmas in the epilogue); 17-25 round U differently
 // (product-of-factors log, |l| sums + w.b) at ~1e-7 relative; 21 also rounds the logits
 // differently (z pre-scaled by -log2 e).
@@ -1385,7 +1400,7 @@ int check_ev(const nmx_eval_batch* ev) {
 // PMC (scripts/pmc_kernel.sh): MFMA pipe busy 82.5% (19) vs 72.4% (11) of SIMD cycles.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
-  return e ? atoi(e) : 30;
+  return e ? atoi(e) : 36;
 }
 
 template <int KS, int NBUF, bool PRIO>
@@ -1500,7 +1515,7 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const float* Xp = (const float*)packed;
   const int KS = k_of(dim) / 2;
   const int var = variant();
-  if (var >= 30 && var <= 35) {
+  if (var >= 30 && var <= 36) {
     const int S2 = x3_num_splits(n_rows);
     pepart = (double*)((char*)workspace + ((size_t)S2 * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
     const int64_t nt = x3_ntiles(n_rows);
@@ -1518,7 +1533,8 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   else if (var == 32) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 3, 2, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
   else if (var == 33) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
   else if (var == 34) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
-  else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 2, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
+  else if (var == 35) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 2, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
+  else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true, 0, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
     if (KB == 4) { NMX_X3(4, 2) }
     else if (KB == 3) { NMX_X3(3, 2) }
     else if (KB == 2) { NMX_X3(2, 1) }
