@@ -11,7 +11,7 @@ line = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 n = int(line["leapfrog_launches"])
 out = {"timed_launches": n, "bench_potential_ms_per_launch": line["potential_ms_per_launch"]}
 total = 0.0
-for key in ("logreg_rowlanes", "logreg_finalize"):
+for key in ("logreg_x3", "logreg_finalize"):
     k = sorted((r for r in rows if key in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))[-n:]
     ms = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in k) / len(k) / 1e6
     out[f"{key}_ms_avg"] = ms

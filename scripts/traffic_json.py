@@ -10,12 +10,15 @@ import statistics
 import sys
 
 
+KERNEL = os.environ.get("TRAFFIC_KERNEL", "logreg_x3")
+
+
 def values(root, counter):
     out = []
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "logreg_rowlanes" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                if KERNEL in row["Kernel_Name"] and row["Counter_Name"] == counter:
                     out.append(float(row["Counter_Value"]))
     return out
 
@@ -33,9 +36,9 @@ out = {
     "write_size_kb_median": w_kb,
     "dispatches": len(fetch),
     "hbm_bytes_per_launch": (2.0 * f_kb + w_kb) * 1024.0,
-    "algorithmic_bytes_note": "packed X 581120 rows x 57 f32 = 132.5 MB read once per launch (chain tiles of a "
-                              "split share it through the XCD L2); slabs 128 x 55 x 4096 f32 + 128 x 4096 f64 "
-                              "= 119.5 MB written",
+    "algorithmic_bytes_note": "split-bf16 tiles: 18157 x 25 KB = 465 MB of packed X read once per launch "
+                              "(the chain groups of a split share it through the XCD L2); slabs 256 x 55 x 4096 "
+                              "f32 + 256 x 4096 f64 = 239 MB written (read back by k_logreg_finalize)",
 }
 with open(sys.argv[3], "w") as f:
     json.dump(out, f, indent=1)
