@@ -17,6 +17,8 @@
 #include <string.h>
 
 #include "nmx_api_internal.h"
+#include <stdlib.h>
+
 #include "nmx_common.h"
 
 namespace {
@@ -26,7 +28,15 @@ constexpr int NPART = 2 * MAXD + 3;  // KE, checkpoint dots (2 per level), whole
 constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide schedule)
 
 inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
-inline int num_slices(int D) { return D >= WIDE_MIN_D ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
+// NMX_WIDE_MIN_D overrides the threshold (A/B experiments; a function of D alone either way)
+inline int wide_min_d() {
+  static const int v = [] {
+    const char* e = getenv("NMX_WIDE_MIN_D");
+    return e ? atoi(e) : WIDE_MIN_D;
+  }();
+  return v;
+}
+inline int num_slices(int D) { return D >= wide_min_d() ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
 constexpr size_t ALIGN = 256;
 
 inline size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }

@@ -3,23 +3,24 @@
 //   U(b)  = sum_n [max(l_n,0) + log1p(exp(-|l_n|)) - y_n l_n] + sum_d [b_d^2/2 + log(2pi)/2]
 //   dU/db = X^T (sigmoid(l) - y) + b,      l = X b          
 //
-// For a 32-row tile and 32 chains a wave computes L = X.Z with v_mfma_f32_32x32x2_f32
-// (exact f32 fma chains), applies the Bernoulli epilogue to the accumulator registers in
-// place, and feeds those same registers as the B operand of G += X^T.R: the 32x32 result
-// holds chains on the lane and rows in the registers, and the 32x32x2 B operand wants
-// exactly (row pair, chain) on (lane half, lane) -- no shuffle, no LDS round trip, and the
+// Default kernel: k_logreg_x3 (variant 36), f32-accurate split-bf16 GEMMs on the bf16 matrix
+// cores (section "Split-bf16 kernel" below).  f32-MFMA forms (variant 22 k_logreg_rowlanes,
+// the generic k_logreg_tiles) stay as A/B references.  In all of them, for a 32-row tile and
+// 32 chains a wave computes L = X.Z, applies the Bernoulli epilogue to the accumulator
+// registers in place and feeds them as the B operand of G += X^T.R: the 32x32 result holds
+// chains on the lane and rows in the registers, which is the B-operand layout (for the
+// 32x32x16 bf16 form with the k order permuted) -- no shuffle, no LDS round trip, and the
 // N x C logit matrix never exists in memory.
 //
-// Packed X (nmx_logreg_pack): 64-row tiles, each row K+1 floats (K = round_up(D, 2)):
-// x_0..x_{D-1}, zero pad up to K, then the label y.  The odd row stride K+1 makes the
-// GEMM1 operand read (32 lanes = 32 rows, same column) bank-conflict free and puts the
-// label next to its row.  A tile is one contiguous block, copied to LDS with 16-byte loads.
+// Packed X (nmx_logreg_pack): f32 rows for the f32 kernels (128-row padding, each row K+1
+// floats, K = round_up(D, 2): x_0..x_{D-1}, zero pad, label; the odd stride makes the GEMM1
+// operand read bank-conflict free), the float64 column terms w, then the split-bf16 tiles.
 //
-// Work split: grid = chain groups (128 chains = 4 waves) x S row splits.  S depends on
-// n_rows only, and each split sums its rows in a fixed order, so a chain's U and dU do
-// not depend on how many chains share the launch (GPU-count invariance).  Per-split
-// partials go to slabs reduced in fixed order by k_logreg_finalize.  Workgroups of the
-// same split are placed on one XCD (blockIdx % 8) so the chain groups share X tiles in L2.
+// Work split: grid = chain groups x S row splits.  S depends on n_rows only, and each split
+// sums its rows in a fixed order, so a chain's U and dU do not depend on how many chains
+// share the launch (GPU-count invariance).  Per-split partials go to slabs reduced in fixed
+// order by k_logreg_finalize.  Workgroups of the same split are placed on one XCD
+// (blockIdx % 8) so the chain groups share X tiles in L2.
 #include <math.h>
 #include <stdlib.h>
 
@@ -208,99 +209,15 @@ __global__ __launch_bounds__(NW * 64) void k_logreg_tiles(const float* __restric
 }
 
 // ---------------------------------------------------------------------------------------
-// Row-lane kernel (the production path for covtype, D = 55).
-//
-// Workgroup = 4 waves sharing ONE 32-chain tile; each stage is 128 rows (4 subtiles of 32)
-// filled into LDS by global_load_lds (double-buffered, no VGPR staging), and wave w takes
-// subtile w, so the 4 waves are 4 "row lanes" of the split.  At the end the lanes' partial
-// gradients are combined in a fixed order.  Compared with one wave walking all rows of a
-// split this gives 4x the parallelism per chain, which is what bounds a launch when only a
-// few chains are still integrating (the tail of a run, sync-mode stragglers); the
-// summation order depends on n_rows only, never on how many chains are evaluated.
+// f32-MFMA row-lane kernel (variant 22, D = 55): see k_logreg_rowlanes below.
 // ---------------------------------------------------------------------------------------
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-template <int KS>
-__device__ __forceinline__ void gemm1(const float* xt, const float (&zb)[KS], int l31, int h, f32x16& acc) {
-  constexpr int XS = 2 * KS + 1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[s], acc, 0, 0, 0);
-}
-
-// acc <- sigmoid(l) - y in place; accumulates sum(max(l,0) - l*y) and sum(log2(1+e^-|l|))
-template <int KS, bool MASK>
-__device__ __forceinline__ void epilogue(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
-                                         float& lin, float& lg2) {
-  constexpr int XS = 2 * KS + 1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const float y = xt[rr * XS + (XS - 1)];
-    const float l = acc[r];
-    const float e = __builtin_amdgcn_exp2f(-fabsf(l) * LOG2E);
-    const float ope = 1.0f + e;
-    const float inv = __builtin_amdgcn_rcpf(ope);
-    const float num = l >= 0.0f ? 1.0f : e;
-    // explicit fmas: the rounding must not depend on how the compiler contracts (kernel
-    // variants compute bitwise the same values)
-    float res = __builtin_fmaf(num, inv, -y);
-    float li = __builtin_fmaf(-l, y, fmaxf(l, 0.0f));
-    float lo = __builtin_amdgcn_logf(ope);
-    if (MASK) {
-      const bool ok = rowbase + rr < n_rows;
-      res = ok ? res : 0.0f;
-      li = ok ? li : 0.0f;
-      lo = ok ? lo : 0.0f;
-    }
-    lin += li;
-    lg2 += lo;
-    acc[r] = res;
-  }
-}
-
-// Same as epilogue(), with sum(log2(1+e)) taken as log2 of the product of the 16 factors
-// (each in [1, 2], so the product stays below 2^16): one v_log per 16 rows instead of 16.
-// The product rounds 16 times (<= ~1e-6 relative, ~1e-6 absolute after the log) -- far below
-// the f32 rounding of U itself (|U| ~ 1e5); the gradient path is unchanged.
-template <int KS, bool MASK>
-__device__ __forceinline__ void epilogue_prod(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
-                                              float& lin, float& lg2) {
-  constexpr int XS = 2 * KS + 1;
-  float prod = 1.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const float y = xt[rr * XS + (XS - 1)];
-    const float l = acc[r];
-    const float e = __builtin_amdgcn_exp2f(-fabsf(l) * LOG2E);
-    float ope = 1.0f + e;
-    const float inv = __builtin_amdgcn_rcpf(ope);
-    const float num = l >= 0.0f ? 1.0f : e;
-    // explicit fmas: the rounding must not depend on how the compiler contracts (kernel
-    // variants compute bitwise the same values)
-    float res = __builtin_fmaf(num, inv, -y);
-    float li = __builtin_fmaf(-l, y, fmaxf(l, 0.0f));
-    if (MASK) {
-      const bool ok = rowbase + rr < n_rows;
-      res = ok ? res : 0.0f;
-      li = ok ? li : 0.0f;
-      ope = ok ? ope : 1.0f;
-    }
-    lin += li;
-    prod *= ope;
-    acc[r] = res;
-  }
-  lg2 += __builtin_amdgcn_logf(prod);
-}
-
-// epilogue_prod plus the linear part taken out of the row loop: with
+// acc <- sigmoid(l) - y in place, with the linear part of U taken out of the row loop:
 //   max(l,0) - l y = (|l| + l)/2 - l y,   sum_n l_n = (sum_n x_n) . b,   sum_n l_n y_n = (X^T y) . b,
 // the rows only accumulate |l| and the chain adds w . b once, w = sum_n x_n / 2 - X^T y
-// (k_logreg_colsums, float64).  4 VALU ops per row fewer; the gradient path is unchanged.
+// (k_logreg_colsums, float64); log(1+e) summed as log2 of the product of the 16 factors.
 template <int KS, bool MASK>
 __device__ __forceinline__ void epilogue_abs(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
                                              float& lin, float& lg2) {
@@ -331,306 +248,23 @@ __device__ __forceinline__ void epilogue_abs(const float* xt, int h, int64_t row
   lg2 += __builtin_amdgcn_logf(prod);
 }
 
-// epilogue_abs on m = -l log2(e) (z pre-scaled in GEMM1): e = 2^-|m| straight from the
-// accumulator (no multiply); lin collects |m| / 2 (the caller scales by ln 2).
-template <int KS, bool MASK>
-__device__ __forceinline__ void epilogue_log2(const float* xt, int h, int64_t rowbase, int64_t n_rows, f32x16& acc,
-                                              float& lin, float& lg2) {
-  constexpr int XS = 2 * KS + 1;
-  float prod = 1.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const float y = xt[rr * XS + (XS - 1)];
-    const float m = acc[r];
-    float am = fabsf(m);
-    const float e = __builtin_amdgcn_exp2f(-am);
-    float ope = 1.0f + e;
-    const float inv = __builtin_amdgcn_rcpf(ope);
-    const float num = m <= 0.0f ? 1.0f : e;
-    float res = __builtin_fmaf(num, inv, -y);
-    if (MASK) {
-      const bool ok = rowbase + rr < n_rows;
-      res = ok ? res : 0.0f;
-      am = ok ? am : 0.0f;
-      ope = ok ? ope : 1.0f;
-    }
-    lin += am;
-    prod *= ope;
-    acc[r] = res;
-  }
-  lin *= 0.5f;
-  lg2 += __builtin_amdgcn_logf(prod);
-}
-
-template <int KS>
-__device__ __forceinline__ void gemm2(const float* xt, const f32x16& res, int l31, int h, f32x16& g0, f32x16& g1) {
-  constexpr int XS = 2 * KS + 1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-    g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], res[r], g0, 0, 0, 0);
-    if (KS > 16) g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], res[r], g1, 0, 0, 0);
-  }
-}
-
 constexpr int RL_WAVES = 4;             // row lanes per workgroup
 constexpr int RL_ROWS = 32 * RL_WAVES;  // rows per stage (= PACK)
 static_assert(RL_ROWS == PACK, "row-lane stage must equal the packing granularity");
 
-template <int KS, int NBUF, bool PRIO>
-__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes(const float* __restrict__ Xp, int64_t n_rows,
-                                                                      int nstages, int D, int S, int Gt,
-                                                                      nmx_eval_batch ev, float* __restrict__ gpart,
-                                                                      double* __restrict__ pepart) {
-  constexpr int XS = 2 * KS + 1;
-  constexpr int STAGE = RL_ROWS * XS;               // floats per stage
-  constexpr int BUF = (STAGE + LDS_SLACK + 255) / 256 * 256;
-  constexpr int CHUNKS = STAGE / 4;                 // 16-byte pieces
-  constexpr int NINST = (CHUNKS + 63) / 64;         // wave-instructions per stage
-  extern __shared__ __attribute__((aligned(16))) float xs[];
-  const int b = blockIdx.x;
-  const int xcd = b & 7;
-  const int q = b >> 3;
-  const int ct = q % Gt;
-  const int split = (q / Gt) * 8 + xcd;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int h = lane >> 5;
-  const int l31 = lane & 31;
-  const int ldc = ev.ldc;
-  const int pos = ct * 32 + l31;  // batch position (slab column); same chains in all 4 waves
-  const bool cin = pos < ldc;
-  const int c = cin ? nmx_eval_chain(ev, pos) : -1;
-  const bool act = c >= 0;
-  if (!__any(act)) return;  // identical in all waves of the workgroup
-
-  const int per = (nstages + S - 1) / S;
-  const int t0 = split * per;
-  const int t1 = min(t0 + per, nstages);
-
-  auto stage_in = [&](int t, int buf) {
-    const char* src = reinterpret_cast<const char*>(Xp + (size_t)t * STAGE);
-    float* dst = xs + buf * BUF;
-#pragma unroll
-    for (int i = w; i < NINST; i += RL_WAVES) {
-      const int chunk = i * 64 + lane;
-      if (chunk < CHUNKS)
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + chunk * 16),
-                                         (void __attribute__((address_space(3)))*)(dst + i * 256), 16, 0, 0);
-    }
-  };
-
-  float zb[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 2 * s + h;
-    zb[s] = (k < D && act) ? ev.z[(size_t)k * ldc + c] : 0.0f;
-  }
-  f32x16 g0, g1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    g0[r] = 0.0f;
-    g1[r] = 0.0f;
-  }
-  double pe = 0.0;
-  if (NBUF == 2 && t0 < t1) stage_in(t0, 0);
-  __syncthreads();
-  for (int t = t0; t < t1; ++t) {
-    const int buf = NBUF == 2 ? (t - t0) & 1 : 0;
-    if (NBUF == 2) {
-      if (t + 1 < t1) stage_in(t + 1, buf ^ 1);
-    } else {
-      stage_in(t, 0);
-      __syncthreads();
-    }
-    const float* xt = xs + buf * BUF + w * 32 * XS;
-    const int64_t rb = (int64_t)t * RL_ROWS + w * 32;
-    f32x16 a0;
-    float lin = 0.0f, lg2 = 0.0f;
-    // PRIO: waves in their MFMA chains get issue priority over waves in the VALU epilogue,
-    // so co-resident waves drift out of phase and the epilogues run under other waves' MFMAs
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    gemm1<KS>(xt, zb, l31, h, a0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    if (rb + 32 <= n_rows) epilogue<KS, false>(xt, h, rb, n_rows, a0, lin, lg2);
-    else epilogue<KS, true>(xt, h, rb, n_rows, a0, lin, lg2);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    gemm2<KS>(xt, a0, l31, h, g0, g1);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    pe += (double)lin + (double)lg2 * (double)LN2;
-    __syncthreads();  // drains this stage's global_load_lds (vmcnt(0)) and frees buf
-  }
-  pe += __shfl_xor(pe, 32);
-
-  // fixed-order combination of the 4 row lanes: lane partials staged through LDS
-  float* red = xs;                                   // [RL_WAVES][32][64] floats
-  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    red[(w * 32 + r) * 64 + lane] = g0[r];
-    red[(w * 32 + 16 + r) * 64 + lane] = g1[r];
-  }
-  red_pe[w * 64 + lane] = pe;
-  __syncthreads();
-  if (w == 0 && cin) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
-#pragma unroll
-      for (int ww = 1; ww < RL_WAVES; ++ww) {
-        s0 += red[(ww * 32 + r) * 64 + lane];
-        s1 += red[(ww * 32 + 16 + r) * 64 + lane];
-      }
-      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
-      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
-    }
-    if (h == 0) {
-      double sp = red_pe[lane];
-#pragma unroll
-      for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
-      pepart[(size_t)split * ldc + pos] = sp;
-    }
-  }
-}
-
-// Wave-pipelined variant: the 4 row lanes of a workgroup never synchronise inside the
-// loop.  Wave w owns the 32-row subtile w of each 128-row stage; it prefetches its next
-// subtile into registers (8 x 16 B per lane) while the MFMAs of the current one run,
-// then writes it to its private LDS slice (the operand transpose) -- so neither global
-// latency nor a workgroup barrier sits between two tiles.
+// f32-MFMA row-lane kernel (variant 22; the default before the split-bf16 kernel, kept as the
+// f32 A/B reference).  Workgroup = 4 waves sharing ONE 32-chain tile; each wave is a "row
+// lane" taking one 32-row subtile of each 128-row stage, DMA'd into its own LDS slice by
+// buffer LDS-DMA (no workgroup barrier in the row loop); the last stage (rows >= N) is peeled
+// so the unmasked epilogue is branch-free.  The 4 lanes' partials are combined in a fixed
+// order at the end; S row splits depend on n_rows only.
 template <int KS>
-__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_wavepipe(const float* __restrict__ Xp, int64_t n_rows,
-                                                                    int nstages, int D, int S, int Gt,
-                                                                    nmx_eval_batch ev, float* __restrict__ gpart,
-                                                                    double* __restrict__ pepart) {
-  constexpr int XS = 2 * KS + 1;
-  constexpr int SUB = 32 * XS;                      // floats per wave subtile
-  constexpr int CHUNKS = SUB / 4;                   // 16-byte pieces (SUB % 4 == 0 for XS odd? see assert)
-  constexpr int NCH = (CHUNKS + 63) / 64;           // float4 per lane
-  constexpr int WBUF = (SUB + 3) / 4 * 4 + 64;      // per-wave LDS floats
-  static_assert((32 * XS) % 4 == 0, "subtile must be a whole number of float4");
-  extern __shared__ __attribute__((aligned(16))) float xs[];
-  const int b = blockIdx.x;
-  const int xcd = b & 7;
-  const int q = b >> 3;
-  const int ct = q % Gt;
-  const int split = (q / Gt) * 8 + xcd;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int h = lane >> 5;
-  const int l31 = lane & 31;
-  const int ldc = ev.ldc;
-  const int pos = ct * 32 + l31;
-  const bool cin = pos < ldc;
-  const int c = cin ? nmx_eval_chain(ev, pos) : -1;
-  const bool act = c >= 0;
-  if (!__any(act)) return;
-
-  const int per = (nstages + S - 1) / S;
-  const int t0 = split * per;
-  const int t1 = min(t0 + per, nstages);
-  float* const xt = xs + w * WBUF;
-
-  float zb[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 2 * s + h;
-    zb[s] = (k < D && act) ? ev.z[(size_t)k * ldc + c] : 0.0f;
-  }
-  f32x16 g0, g1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    g0[r] = 0.0f;
-    g1[r] = 0.0f;
-  }
-  double pe = 0.0;
-  float4 pf[NCH];
-  auto fetch = [&](int t) {
-    const float4* src = reinterpret_cast<const float4*>(Xp + ((size_t)t * RL_ROWS + w * 32) * XS);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int chunk = i * 64 + lane;
-      pf[i] = chunk < CHUNKS ? src[chunk] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int chunk = i * 64 + lane;
-      if (chunk < CHUNKS) reinterpret_cast<float4*>(xt)[chunk] = pf[i];
-    }
-  };
-  if (t0 < t1) fetch(t0);
-  for (int t = t0; t < t1; ++t) {
-    commit();                       // LDS in-order per wave: the reads below see it
-    if (t + 1 < t1) fetch(t + 1);   // in flight during this tile's MFMAs
-    const int64_t rb = (int64_t)t * RL_ROWS + w * 32;
-    f32x16 a0;
-    float lin = 0.0f, lg2 = 0.0f;
-    {
-      __builtin_amdgcn_s_setprio(1);
-      gemm1<KS>(xt, zb, l31, h, a0);
-      __builtin_amdgcn_s_setprio(0);
-      if (rb + 32 <= n_rows) epilogue<KS, false>(xt, h, rb, n_rows, a0, lin, lg2);
-      else epilogue<KS, true>(xt, h, rb, n_rows, a0, lin, lg2);
-      __builtin_amdgcn_s_setprio(1);
-      gemm2<KS>(xt, a0, l31, h, g0, g1);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    pe += (double)lin + (double)lg2 * (double)LN2;
-  }
-  pe += __shfl_xor(pe, 32);
-  __syncthreads();
-
-  float* red = xs;                                   // [RL_WAVES][32][64] floats
-  double* red_pe = reinterpret_cast<double*>(xs + RL_WAVES * 32 * 64);  // [RL_WAVES][64]
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    red[(w * 32 + r) * 64 + lane] = g0[r];
-    red[(w * 32 + 16 + r) * 64 + lane] = g1[r];
-  }
-  red_pe[w * 64 + lane] = pe;
-  __syncthreads();
-  if (w == 0 && cin) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float s0 = red[r * 64 + lane], s1 = red[(16 + r) * 64 + lane];
-#pragma unroll
-      for (int ww = 1; ww < RL_WAVES; ++ww) {
-        s0 += red[(ww * 32 + r) * 64 + lane];
-        s1 += red[(ww * 32 + 16 + r) * 64 + lane];
-      }
-      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
-      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
-    }
-    if (h == 0) {
-      double sp = red_pe[lane];
-#pragma unroll
-      for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[ww * 64 + lane];
-      pepart[(size_t)split * ldc + pos] = sp;
-    }
-  }
-}
-
-// Row lanes with CT chain tiles per wave: every X operand read from LDS feeds CT MFMAs, and
-// each stage's load + barrier is amortised over CT x the matrix work.  Per chain the MFMA
-// sequence (rows, k order, lanes) is the one of k_logreg_rowlanes, so the sums are bitwise
-// the same; only the grouping of chains into workgroups differs (ct = 64-chain group).
-template <int KS, int CT, bool PRIO, bool ILP, int EPI, bool WAVE, int MINB>
-__global__ __launch_bounds__(RL_WAVES * 64, MINB) void k_logreg_rowlanes_ct(const float* __restrict__ Xp,
-                                                                         int64_t n_rows, int nstages, int D, int S,
-                                                                         int Gt, nmx_eval_batch ev,
-                                                                         float* __restrict__ gpart,
-                                                                         double* __restrict__ pepart) {
+__global__ __launch_bounds__(RL_WAVES * 64, 2) void k_logreg_rowlanes(const float* __restrict__ Xp, int64_t n_rows,
+                                                                     int nstages, int D, int S, int Gt,
+                                                                     nmx_eval_batch ev, float* __restrict__ gpart,
+                                                                     double* __restrict__ pepart) {
   constexpr int XS = 2 * KS + 1;
   constexpr int STAGE = RL_ROWS * XS;
-  constexpr int CHUNKS = STAGE / 4;
-  constexpr int NINST = (CHUNKS + 63) / 64;
   constexpr int WPIECES = (32 * XS + 255) / 256;  // 1 KB DMA pieces per wave subtile
   constexpr int WSLICE = WPIECES * 256;           // floats per wave slice
   extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -645,15 +279,9 @@ __global__ __launch_bounds__(RL_WAVES * 64, MINB) void k_logreg_rowlanes_ct(cons
   const int h = lane >> 5;
   const int l31 = lane & 31;
   const int ldc = ev.ldc;
-  int cc[CT];
-  bool any = false;
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int pos = (ct * CT + t) * 32 + l31;
-    cc[t] = pos < ldc ? nmx_eval_chain(ev, pos) : -1;
-    any |= cc[t] >= 0;
-  }
-  if (!__any(any)) return;  // identical in all waves of the workgroup
+  const int pos = ct * 32 + l31;
+  const int cc = pos < ldc ? nmx_eval_chain(ev, pos) : -1;
+  if (!__any(cc >= 0)) return;  // identical in all waves of the workgroup
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)Xp, 0, nstages * STAGE * 4, 0x00020000);
@@ -662,176 +290,93 @@ __global__ __launch_bounds__(RL_WAVES * 64, MINB) void k_logreg_rowlanes_ct(cons
   const int t0 = split * per;
   const int t1 = min(t0 + per, nstages);
 
-  float zb[CT][KS];
+  float zb[KS];
 #pragma unroll
-  for (int t = 0; t < CT; ++t)
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    zb[s] = (k < D && cc >= 0) ? ev.z[(size_t)k * ldc + cc] : 0.0f;
+  }
+  f32x16 g0, g1;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int k = 2 * s + h;
-      zb[t][s] = (k < D && cc[t] >= 0) ? ev.z[(size_t)k * ldc + cc[t]] : 0.0f;
-      if constexpr (EPI == 3) zb[t][s] *= -LOG2E;  // GEMM1 yields -l log2(e) (epilogue_log2)
-    }
-  f32x16 g0[CT], g1[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      g0[t][r] = 0.0f;
-      g1[t][r] = 0.0f;
-    }
-  double pe[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) pe[t] = 0.0;
+  for (int r = 0; r < 16; ++r) {
+    g0[r] = 0.0f;
+    g1[r] = 0.0f;
+  }
+  double pe = 0.0;
   // TAIL: the stage holds rows >= n_rows (only the last one can): masked epilogue
   auto stage = [&](int st, auto tailc) {
     constexpr bool TAIL = decltype(tailc)::value;
-    const float* xt;
-    if constexpr (WAVE) {
-      // wave-private pipeline: each wave DMAs only its own 32-row subtile into its own LDS
-      // slice and waits for its own loads -- no workgroup barrier couples the 4 SIMDs.  Its
-      // previous reads of the slice were consumed (MFMA/VALU operands) before this point.
-      static_assert(CT == 1, "wave-private staging is written for one chain tile");
-      float* xw = xs + wu * WSLICE;
-      const unsigned base = (unsigned)(((int64_t)st * RL_ROWS + wu * 32) * XS * 4);
-      asm volatile("" ::: "memory");
+    // wave-private pipeline: each wave DMAs only its own 32-row subtile into its own LDS slice
+    // and waits for its own loads; its previous reads of the slice were consumed (MFMA/VALU
+    // operands) before this point
+    float* xt = xs + wu * WSLICE;
+    const unsigned base = (unsigned)(((int64_t)st * RL_ROWS + wu * 32) * XS * 4);
+    asm volatile("" ::: "memory");
 #pragma unroll
-      for (int i = 0; i < WPIECES; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(xw + i * 256), 16,
-                                                 lane * 16, base + i * 1024, 0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      xt = xw;
-    } else {
-      // buffer LDS-DMA: scalar descriptor + stage offset, one 32-bit lane offset; the last
-      // piece's lanes past the stage read the next stage (or 0 past the end, range check)
-      // into the LDS slack
-#pragma unroll
-      for (int j = 0; j < (NINST + RL_WAVES - 1) / RL_WAVES; ++j) {
-        const int i = wu + j * RL_WAVES;
-        if (i < NINST)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              xrs, (__attribute__((address_space(3))) void*)(xs + i * 256), 16, lane * 16,
-              (unsigned)(st * STAGE * 4 + i * 1024), 0, 0);
-      }
-      __syncthreads();
-      xt = xs + w * 32 * XS;
-    }
+    for (int i = 0; i < WPIECES; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(xt + i * 256), 16,
+                                               lane * 16, base + i * 1024, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int64_t rb = (int64_t)st * RL_ROWS + w * 32;
-    f32x16 a[CT];
+    f32x16 a;
 #pragma unroll
-    for (int t = 0; t < CT; ++t)
+    for (int r = 0; r < 16; ++r) a[r] = 0.0f;
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) a[t][r] = 0.0f;
-    auto epi = [&](int t) {
-      float lin = 0.0f, lg2 = 0.0f;
-      // per wave, as in k_logreg_rowlanes: only the waves holding rows >= n_rows mask
-      if constexpr (EPI == 3) {
-        if (TAIL && rb + 32 > n_rows) epilogue_log2<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
-        else epilogue_log2<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
-      } else if constexpr (EPI == 2) {
-        if (TAIL && rb + 32 > n_rows) epilogue_abs<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
-        else epilogue_abs<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
-      } else if constexpr (EPI == 1) {
-        if (TAIL && rb + 32 > n_rows) epilogue_prod<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
-        else epilogue_prod<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
-      } else {
-        if (TAIL && rb + 32 > n_rows) epilogue<KS, true>(xt, h, rb, n_rows, a[t], lin, lg2);
-        else epilogue<KS, false>(xt, h, rb, n_rows, a[t], lin, lg2);
-      }
-      pe[t] += (EPI == 3 ? (double)LN2 : 1.0) * (double)lin + (double)lg2 * (double)LN2;
-    };
-    auto g1_tile = [&](int t) {
+    for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[s], a, 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    float lin = 0.0f, lg2 = 0.0f;
+    // only the waves holding rows >= n_rows mask
+    if (TAIL && rb + 32 > n_rows) epilogue_abs<KS, true>(xt, h, rb, n_rows, a, lin, lg2);
+    else epilogue_abs<KS, false>(xt, h, rb, n_rows, a, lin, lg2);
+    pe += (double)lin + (double)lg2 * (double)LN2;
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        a[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[l31 * XS + 2 * s + h], zb[t][s], a[t], 0, 0, 0);
-    };
-    auto g2_tile = [&](int t) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-        g0[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], a[t][r], g0[t], 0, 0, 0);
-        if (KS > 16) g1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], a[t][r], g1[t], 0, 0, 0);
-      }
-    };
-    if constexpr (ILP) {
-      // tile t's epilogue (VALU) is independent of tile t+1's GEMM1 and of tile t-1's GEMM2:
-      // issue them side by side so the vector work runs in the MFMAs' shadow
-      static_assert(CT == 2, "ILP schedule pairs two chain tiles");
-      g1_tile(0);
-      g1_tile(1);
-      epi(0);
-      g2_tile(0);
-      epi(1);
-      g2_tile(1);
-    } else {
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const float x = xt[l31 * XS + 2 * s + h];
-#pragma unroll
-        for (int t = 0; t < CT; ++t) a[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, zb[t][s], a[t], 0, 0, 0);
-      }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-      for (int t = 0; t < CT; ++t) epi(t);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float x0 = xt[rr * XS + l31];
-        const float x1 = xt[rr * XS + 32 + l31];
-#pragma unroll
-        for (int t = 0; t < CT; ++t) {
-          g0[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, a[t][r], g0[t], 0, 0, 0);
-          if (KS > 16) g1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, a[t][r], g1[t], 0, 0, 0);
-        }
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+      g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + l31], a[r], g0, 0, 0, 0);
+      if (KS > 16) g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xt[rr * XS + 32 + l31], a[r], g1, 0, 0, 0);
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    if constexpr (!WAVE) __syncthreads();
+    __builtin_amdgcn_s_setprio(0);
   };
   const int t_full = (int)min((int64_t)t1, n_rows / RL_ROWS);  // stages with all 128 rows < n_rows
   int st = t0;
   for (; st < t_full; ++st) stage(st, std::false_type{});
   for (; st < t1; ++st) stage(st, std::true_type{});
 
-  if constexpr (WAVE) __syncthreads();  // every wave is done with its slice
-  // fixed-order combination of the 4 row lanes, one chain tile at a time: waves 1-3 park
-  // their partials in LDS, wave 0 adds them to its registers in wave order
+  __syncthreads();  // every wave is done with its slice
+  // fixed-order combination of the 4 row lanes: waves 1-3 park their partials in LDS, wave 0
+  // adds them to its registers in wave order
   float* red = xs;                                                            // [RL_WAVES-1][32][64]
   double* red_pe = reinterpret_cast<double*>(xs + (RL_WAVES - 1) * 32 * 64);  // [RL_WAVES-1][64]
+  const double p = pe + __shfl_xor(pe, 32);
+  if (w > 0) {
 #pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const double p = pe[t] + __shfl_xor(pe[t], 32);
-    const int pos = (ct * CT + t) * 32 + l31;
-    if (t > 0) __syncthreads();  // the previous tile's reads are done
-    if (w > 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        red[((w - 1) * 32 + r) * 64 + lane] = g0[t][r];
-        red[((w - 1) * 32 + 16 + r) * 64 + lane] = g1[t][r];
-      }
-      red_pe[(w - 1) * 64 + lane] = p;
+    for (int r = 0; r < 16; ++r) {
+      red[((w - 1) * 32 + r) * 64 + lane] = g0[r];
+      red[((w - 1) * 32 + 16 + r) * 64 + lane] = g1[r];
     }
-    __syncthreads();
-    if (w == 0 && pos < ldc) {
+    red_pe[(w - 1) * 64 + lane] = p;
+  }
+  __syncthreads();
+  if (w == 0 && pos < ldc) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float s0 = g0[t][r], s1 = g1[t][r];
+    for (int r = 0; r < 16; ++r) {
+      float s0 = g0[r], s1 = g1[r];
 #pragma unroll
-        for (int ww = 1; ww < RL_WAVES; ++ww) {
-          s0 += red[((ww - 1) * 32 + r) * 64 + lane];
-          s1 += red[((ww - 1) * 32 + 16 + r) * 64 + lane];
-        }
-        const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
-        if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
+      for (int ww = 1; ww < RL_WAVES; ++ww) {
+        s0 += red[((ww - 1) * 32 + r) * 64 + lane];
+        s1 += red[((ww - 1) * 32 + 16 + r) * 64 + lane];
       }
-      if (h == 0) {
-        double sp = p;
+      const int d = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = s0;
+      if (d + 32 < D) gpart[((size_t)split * D + d + 32) * ldc + pos] = s1;
+    }
+    if (h == 0) {
+      double sp = p;
 #pragma unroll
-        for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[(ww - 1) * 64 + lane];
-        pepart[(size_t)split * ldc + pos] = sp;
-      }
+      for (int ww = 1; ww < RL_WAVES; ++ww) sp += red_pe[(ww - 1) * 64 + lane];
+      pepart[(size_t)split * ldc + pos] = sp;
     }
   }
 }
@@ -1378,71 +923,27 @@ int check_ev(const nmx_eval_batch* ev) {
 //      interleaved with sched_barrier at 3/2 workgroups per CU.  30-35 are bitwise equal.
 //      C=4096 all-active, f32-equivalent TFLOP/s (scripts/logreg_variant_check.py, one box):
 //      36: 180.9, 33: 178.1, 30: 175.0 (others 165-175); f32-MFMA 22: 116.5.
-// f32-MFMA forms (< 30).  The gradient is bitwise the same in all row-lane forms
-// (same MFMA sequence per chain, explicit fmas in the epilogue); 17-25 round U differently
-// (product-of-factors log, |l| sums + w.b) at ~1e-7 relative; 21 also rounds the logits
-// differently (z pre-scaled by -log2 e).
-//   22 (default) k_logreg_rowlanes_ct, 1 chain tile, wave-private LDS-DMA staging (no
-//      workgroup barrier in the row loop), peeled tail stage (124 VGPRs -> 4 waves/SIMD),
-//      s_setprio, epilogue_abs;  23 = 22 without s_setprio;  24 = 22 at >= 5 workgroups/CU
-//      (96 VGPRs, spills)
-//   19 same as 22 with workgroup-shared stages + barrier;  20 without s_setprio;  25 at 5/CU;
-//      21 = 19 on pre-scaled z
-//   17 / 18  19 with epilogue_prod, with / without s_setprio
-//   14 / 16  19 with the plain epilogue, with / without s_setprio
-//   12 / 13  two chain tiles per wave (256 / 248 VGPRs, 2 waves/SIMD), 15 = 13 with the two
-//            tiles' epilogues scheduled beside the other tile's MFMAs
-//   11 k_logreg_rowlanes (global_load_lds, 177 VGPRs, 2 waves/SIMD), 5 without s_setprio,
-//    4 double-buffered stages, 8 barrier-free wave pipeline, 0 generic tile kernel.
-// Measured at C=4096 (scripts/bench_potential.py, MI355X), TFLOP/s: 22: 117.2, 21: 117.4,
-// 19: 116.4, 23: 115.5, 25: 114.8, 20: 114.6, 24: 113.3, 17: 112.9, 14: 109.8, 16: 109.4,
-// 11: 103.5, 13: 103.0, 15: 102.9, 12: 97.0; earlier: 5: 103.0, 8: 101.6, 4: 98.2.
-// PMC (scripts/pmc_kernel.sh): MFMA pipe busy 82.5% (19) vs 72.4% (11) of SIMD cycles.
+// f32-MFMA forms: 22 = k_logreg_rowlanes (117.2 TFLOP/s all-active, 75% of the f32 peak);
+//   any other value < 30 = the generic tile kernel k_logreg_tiles (also the path for D != 55).
+//   Earlier f32 experiments (shared stages + barrier, two chain tiles per wave, 5 workgroups
+//   per CU, register-prefetch pipelines, epilogue forms) measured 97-117 TFLOP/s and were
+//   removed; the numbers are in DESIGN.md.
 int variant() {
   const char* e = getenv("NMX_LOGREG_VARIANT");
   return e ? atoi(e) : 36;
 }
 
-template <int KS, int NBUF, bool PRIO>
-void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
-                     double* pepart, hipStream_t s) {
-  const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
-  const int S = num_splits(n_rows);
-  const int Gt = ev->ldc / 32;
-  constexpr int BUF = (RL_ROWS * (2 * KS + 1) + LDS_SLACK + 255) / 256 * 256;
-  size_t lds = (size_t)NBUF * BUF * sizeof(float);
-  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
-  if (lds < red) lds = red;
-  hipLaunchKernelGGL((k_logreg_rowlanes<KS, NBUF, PRIO>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages,
-                     D, S, Gt, *ev, gpart, pepart);
-}
-
-template <int KS, int CT, bool PRIO, bool ILP = false, int EPI = 0, bool WAVE = false, int MINB = 2>
-void launch_rowlanes_ct(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart,
-                        double* pepart, hipStream_t s) {
-  const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
-  const int S = num_splits(n_rows);
-  const int Gt = ev->ldc / (32 * CT);  // ldc % 64 == 0 (check_ev)
-  constexpr int BUF = (RL_ROWS * (2 * KS + 1) + LDS_SLACK + 255) / 256 * 256;
-  constexpr int WBUF = RL_WAVES * ((32 * (2 * KS + 1) + 255) / 256 * 256);
-  size_t lds = (size_t)(WAVE ? WBUF : BUF) * sizeof(float);
-  const size_t red = (size_t)(RL_WAVES - 1) * 32 * 64 * sizeof(float) + (RL_WAVES - 1) * 64 * sizeof(double);
-  if (lds < red) lds = red;
-  hipLaunchKernelGGL((k_logreg_rowlanes_ct<KS, CT, PRIO, ILP, EPI, WAVE, MINB>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows,
-                     nstages, D, S, Gt, *ev, gpart, pepart);
-}
-
 template <int KS>
-void launch_wavepipe(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart, double* pepart,
+void launch_rowlanes(const float* Xp, int64_t n_rows, int D, const nmx_eval_batch* ev, float* gpart, double* pepart,
                      hipStream_t s) {
   const int nstages = (int)(npad_of(n_rows) / RL_ROWS);
   const int S = num_splits(n_rows);
   const int Gt = ev->ldc / 32;
-  constexpr int WBUF = (32 * (2 * KS + 1) + 3) / 4 * 4 + 64;
-  size_t lds = (size_t)RL_WAVES * WBUF * sizeof(float);
-  const size_t red = (size_t)RL_WAVES * 32 * 64 * sizeof(float) + RL_WAVES * 64 * sizeof(double);
+  constexpr int WBUF = RL_WAVES * ((32 * (2 * KS + 1) + 255) / 256 * 256);
+  size_t lds = (size_t)WBUF * sizeof(float);
+  const size_t red = (size_t)(RL_WAVES - 1) * 32 * 64 * sizeof(float) + (RL_WAVES - 1) * 64 * sizeof(double);
   if (lds < red) lds = red;
-  hipLaunchKernelGGL((k_logreg_wavepipe<KS>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages, D, S,
+  hipLaunchKernelGGL((k_logreg_rowlanes<KS>), dim3(Gt * S), dim3(RL_WAVES * 64), lds, s, Xp, n_rows, nstages, D, S,
                      Gt, *ev, gpart, pepart);
 }
 
@@ -1547,25 +1048,8 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
                        *ev, wcol, shift);
     return nmx_check_launch("k_logreg_finalize");
   }
-  const bool epi_abs = KS == 28 && var >= 19 && var <= 25;
-  if (KS == 28 && var == 4) launch_rowlanes<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
-  else if (KS == 28 && var == 5) launch_rowlanes<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 8) launch_wavepipe<28>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 11) launch_rowlanes<28, 1, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 12) launch_rowlanes_ct<28, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 13) launch_rowlanes_ct<28, 2, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 14) launch_rowlanes_ct<28, 1, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 15) launch_rowlanes_ct<28, 2, false, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 16) launch_rowlanes_ct<28, 1, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 17) launch_rowlanes_ct<28, 1, true, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 18) launch_rowlanes_ct<28, 1, false, false, 1>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 19) launch_rowlanes_ct<28, 1, true, false, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 20) launch_rowlanes_ct<28, 1, false, false, 2>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 21) launch_rowlanes_ct<28, 1, true, false, 3>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 22) launch_rowlanes_ct<28, 1, true, false, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 23) launch_rowlanes_ct<28, 1, false, false, 2, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 24) launch_rowlanes_ct<28, 1, true, false, 2, true, 5>(Xp, n_rows, dim, ev, gpart, pepart, s);
-  else if (KS == 28 && var == 25) launch_rowlanes_ct<28, 1, true, false, 2, false, 5>(Xp, n_rows, dim, ev, gpart, pepart, s);
+  const bool epi_abs = KS == 28 && var == 22;  // w.b linear term (epilogue_abs)
+  if (KS == 28 && var == 22) launch_rowlanes<28>(Xp, n_rows, dim, ev, gpart, pepart, s);  // covtype, D = 55
   else if (KS == 28) launch_tiles<28, true>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 4) launch_tiles<4, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   else if (KS <= 8) launch_tiles<8, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
