@@ -208,7 +208,12 @@ int nmx_pe_stochastic_volatility(const float* returns, int T, const nmx_eval_bat
 /* Centred funnel (examples/funnel.py:44-46): y ~ N(0,3), x ~ N(0, exp(y/2))^(dim-1);
  * z = (x[dim-1], y). */
 int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* workspace, void* stream);
-/* Workspace (per-slice partial sums) of the two kernels above for num_chains chains. */
+/* Non-centred funnel: examples/funnel.py:49 reparam(model, config={"x": LocScaleReparam(0)})
+ * (numpyro/infer/reparam.py:104-145, centered = 0): x_decentered ~ N(0,1)^(dim-1), y ~ N(0,3);
+ * z = (x_decentered[dim-1], y); the deterministic site x = exp(y/2) x_decentered is formed
+ * host side.  Replaces value_and_grad of the reparameterized potential_fn. */
+int nmx_pe_funnel_noncentered(int dim, const nmx_eval_batch* ev, void* workspace, void* stream);
+/* Workspace (per-slice partial sums) of the three kernels above for num_chains chains. */
 size_t nmx_pe_wide_workspace_bytes(int dim, int num_chains);
 
 /* Bayesian neural network (examples/bnn.py:43-74): X [N][Dx], Y [N] (D_Y = 1), H hidden

@@ -8,6 +8,8 @@
 // (SURVEY.md Appendix A, C2 and C4).
 #include <math.h>
 
+#include <algorithm>
+
 #include "nmx_api_internal.h"
 #include "nmx_common.h"
 
@@ -181,6 +183,50 @@ __global__ __launch_bounds__(64 * WAVES) void k_funnel_fin(int D, nmx_eval_batch
   ev.grad[(size_t)K * ldc + c] = y / 9.0f + 0.5f * Kf - 0.5f * e * sx;
 }
 
+// funnel, non-centred (examples/funnel.py:49, reparam(model, {"x": LocScaleReparam(0)}),
+// numpyro/infer/reparam.py:104-145): z = (x_decentered[K], y), x = exp(y/2) x_decentered is a
+// deterministic site (host side).  U = y^2/18 + log(3 sqrt(2 pi)) + sum_i [x_i^2/2 + log(2 pi)/2];
+// dU/dx_i = x_i, dU/dy = y/9.
+__global__ __launch_bounds__(64 * WAVES) void k_funnel_nc_part(int D, nmx_eval_batch ev, float* __restrict__ part) {
+  __shared__ float lds[WAVES * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + lane);
+  const bool act = c >= 0;
+  if (!__syncthreads_or(act)) return;
+  const int ldc = ev.ldc;
+  const int K = D - 1;
+  float sx[1] = {0.0f};
+  const int i0 = blockIdx.y * SLICE, i1 = min(K, i0 + SLICE);
+  if (act) {
+    for (int i = i0 + wv; i < i1; i += WAVES) {
+      const size_t idx = (size_t)i * ldc + c;
+      const float x = ev.z[idx];
+      sx[0] += x * x;
+      ev.grad[idx] = x;
+    }
+  }
+  wave_block_sum<1>(sx, lds);
+  if (act && wv == 0) part[(size_t)blockIdx.y * ldc + c] = sx[0];
+}
+
+__global__ __launch_bounds__(64 * WAVES) void k_funnel_nc_fin(int D, nmx_eval_batch ev,
+                                                            const float* __restrict__ part) {
+  __shared__ float lds[WAVES * 64];
+  const int c = nmx_eval_chain(ev, blockIdx.x * 64 + (threadIdx.x & 63));
+  if (!__syncthreads_or(c >= 0)) return;
+  const int ldc = ev.ldc;
+  const int K = D - 1;
+  float sv[1];
+  if (!slice_sums<1>(part, num_slices(K), ldc, c, sv, lds)) return;
+  const float y = ev.z[(size_t)K * ldc + c];
+  ev.pe[c] = y * y / 18.0f + 2.0175508218727822f + 0.5f * sv[0] + (float)K * 0.9189385332046727f;
+  ev.grad[(size_t)K * ldc + c] = y / 9.0f;
+}
+
+// chain-group blocks needed: positions >= num_chains hold no chain (with a compacted list,
+// num_chains bounds its count -- nmx_eval_batch)
+inline int groups_of(const nmx_eval_batch* ev) { return (std::min(ev->num_chains, ev->ldc) + 63) / 64; }
+
 int check_ev(const nmx_eval_batch* ev, const void* workspace) {
   if (!ev || !ev->z || !ev->grad || !ev->pe) return nmx_fail(NMX_ERR_INVALID, "eval batch has NULL pointers");
   if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
@@ -202,8 +248,9 @@ extern "C" int nmx_pe_stochastic_volatility(const float* returns, int T, const n
   if (!returns || T <= 1) return nmx_fail(NMX_ERR_INVALID, "stochastic_volatility: need T > 1 returns");
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
-  hipLaunchKernelGGL(k_sv_part, dim3(ev->ldc / 64, num_slices(T)), dim3(64 * WAVES), 0, s, returns, T, *ev, part);
-  hipLaunchKernelGGL(k_sv_fin, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, s, T, *ev, part);
+  const int G = groups_of(ev);
+  hipLaunchKernelGGL(k_sv_part, dim3(G, num_slices(T)), dim3(64 * WAVES), 0, s, returns, T, *ev, part);
+  hipLaunchKernelGGL(k_sv_fin, dim3(G), dim3(64 * WAVES), 0, s, T, *ev, part);
   return nmx_check_launch("k_sv");
 }
 
@@ -212,7 +259,19 @@ extern "C" int nmx_pe_funnel(int dim, const nmx_eval_batch* ev, void* workspace,
   if (dim < 2) return nmx_fail(NMX_ERR_INVALID, "funnel: dim must be >= 2");
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
-  hipLaunchKernelGGL(k_funnel_part, dim3(ev->ldc / 64, num_slices(dim - 1)), dim3(64 * WAVES), 0, s, dim, *ev, part);
-  hipLaunchKernelGGL(k_funnel_fin, dim3(ev->ldc / 64), dim3(64 * WAVES), 0, s, dim, *ev, part);
+  const int G = groups_of(ev);
+  hipLaunchKernelGGL(k_funnel_part, dim3(G, num_slices(dim - 1)), dim3(64 * WAVES), 0, s, dim, *ev, part);
+  hipLaunchKernelGGL(k_funnel_fin, dim3(G), dim3(64 * WAVES), 0, s, dim, *ev, part);
   return nmx_check_launch("k_funnel");
+}
+
+extern "C" int nmx_pe_funnel_noncentered(int dim, const nmx_eval_batch* ev, void* workspace, void* stream) {
+  if (int st = check_ev(ev, workspace)) return st;
+  if (dim < 2) return nmx_fail(NMX_ERR_INVALID, "funnel_noncentered: dim must be >= 2");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  const int G = groups_of(ev);
+  hipLaunchKernelGGL(k_funnel_nc_part, dim3(G, num_slices(dim - 1)), dim3(64 * WAVES), 0, s, dim, *ev, part);
+  hipLaunchKernelGGL(k_funnel_nc_fin, dim3(G), dim3(64 * WAVES), 0, s, dim, *ev, part);
+  return nmx_check_launch("k_funnel_nc");
 }

@@ -188,11 +188,13 @@ class MCMC:
         self._last_state = self._snapshot(eng, seed)
 
     # ------------------------------------------------------------------ results
-    def _site_arrays(self, group_by_chain):
+    def _site_arrays(self, group_by_chain, include_deterministic=True):
         eng = self._engine
         S = self._samples.shape[0]
         flat = self._samples[:, :, :eng.C].permute(2, 0, 1)  # [C, S, D]
         out = eng.potential.unflatten(flat)
+        if include_deterministic:
+            out.update(eng.potential.deterministic(out))
         if not group_by_chain:
             out = {k: v.reshape(eng.C * S, *v.shape[2:]) for k, v in out.items()}
         return out
@@ -229,11 +231,12 @@ class MCMC:
         rank's chains (moments and diagnostics by all_reduce, quantiles from the gathered
         draws) and rank 0 prints it."""
         rank, world = shard.dist_info()
+        arrays = self._site_arrays(True, include_deterministic=not exclude_deterministic)
         if world == 1:
-            sites = {k: v.detach().cpu().numpy() for k, v in self._site_arrays(True).items()}
+            sites = {k: v.detach().cpu().numpy() for k, v in arrays.items()}
             diagnostics.print_summary(sites, prob=prob)
         else:
-            stats = shard.summary(self._site_arrays(True), prob=prob)
+            stats = shard.summary(arrays, prob=prob)
             if rank == 0:
                 diagnostics.print_summary_table(stats, prob)
         ef = self.get_extra_fields()

@@ -106,6 +106,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_stochastic_volatility": (c_int, [c_vp, c_int, _evp, c_vp, c_vp]),
     "nmx_pe_funnel": (c_int, [c_int, _evp, c_vp, c_vp]),
+    "nmx_pe_funnel_noncentered": (c_int, [c_int, _evp, c_vp, c_vp]),
     "nmx_pe_wide_workspace_bytes": (c_size, [c_int, c_int]),
     "nmx_pe_bnn": (c_int, [c_vp, c_vp, c_int, c_int, c_int, _evp, c_vp, c_vp]),
     "nmx_pe_bnn_workspace_bytes": (c_size, [c_int, c_int, c_int]),

@@ -51,6 +51,10 @@ class Potential:
             self._codes = torch.tensor(codes, dtype=torch.int8, device=self.device)
         return self._codes
 
+    def deterministic(self, sites):
+        """Deterministic sites computed from the sampled ones ({} unless the model has any)."""
+        return {}
+
     def unflatten(self, flat):
         """[..., D] -> {site: [..., *shape]} (ravel_pytree order)."""
         out, o = {}, 0
@@ -186,6 +190,31 @@ class Funnel(Potential):
         return 2 * 4 * self.dim
 
 
+class FunnelNonCentered(Potential):
+    """examples/funnel.py:49, ``reparam(model, config={"x": LocScaleReparam(0)})``: the
+    decentered site x_decentered ~ N(0, 1)^(dim-1) replaces x (numpyro/infer/reparam.py:
+    104-145 with centered = 0), and x = 0 + exp(y/2) * x_decentered is a deterministic site."""
+
+    def __init__(self, dim=10):
+        self.dim = int(dim)
+        self.sites = [("x_decentered", (self.dim - 1,), REAL), ("y", (), REAL)]
+
+    def _bind(self, C, ldc, device):
+        self.workspace = torch.empty(lib().nmx_pe_wide_workspace_bytes(self.dim, C), dtype=torch.uint8,
+                                     device=device)
+
+    def evaluate(self, ev, stream):
+        check(lib().nmx_pe_funnel_noncentered(self.dim, ctypes.byref(ev), ptr(self.workspace), stream),
+              "nmx_pe_funnel_noncentered")
+
+    def deterministic(self, sites):
+        # reparam.py:140-142: value = loc + scale ** (1 - centered) * (decentered - centered * loc)
+        return {"x": torch.exp(sites["y"] / 2)[..., None] * sites["x_decentered"]}
+
+    def bytes_per_eval(self):
+        return 2 * 4 * self.dim
+
+
 class BNN(Potential):
     """examples/bnn.py:43-74: w1 [Dx,H], w2 [H,H], w3 [H,1] ~ N(0,1), prec_obs ~ Gamma(3,1),
     Y ~ N(tanh(tanh(X w1) w2) w3, 1/sqrt(prec_obs)); sites in ravel_pytree (sorted) order."""
@@ -284,6 +313,10 @@ stochastic_volatility = FusedModel(
     "examples/stochastic_volatility.py:57-65 model(returns)")
 
 funnel = FusedModel("funnel", lambda dim=10: Funnel(dim), "examples/funnel.py:44-46 model(dim)")
+
+funnel_reparam = FusedModel(
+    "funnel_reparam", lambda dim=10: FunnelNonCentered(dim),
+    'examples/funnel.py:49 reparam_model = reparam(model, config={"x": LocScaleReparam(0)})')
 
 bnn = FusedModel("bnn", lambda X, Y, D_H, D_Y=1: BNN(X, Y, D_H, D_Y), "examples/bnn.py:43-74 model(X, Y, D_H)")
 

@@ -117,6 +117,32 @@ class Funnel:
         return self.dtype(-self.log_joint(z)), g.astype(self.dtype)
 
 
+class FunnelNonCentered:
+    """examples/funnel.py:49, reparam(model, config={"x": LocScaleReparam(0)}) with
+    numpyro/infer/reparam.py:104-145 at centered = 0: x_decentered ~ N(0, 1)^(dim-1),
+    y ~ N(0, 3); deterministic x = exp(y/2) * x_decentered.  z = (x_decentered[dim-1], y)."""
+
+    def __init__(self, dim=10, dtype=np.float64):
+        self.dim = dim
+        self.K = dim - 1
+        self.dtype = dtype
+        self.sites = (("x_decentered", self.K, "real"), ("y", None, "real"))
+
+    def log_joint(self, z):
+        xd, y = z[:-1], z[-1]
+        return _lpN(y, 0.0, 3.0) + _lpN(xd, 0.0, 1.0).sum()
+
+    def pe_grad(self, z):
+        z = np.asarray(z, np.float64)
+        g = z.copy()
+        g[-1] = z[-1] / 9.0
+        return self.dtype(-self.log_joint(z)), g.astype(self.dtype)
+
+    def deterministic(self, z):
+        z = np.asarray(z, np.float64)
+        return {"x": np.exp(z[..., -1:] / 2) * z[..., :-1]}
+
+
 class StochasticVolatility:
     """examples/stochastic_volatility.py:57-65: sigma ~ Exp(50), s ~ GRW(sigma, T),
     nu ~ Exp(0.1), r ~ StudentT(nu, 0, exp(s)).  z = (log nu, s[T], log sigma)."""

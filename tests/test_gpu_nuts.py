@@ -311,6 +311,29 @@ def test_funnel_diag_runs(device):
     assert abs(y.mean()) < 1.5 and 1.5 < y.std() < 4.0  # y ~ N(0, 3) (centred funnel is hard)
 
 
+def test_funnel_reparam_non_centered(device, capsys):
+    """examples/funnel.py non-centred run: y ~ N(0, 3) and x_decentered ~ N(0, 1) are recovered
+    without divergences; the deterministic site x = exp(y/2) x_decentered comes back with the
+    samples and print_summary leaves it out unless exclude_deterministic=False."""
+    mcmc = MCMC(NUTS(P.funnel_reparam), num_warmup=300, num_samples=300, num_chains=128)
+    mcmc.run(0, 10, extra_fields=("diverging",))
+    s = {k: v.cpu().numpy() for k, v in mcmc.get_samples().items()}
+    assert set(s) == {"x", "x_decentered", "y"}
+    assert s["x"].shape == s["x_decentered"].shape == (128 * 300, 9)
+    np.testing.assert_allclose(s["x"], np.exp(s["y"] / 2)[:, None] * s["x_decentered"], rtol=1e-6)
+    assert abs(s["y"].mean()) < 0.3 and abs(s["y"].std() - 3.0) < 0.3
+    assert abs(s["x_decentered"].mean()) < 0.05 and abs(s["x_decentered"].std() - 1.0) < 0.05
+    assert int(mcmc.get_extra_fields()["diverging"].sum()) == 0
+    def row_names():
+        return {ln.split()[0] for ln in capsys.readouterr().out.splitlines() if ln.strip()}
+
+    mcmc.print_summary()
+    names = row_names()
+    assert "x_decentered[0]" in names and "y" in names and "x[0]" not in names
+    mcmc.print_summary(exclude_deterministic=False)
+    assert "x[0]" in row_names()
+
+
 @pytest.mark.parametrize("dense", [False, True])
 def test_bnn_fits_data(device, dense):
     """examples/bnn.py (small H): the posterior-mean network fits the training data and

@@ -205,6 +205,20 @@ def test_funnel_matches_oracle(device, dim):
         np.testing.assert_allclose(g[c], gr, rtol=1e-4, atol=1e-3 * max(1.0, np.abs(gr).max() * 1e-2))
 
 
+@pytest.mark.parametrize("dim", [10, 10000])
+def test_funnel_noncentered_matches_oracle(device, dim):
+    from numpyro_amd.potentials import FunnelNonCentered
+
+    rs = np.random.RandomState(dim + 1)
+    Z = rs.uniform(-2, 2, (65, dim)).astype(np.float32)
+    pe, g = _eval(FunnelNonCentered(dim), Z, device)
+    ref = OP.FunnelNonCentered(dim)
+    for c in range(65):
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c], pr, rtol=2e-5)
+        np.testing.assert_allclose(g[c], gr, rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("N,H", [(100, 69), (50, 5), (37, 16)])
 def test_bnn_matches_oracle(device, N, H):
     """examples/bnn.py model (D_X = 3, D_Y = 1) at the BASELINE width H = 69 (D = 5038) and

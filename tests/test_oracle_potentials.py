@@ -28,6 +28,7 @@ def _models():
         "logreg": (P.LogisticRegression(X, y), 5),
         "eight_schools": (P.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA), 10),
         "funnel": (P.Funnel(12), 12),
+        "funnel_noncentered": (P.FunnelNonCentered(12), 12),
         "sv": (P.StochasticVolatility(datasets.sp500_synthetic(T=40)), 42),
         "bnn": (P.BNN(Xb, Yb, H=4), 1 + 12 + 16 + 4),
     }
@@ -99,3 +100,19 @@ def test_covtype_synthetic_statistics():
     np.testing.assert_allclose(X[:, :-1].mean(0), 0, atol=1e-5)
     np.testing.assert_allclose(X[:, :-1].std(0), 1, atol=1e-4)
     assert 0.30 < y.mean() < 0.38  # 33.8% positives at full size
+
+
+def test_funnel_noncentered_matches_scipy_and_reparam():
+    """Non-centred funnel: log density = N(0,3).logpdf(y) + sum N(0,1).logpdf(x_dec), and the
+    deterministic x = exp(y/2) x_dec has the centred model's conditional N(0, exp(y/2))."""
+    rs = np.random.RandomState(3)
+    m = P.FunnelNonCentered(6)
+    for _ in range(5):
+        z = rs.randn(6) * 1.5
+        want = stats.norm(0, 3).logpdf(z[-1]) + stats.norm(0, 1).logpdf(z[:-1]).sum()
+        np.testing.assert_allclose(m.log_joint(z), want, rtol=1e-12)
+        x = m.deterministic(z)["x"]
+        np.testing.assert_allclose(x, np.exp(z[-1] / 2) * z[:-1])
+        # change of variables: the centred log density at (x, y) = non-centred - log|dx/dx_dec|
+        np.testing.assert_allclose(P.Funnel(6).log_joint(np.append(x, z[-1])),
+                                   m.log_joint(z) - 5 * z[-1] / 2, rtol=1e-10)
