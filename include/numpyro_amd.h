@@ -260,6 +260,19 @@ int nmx_gemm_chains(const float* At, int lda, int dim, const float* In, float* O
 /* Workspace for split-K (K split in a number of parts that depends on dim only; partials
  * summed in a fixed order).  0 = no split; a NULL workspace also disables it. */
 size_t nmx_gemm_chains_workspace_bytes(int dim, int ldc);
+/* The same products f32-accurate on the bf16 matrix cores (split-bf16: each f32 operand as
+ * three bf16 terms, six bf16 products per 16-deep k-step, f32 accumulation; the scheme of the
+ * covtype kernel).  A is packed once into MFMA-fragment order (Ap, nmx_gemm_x3_packed_a_bytes
+ * = 6 lda^2 bytes; At as for nmx_gemm_chains, re-pack whenever At changes); each call splits
+ * In into `split` (nmx_gemm_x3_split_bytes(lda, ldc)) and runs the product with the tiles,
+ * triangle skipping, split-K workspace (nmx_gemm_chains_workspace_bytes) and fixed-order
+ * reduction of nmx_gemm_chains.  Requires 6 lda^2 and 6 lda ldc < 2^31. */
+size_t nmx_gemm_x3_packed_a_bytes(int lda);
+int nmx_gemm_x3_pack_a(const float* At, int lda, void* Ap, void* stream);
+size_t nmx_gemm_x3_split_bytes(int lda, int ldc);
+int nmx_gemm_chains_x3(const void* Ap, int lda, int dim, const float* In, float* Out, const float* bias,
+                       int triangle, int ldc, const int32_t* phase, const int32_t* active_count, int num_chains,
+                       void* split, void* workspace, void* stream);
 /* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
  * (p < *count, device-side count, grid sized for ldo / ldi positions). */
 int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,

@@ -424,6 +424,193 @@ __global__ __launch_bounds__(256) void k_unpack(const float* __restrict__ in, in
   if (pe_in && blockIdx.x == 0 && threadIdx.x < 64) pe_out[c] = pe_in[p];
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-bf16 chain products (f32-accurate on the bf16 matrix cores; the scheme of the covtype
+// kernel, potential_logreg.hip "Split-bf16 kernel"): every f32 operand as three bf16 terms,
+// six bf16 products (a3b1 + a2b2 + a1b3 + a2b1 + a1b2 + a1b1) per 16-deep k-step into f32
+// accumulators.  A (= T or T^T, constant between adaptation windows) is packed once into
+// MFMA-fragment order (nmx_gemm_x3_pack_a); each call splits In into fragment order first
+// (k_x3_split_b, ~6 B written per f32 read), then k_gemm_x3 streams both through a 2-slot
+// LDS ring by buffer LDS-DMA.  Tiles, triangle skipping, split-K boundaries, the XCD-aware
+// order and the fixed-order reduction are those of k_gemm_chains; a column's result depends
+// only on its own data (packed == dense-batch bitwise).
+//   Ap piece ((ks * n_it + it) * 3 + p): lane (r, h) = A[32 it + r][16 ks + 8 h + j], plane p
+//   Bp piece ((ks * n_ct + ct) * 3 + p): lane (r, h) = In[16 ks + 8 h + j][32 ct + r], plane p
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h1 = (__bf16)v[j];
+    const float e1 = v[j] - (float)h1;
+    const __bf16 h2 = (__bf16)e1;
+    const float e2 = e1 - (float)h2;
+    b1[j] = h1;
+    b2[j] = h2;
+    b3[j] = (__bf16)e2;
+  }
+}
+
+// one thread per (k-step, row tile, lane): the three planes of one A fragment lane
+__global__ __launch_bounds__(256) void k_x3_pack_a(const float* __restrict__ At, int lda, bf16x8* __restrict__ Ap) {
+  const int n_it = lda / 32, n_ks = lda / 16;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n_ks * n_it * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t q = i >> 6;
+  const int it = (int)(q % n_it), ks = (int)(q / n_it);
+  const int r = lane & 31, h = lane >> 5;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = At[(size_t)(16 * ks + 8 * h + j) * lda + 32 * it + r];
+  bf16x8 b1, b2, b3;
+  split3(v, b1, b2, b3);
+  const size_t base = (size_t)q * 3 * 64 + lane;
+  Ap[base] = b1;
+  Ap[base + 64] = b2;
+  Ap[base + 128] = b3;
+}
+
+// one thread per (k-step, chain tile, lane); rows >= D read as zero
+__global__ __launch_bounds__(256) void k_x3_split_b(const float* __restrict__ In, int D, int ldc, int n_ks,
+                                                    const int32_t* __restrict__ count, bf16x8* __restrict__ Bp) {
+  const int n_ct = ldc / 32;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n_ks * n_ct * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t q = i >> 6;
+  const int ct = (int)(q % n_ct), ks = (int)(q / n_ct);
+  if (count && ct * 32 >= *count) return;  // packed columns: tiles past the count are never read
+  const int r = lane & 31, h = lane >> 5;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * ks + 8 * h + j;
+    v[j] = k < D ? In[(size_t)k * ldc + 32 * ct + r] : 0.0f;
+  }
+  bf16x8 b1, b2, b3;
+  split3(v, b1, b2, b3);
+  const size_t base = (size_t)q * 3 * 64 + lane;
+  Bp[base] = b1;
+  Bp[base + 64] = b2;
+  Bp[base + 128] = b3;
+}
+
+constexpr int X3_PIECES = 2 * (4 * 3 + 2 * 3);  // per 32-deep stage: A 2 x 12, B 2 x 6 pieces of 1 KB
+
+__global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
+                                                    const char* __restrict__ Bp, float* __restrict__ Out,
+                                                    const float* __restrict__ bias, int triangle, int ldc,
+                                                    const int32_t* __restrict__ phase,
+                                                    const int32_t* __restrict__ count, int C,
+                                                    float* __restrict__ part, int ksplit, int order, int n_rt,
+                                                    int n_ct) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];  // (the TU's one dynamic-LDS symbol)
+  char* const lds = reinterpret_cast<char*>(lds_f);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int rt_i = blockIdx.x, ct_i = blockIdx.y;
+  if (order) {
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    rt_i = (q / n_ct) * 8 + xcd;
+    ct_i = q % n_ct;
+    if (rt_i >= n_rt) return;
+  }
+  const int i0 = rt_i * TM;
+  const int c0 = ct_i * TN;
+  if (count) {
+    if (c0 >= *count) return;
+  } else {
+    const int c = c0 + lane;
+    const bool act = c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+    if (!__any(act)) return;
+  }
+  const int kt_lo = triangle == 1 ? i0 / BK : 0;
+  const int kt_hi = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
+  const int z = blockIdx.z;
+  const int kt_begin = kt_lo + (int)((int64_t)(kt_hi - kt_lo) * z / ksplit);
+  const int nk = kt_lo + (int)((int64_t)(kt_hi - kt_lo) * (z + 1) / ksplit);
+
+  const int n_it = lda / 32, n_ct32 = ldc / 32;
+  const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Ap, 0, (int)min((int64_t)lda * lda * 6, (int64_t)0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Bp, 0, (int)min((int64_t)(lda / 16) * ldc * 16 * 6, (int64_t)0x7fffffff), 0x00020000);
+  // stage kt (k-steps 2 kt, 2 kt + 1): pieces [s][12 A: row tile x plane] then [s][6 B: chain
+  // tile x plane]; wave wu DMAs pieces 9 wu .. 9 wu + 8, each at base + kt * stride (bytes)
+  constexpr int PW = X3_PIECES / 4;
+  unsigned pbase[PW], pstride[PW];
+#pragma unroll
+  for (int jj = 0; jj < PW; ++jj) {
+    const int pc = wu * PW + jj;
+    if (pc < 24) {
+      const int sb = pc / 12, e = pc % 12;
+      pbase[jj] = (unsigned)(((sb * n_it + 4 * rt_i) * 3 + e) * 1024);
+      pstride[jj] = (unsigned)(2 * n_it * 3 * 1024);
+    } else {
+      const int sb = (pc - 24) / 6, e = (pc - 24) % 6;
+      pbase[jj] = (unsigned)(((sb * n_ct32 + 2 * ct_i) * 3 + e) * 1024);
+      pstride[jj] = (unsigned)(2 * n_ct32 * 3 * 1024);
+    }
+  }
+  auto issue = [&](int kt, int buf) {
+    char* st = lds + buf * X3_PIECES * 1024;
+#pragma unroll
+    for (int jj = 0; jj < PW; ++jj) {
+      const int pc = wu * PW + jj;  // wave-uniform
+      const unsigned so = pbase[jj] + (unsigned)kt * pstride[jj];
+      if (pc < 24)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(st + pc * 1024), 16,
+                                                 lane * 16, so, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)(st + pc * 1024), 16,
+                                                 lane * 16, so, 0, 0);
+    }
+  };
+
+  f32x16 acc[2];
+#pragma unroll
+  for (int cl = 0; cl < 2; ++cl)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[cl][r] = 0.0f;
+  if (kt_begin < nk) issue(kt_begin, 0);
+  for (int kt = kt_begin; kt < nk; ++kt) {
+    const int buf = (kt - kt_begin) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");  // stage kt landed in every wave; stage kt-1 consumed
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + buf * X3_PIECES * 1024) + lane;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 a1 = fr[(s * 12 + w * 3 + 0) * 64], a2 = fr[(s * 12 + w * 3 + 1) * 64],
+                   a3 = fr[(s * 12 + w * 3 + 2) * 64];
+#pragma unroll
+      for (int cl = 0; cl < 2; ++cl) {
+        const bf16x8 b1 = fr[(24 + s * 6 + cl * 3 + 0) * 64], b2 = fr[(24 + s * 6 + cl * 3 + 1) * 64],
+                     b3 = fr[(24 + s * 6 + cl * 3 + 2) * 64];
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[cl], 0, 0, 0);
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[cl], 0, 0, 0);
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[cl], 0, 0, 0);
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc[cl], 0, 0, 0);
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc[cl], 0, 0, 0);
+        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[cl], 0, 0, 0);
+      }
+    }
+  }
+  float* const dst = ksplit > 1 ? part + (size_t)z * D * ldc : Out;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = i0 + w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (i < D) {
+      const float bi = (bias && ksplit == 1) ? bias[i] : 0.0f;
+      const int ca = c0 + l31, cb = c0 + 32 + l31;
+      if (ca < ldc) dst[(size_t)i * ldc + ca] = acc[0][r] + bi;
+      if (cb < ldc) dst[(size_t)i * ldc + cb] = acc[1][r] + bi;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count,
@@ -512,6 +699,66 @@ extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In,
     hipLaunchKernelGGL(k_gemm_reduce, dim3((D + 15) / 16, ldc / TN), dim3(256), 0, (hipStream_t)stream,
                        (const float*)workspace, ks, D, ldc, Out, bias, phase, active_count, num_chains);
   return nmx_check_launch("k_gemm_chains");
+}
+
+extern "C" size_t nmx_gemm_x3_packed_a_bytes(int lda) {
+  return lda > 0 && lda % TM == 0 ? (size_t)lda * lda * 6 : 0;
+}
+
+extern "C" int nmx_gemm_x3_pack_a(const float* At, int lda, void* Ap, void* stream) {
+  if (!At || !Ap || lda <= 0 || lda % TM) return nmx_fail(NMX_ERR_INVALID, "gemm_x3_pack_a: bad arguments");
+  const int64_t n = (int64_t)(lda / 16) * (lda / 32) * 64;
+  hipLaunchKernelGGL(k_x3_pack_a, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, At, lda,
+                     (bf16x8*)Ap);
+  return nmx_check_launch("k_x3_pack_a");
+}
+
+extern "C" size_t nmx_gemm_x3_split_bytes(int lda, int ldc) {
+  return lda > 0 && ldc > 0 ? (size_t)(lda / 16) * 16 * ldc * 6 : 0;
+}
+
+extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* In, float* Out, const float* bias,
+                                  int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
+                                  int num_chains, void* split, void* workspace, void* stream) {
+  if (!Ap || !In || !Out || !split) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: NULL operand");
+  if (D <= 0 || ldc % 64 || num_chains <= 0 || num_chains > ldc)
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: bad sizes (D=%d ldc=%d C=%d)", D, ldc, num_chains);
+  if (lda % TM || lda < nmx_dense_padded_dim(D))
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: lda must be a multiple of %d >= padded D", TM);
+  if (In == Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: In and Out must not alias");
+  if (triangle < 0 || triangle > 2) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: triangle must be 0, 1 or 2");
+  if ((int64_t)lda * lda * 6 > 0x7fffffff || (int64_t)lda * ldc * 6 > 0x7fffffff)
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: operands exceed 2 GiB (lda=%d ldc=%d)", lda, ldc);
+  hipStream_t s = (hipStream_t)stream;
+  const int n_ks = lda / 16;
+  const int64_t nb = (int64_t)n_ks * (ldc / 32) * 64;
+  hipLaunchKernelGGL(k_x3_split_b, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, In, D, ldc, n_ks,
+                     active_count, (bf16x8*)split);
+  if (int st = nmx_check_launch("k_x3_split_b")) return st;
+  // K-splits: a function of D only (never of C), at most ksplit_for(D) (the workspace size);
+  // measured at D = 10000 (profiles/r01): no split is fastest all-active (2.2 vs 2.4 ms per
+  // triangular product at C = 4096), 2 splits at C = 512 (0.33 vs 0.37)
+  static const int forced_ks = [] {
+    const char* e = getenv("NMX_GEMM_KSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  const int ks = workspace ? (forced_ks > 0 ? forced_ks : (D <= 16384 ? 1 : (D + 8191) / 8192)) : 1;
+  // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
+  // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
+  static const int forced_order = [] {
+    const char* e = getenv("NMX_GEMM_ORDER");
+    return e ? atoi(e) : -1;
+  }();
+  const int n_rt = lda / TM, n_ct = ldc / TN;
+  const int order = forced_order >= 0 ? forced_order : 1;
+  dim3 grid = order ? dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks) : dim3(n_rt, n_ct, ks);
+  hipLaunchKernelGGL(k_gemm_x3, grid, dim3(256), (size_t)2 * X3_PIECES * 1024, s, (const char*)Ap, lda, D,
+                     (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
+                     ks, order, n_rt, n_ct);
+  if (ks > 1)
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((D + 15) / 16, ldc / TN), dim3(256), 0, s, (const float*)workspace, ks,
+                       D, ldc, Out, bias, phase, active_count, num_chains);
+  return nmx_check_launch("k_gemm_x3");
 }
 
 extern "C" int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const float* neg_prec_mu, int dim,

@@ -35,6 +35,13 @@ from .potentials import REAL, Potential
 DENSE, UPPER, LOWER = 0, 1, 2  # nmx_gemm_chains `triangle` (shape of A in Out = A In)
 
 
+def _use_x3():
+    """Split-bf16 products (nmx_gemm_chains_x3, default) or f32 MFMA (NMX_GEMM_X3=0)."""
+    import os
+
+    return os.environ.get("NMX_GEMM_X3", "1") != "0"
+
+
 class Whitening:
     """z = mu + T w, T T^T = M^-1.  Holds the two padded At operands of nmx_gemm_chains."""
 
@@ -46,6 +53,12 @@ class Whitening:
         self.bwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T
         self.mu = torch.zeros(self.D, dtype=torch.float32, device=self.device)
         self._ws = {}
+        self._split = {}
+        self.x3 = _use_x3()
+        if self.x3:  # MFMA-fragment packs of T^T and T (nmx_gemm_x3_pack_a)
+            nb = lib().nmx_gemm_x3_packed_a_bytes(self.lda)
+            self.fwd_p = torch.empty(nb, dtype=torch.uint8, device=self.device)
+            self.bwd_p = torch.empty(nb, dtype=torch.uint8, device=self.device)
         self.set(torch.eye(self.D, dtype=torch.float64, device=self.device), None)
 
     def workspace(self, ldc):
@@ -54,6 +67,27 @@ class Whitening:
             nb = lib().nmx_gemm_chains_workspace_bytes(self.D, ldc)
             self._ws[ldc] = torch.empty(nb, dtype=torch.uint8, device=self.device) if nb else None
         return self._ws[ldc]
+
+    def split_buffer(self, ldc):
+        """Per-call split of the chain operand (nmx_gemm_x3_split_bytes)."""
+        if ldc not in self._split:
+            self._split[ldc] = torch.empty(lib().nmx_gemm_x3_split_bytes(self.lda, ldc), dtype=torch.uint8,
+                                           device=self.device)
+        return self._split[ldc]
+
+    def product(self, forward, x, out, bias, phase, count, num_chains, ldc, stream):
+        """Out = T In (+ bias) if forward else T^T In, on raw device pointers (x, out, bias,
+        phase, count: ints or None): the nmx_gemm_chains(_x3) call of every dense product."""
+        at, ap, tri = (self.fwd_t, getattr(self, "fwd_p", None), UPPER) if forward else \
+            (self.bwd_t, getattr(self, "bwd_p", None), LOWER)
+        ws = ptr(self.workspace(ldc))
+        if self.x3:
+            check(lib().nmx_gemm_chains_x3(ptr(ap), self.lda, self.D, x, out, bias, tri, ldc, phase, count,
+                                           int(num_chains), ptr(self.split_buffer(ldc)), ws, stream),
+                  "nmx_gemm_chains_x3")
+        else:
+            check(lib().nmx_gemm_chains(ptr(at), self.lda, self.D, x, out, bias, tri, ldc, phase, count,
+                                        int(num_chains), ws, stream), "nmx_gemm_chains")
 
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
@@ -69,6 +103,10 @@ class Whitening:
         self._tinv = None
         self.fwd_t[:self.D, :self.D] = T.t().to(torch.float32)
         self.bwd_t[:self.D, :self.D] = T.to(torch.float32)
+        if self.x3:
+            s = native.stream_ptr()
+            check(lib().nmx_gemm_x3_pack_a(ptr(self.fwd_t), self.lda, ptr(self.fwd_p), s), "nmx_gemm_x3_pack_a")
+            check(lib().nmx_gemm_x3_pack_a(ptr(self.bwd_t), self.lda, ptr(self.bwd_p), s), "nmx_gemm_x3_pack_a")
         if mu is not None:
             self.mu.copy_(torch.as_tensor(mu, dtype=torch.float32))
 
@@ -93,16 +131,12 @@ class Whitening:
     def to_model(self, w, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = mu + T w[:, c] for [D, ldc] buffers."""
         ldc = w.shape[-1]
-        check(lib().nmx_gemm_chains(ptr(self.fwd_t), self.lda, self.D, ptr(w), ptr(out), ptr(self.mu), UPPER, ldc,
-                                    ptr(phase), None, int(num_chains or ldc), ptr(self.workspace(ldc)), stream),
-              "nmx_gemm_chains")
+        self.product(True, ptr(w), ptr(out), ptr(self.mu), ptr(phase), None, num_chains or ldc, ldc, stream)
 
     def grad_to_w(self, g, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = T^T g[:, c]."""
         ldc = g.shape[-1]
-        check(lib().nmx_gemm_chains(ptr(self.bwd_t), self.lda, self.D, ptr(g), ptr(out), None, LOWER, ldc,
-                                    ptr(phase), None, int(num_chains or ldc), ptr(self.workspace(ldc)), stream),
-              "nmx_gemm_chains")
+        self.product(False, ptr(g), ptr(out), None, ptr(phase), None, num_chains or ldc, ldc, stream)
 
     def to_whitened(self, z):
         """w = T^-1 (z - mu) for z [D, n] (host-side re-expression at window ends)."""
@@ -158,21 +192,15 @@ class WhitenedPotential(Potential):
             # compacted list: the products run on packed columns of the listed chains only
             check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
                   "nmx_pack_columns")
-            ws = ptr(wt.workspace(ldc))
-            check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ptr(self.wp), ptr(self.zb), ptr(wt.mu), UPPER, ldc,
-                                    None, ev.active_count, C, ws, stream), "nmx_gemm_chains")
+            wt.product(True, ptr(self.wp), ptr(self.zb), ptr(wt.mu), None, ev.active_count, C, ldc, stream)
             self.base.evaluate(self._base_batch(ev), stream)
-            check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ptr(self.wp), None, LOWER, ldc,
-                                    None, ev.active_count, C, ws, stream), "nmx_gemm_chains")
+            wt.product(False, ptr(self.gb), ptr(self.wp), None, None, ev.active_count, C, ldc, stream)
             check(L.nmx_unpack_columns(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
                                        ptr(self.pe_p), ev.pe, stream), "nmx_unpack_columns")
             return
-        ws = ptr(wt.workspace(ldc))
-        check(L.nmx_gemm_chains(ptr(wt.fwd_t), wt.lda, D, ev.z, ptr(self.zb), ptr(wt.mu), UPPER, ldc,
-                                ev.phase, None, C, ws, stream), "nmx_gemm_chains")
+        wt.product(True, ev.z, ptr(self.zb), ptr(wt.mu), ev.phase, None, C, ldc, stream)
         self.base.evaluate(self._base_batch(ev), stream)
-        check(L.nmx_gemm_chains(ptr(wt.bwd_t), wt.lda, D, ptr(self.gb), ev.grad, None, LOWER, ldc,
-                                ev.phase, None, C, ws, stream), "nmx_gemm_chains")
+        wt.product(False, ptr(self.gb), ev.grad, None, ev.phase, None, C, ldc, stream)
 
     def flops_per_eval(self, num_chains):
         """Algorithmic FLOPs of the two triangular products (D^2 each per chain) -- the

@@ -118,6 +118,11 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_dense_padded_dim": (c_int, [c_int]),
     "nmx_gemm_chains": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
     "nmx_gemm_chains_workspace_bytes": (c_size, [c_int, c_int]),
+    "nmx_gemm_x3_packed_a_bytes": (c_size, [c_int]),
+    "nmx_gemm_x3_pack_a": (c_int, [c_vp, c_int, c_vp, c_vp]),
+    "nmx_gemm_x3_split_bytes": (c_size, [c_int, c_int]),
+    "nmx_gemm_chains_x3": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp,
+                                   c_vp]),
     "nmx_pack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_unpack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "nmx_pe_mvn": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, _evp, c_vp]),

@@ -28,7 +28,7 @@ PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def bench_gemm(D, C, reps=10, tri=0):
+def bench_gemm(D, C, reps=10, tri=0, x3=False):
     dev = torch.device("cuda:0")
     lib = native.lib()
     lda = lib.nmx_dense_padded_dim(D)
@@ -42,21 +42,32 @@ def bench_gemm(D, C, reps=10, tri=0):
     s = native.stream_ptr()
     nws = lib.nmx_gemm_chains_workspace_bytes(D, ldc)
     ws = torch.empty(nws, dtype=torch.uint8, device=dev) if nws else None
+    if x3:
+        Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=dev)
+        sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, ldc), dtype=torch.uint8, device=dev)
+        native.check(lib.nmx_gemm_x3_pack_a(native.ptr(At), lda, native.ptr(Ap), s))
+
+    def run():
+        if x3:
+            native.check(lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc,
+                                                None, None, C, native.ptr(sp), native.ptr(ws), s))
+        else:
+            native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc,
+                                             None, None, C, native.ptr(ws), s))
+
     for _ in range(2):
-        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
-                                         None, C, native.ptr(ws), s))
+        run()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
-        native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
-                                         None, C, native.ptr(ws), s))
+        run()
     b.record()
     b.synchronize()
     ms = a.elapsed_time(b) / reps
     tf = (2.0 if tri == 0 else 1.0) * D * D * C / (ms * 1e-3) / 1e12  # triangular: D^2 C useful
     ref = (At[:D, :D].t().double() @ x[:, :8].double())
     err = float((y[:, :8].double() - ref).abs().max() / ref.abs().max())
-    print(json.dumps({"kernel": "k_gemm_chains", "triangle": tri, "D": D, "C": C, "ms": round(ms, 4),
+    print(json.dumps({"kernel": "k_gemm_x3" if x3 else "k_gemm_chains", "triangle": tri, "D": D, "C": C, "ms": round(ms, 4),
                       "useful_tflops": round(tf, 2), "frac": round(tf / PEAK_F32_TFLOPS, 3), "max_rel_err": err}),
           flush=True)
 
@@ -113,6 +124,8 @@ def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None,
         peak = PEAK_F32_TFLOPS
         if name == "covtype" and 30 <= int(os.environ.get("NMX_LOGREG_VARIANT", "36")) <= 36:
             peak = 2500.0 / 6  # split-bf16 kernel: bf16 MFMA peak / 6 products (bench.py)
+        if eng.dense and os.environ.get("NMX_GEMM_X3", "1") != "0":
+            peak = 2500.0 / 6  # split-bf16 chain products (nmx_gemm_chains_x3)
         out["roofline"] = {"bound": "mfma", "achieved_tflops": round(tf, 2), "peak": round(peak, 1),
                            "frac": round(tf / peak, 3)}
     if bytes_per_leapfrog:
@@ -136,9 +149,10 @@ def main():
     if a.what == "gemm":
         D = int(a.rest[0]) if a.rest else 10000
         C = int(a.rest[1]) if len(a.rest) > 1 else 4096
-        bench_gemm(D, C)
-        bench_gemm(D, C, tri=1)
-        bench_gemm(D, C, tri=2)
+        for x3 in (False, True):
+            bench_gemm(D, C, x3=x3)
+            bench_gemm(D, C, tri=1, x3=x3)
+            bench_gemm(D, C, tri=2, x3=x3)
     elif a.what == "funnel":
         D = a.dim
         # dense: two triangular products z = T w, g = T^T g_z (D^2 FLOP each per chain)

@@ -91,6 +91,54 @@ def test_gemm_chains_matches_fp64(device, D, C, tri, split):
                                C, None, None) != 0
 
 
+@pytest.mark.parametrize("tri", [0, 1, 2])
+@pytest.mark.parametrize("D,C,split", [(3, 64, False), (55, 200, False), (300, 256, False), (1000, 70, False),
+                                       (3000, 130, True), (5038, 64, True)])
+def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
+    """Split-bf16 products (nmx_gemm_chains_x3): f32-level error against float64 -- the same
+    bound as the f32-MFMA kernel -- and inactive 64-chain tiles untouched."""
+    rs = np.random.RandomState(D + 7)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    ldc = (C + 63) // 64 * 64
+    A = rs.randn(D, D)
+    A = {0: A, 1: np.triu(A), 2: np.tril(A)}[tri]
+    At = np.zeros((lda, lda), np.float32)
+    At[:D, :D] = A.T
+    In = rs.randn(D, ldc).astype(np.float32)
+    bias = rs.randn(D).astype(np.float32)
+    phase = np.full(ldc, native.PH_DONE, np.int32)
+    act = rs.rand(C) < 0.5
+    act[64:128] = False
+    phase[:C][act] = native.PH_LEAF
+    dAt, dIn, db = (torch.from_numpy(x).to(device) for x in (At, In, bias))
+    dph = torch.from_numpy(phase).to(device)
+    out = torch.full((D, ldc), float("nan"), device=device)
+    nws = lib.nmx_gemm_chains_workspace_bytes(D, ldc)
+    ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=device) if split else None
+    Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=device)
+    sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, ldc), dtype=torch.uint8, device=device)
+    s = native.stream_ptr()
+    native.check(lib.nmx_gemm_x3_pack_a(native.ptr(dAt), lda, native.ptr(Ap), s))
+    native.check(lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(dIn), native.ptr(out), native.ptr(db),
+                                        tri, ldc, native.ptr(dph), None, C, native.ptr(sp),
+                                        native.ptr(ws) if (split and nws) else None, s))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().astype(np.float64)
+    A32 = At[:D, :D].T.astype(np.float64)
+    ref = A32 @ In.astype(np.float64) + bias[:, None]
+    bound = 2e-6 * (np.abs(A32) @ np.abs(In.astype(np.float64)) + np.abs(bias)[:, None]) + 1e-6
+    for t in range(ldc // 64):
+        cols = slice(64 * t, 64 * t + 64)
+        if bool((phase[cols] >= native.PH_LEAF).any()):
+            err = np.abs(o[:, cols] - ref[:, cols])
+            assert np.all(err <= bound[:, cols]), (err / bound[:, cols]).max()
+        else:
+            assert np.all(np.isnan(o[:, cols]))
+    assert lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(dIn), native.ptr(out), None, 0, ldc, None,
+                                  None, C, None, None, None) != 0  # no split buffer
+
+
 def _corr_cov(D, seed=0):
     rs = np.random.RandomState(seed)
     a = np.tril(0.5 * np.fliplr(np.eye(D)) + 0.1 * np.exp(rs.randn(D, D)))
