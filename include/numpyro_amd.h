@@ -171,6 +171,22 @@ int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream);
 int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
                   const int8_t* transform, void* stream);
 
+/* Persistent schedule for one-wave models (dim < 16): ONE launch runs
+ * every remaining transition of [iter_begin, iter_end) of every chain -- each thread owns a
+ * chain and alternates the model's potential (inline) with the fused step until the chain is
+ * DONE (or max_steps leapfrog steps), replacing the host loop of nmx_nuts_step / potential
+ * launches for tiny models such as README.md's eight schools (numpyro/infer/mcmc.py:461-513
+ * _single_chain_mcmc + util.py:277-407 fori_collect over hmc.py:459-530 sample_kernel).  The
+ * device code is the launched path's, so draws are bitwise identical to it.  Per-chain async
+ * only (cfg->sync_chains = 0); call nmx_nuts_resume first, read counters[0] (DONE) after.
+ *   model NMX_SMALL_DIAG_NORMAL:   p0 = mu[n], p1 = prec[n], n = dim
+ *   model NMX_SMALL_EIGHT_SCHOOLS: p0 = y[J], p1 = sigma[J], n = J = dim - 2 */
+#define NMX_SMALL_DIAG_NORMAL 1
+#define NMX_SMALL_EIGHT_SCHOOLS 2
+int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                       const int8_t* transform, int model, const float* p0, const float* p1, int n, int max_steps,
+                       void* stream);
+
 /* ======================================================================================
  * Fused potential-energy + gradient kernels.  Each replaces, for one model,
  * jax.value_and_grad(potential_fn) (numpyro/infer/hmc_util.py:242-252) over

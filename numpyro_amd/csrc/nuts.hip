@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "nmx_common.h"
+#include "nmx_small_models.h"
 
 namespace {
 
@@ -499,7 +500,7 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
 
 // End of step, wave 0: write scalars back, DONE / sync counters, compacted list.
 __device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid, int ph_in,
-                                         const ChainScalars& S, const Act& A) {
+                                         const ChainScalars& S, const Act& A, bool list = true) {
   if (valid) {
     if (S.phase != ph_in || A.leaf || A.start_iter || A.iter_done) store_scalars(a, c, S);
     if (A.fin_done) atomicAdd(&a.counters[0], 1);
@@ -511,6 +512,7 @@ __device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena
   // compacted list of chains whose next leaf is pending: the potential kernels then cost
   // in proportion to the chains still integrating.  List order is arbitrary; a chain's
   // result does not depend on its position.
+  if (!list) return;  // persistent kernel: the potential runs inline, no list
   const int lane = threadIdx.x & 63;
   const bool pend = valid && (A.start_iter || A.prep_leaf);
   const uint64_t m = __ballot(pend);
@@ -818,9 +820,10 @@ __device__ __forceinline__ void momentum_block(uint64_t seed, uint32_t gch, int 
 }
 
 // ---- fused schedule ----------------------------------------------------------------------
-template <int TPC>
-__global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
-  __shared__ float lds[TPC > 1 ? NPART * TPC * 64 : 1];
+// One fused step for the chains of this block (LIST: append the chains whose next leaf is
+// pending to the compacted list; the persistent kernel evaluates inline instead).
+template <int TPC, bool LIST>
+__device__ __forceinline__ void fused_step(const StepArgs& P, float* lds) {
   const nmx_nuts_config& cfg = P.cfg;
   const Arena& a = P.a;
   const int lane = threadIdx.x & 63;
@@ -834,7 +837,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
   const uint64_t seed = cfg.seed;
   // active list [parity ^ 1] was consumed by the previous potential launch; clear it for
   // the next step (which appends to it).  List [parity] was cleared by the previous step.
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+  if (LIST && blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
 
   ChainScalars S;
   Act A;
@@ -873,7 +876,44 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
     S.E0 = S.pe + 0.5f * ke0[0];  // build_tree :1130
     S.energy = S.E0;              // proposal energy of the initial tree (:1137)
   }
-  if (wv == 0) end_step(cfg, a, c, valid, ph_in, S, A);
+  if (wv == 0) end_step(cfg, a, c, valid, ph_in, S, A, LIST);
+}
+
+template <int TPC>
+__global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
+  __shared__ float lds[TPC > 1 ? NPART * TPC * 64 : 1];
+  fused_step<TPC, true>(P, lds);
+}
+
+// ---- persistent schedule for tiny models ----------------------------
+// One launch runs every transition of the run: each thread owns a chain and alternates the
+// model's potential (inline, per chain) with fused_step<1> until the chain is DONE, so there
+// is no host loop, no compacted list and no launch per leapfrog.  The step and the potential
+// are the device code of the launched path (k_nuts_step<1>, potential_small.hip), so the
+// draws are bitwise those of the launched schedule.  Async schedule only (no sync_chains).
+template <class Pot>
+__global__ __launch_bounds__(64) void k_nuts_persistent(StepArgs P, Pot pot, int max_steps) {
+  __shared__ float lds[1];
+  const Arena& a = P.a;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool valid = c < P.cfg.num_chains;
+  for (int it = 0; it < max_steps; ++it) {
+    const int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+    if (!__any(ph != NMX_PH_DONE)) break;  // every chain of the wave finished
+    if (ph == NMX_PH_LEAF) {
+      nmx_eval_batch ev;
+      ev.z = AV(NMX_F_Z_EVAL);
+      ev.grad = AV(NMX_F_G_EVAL);
+      ev.pe = AF(NMX_F_PE_EVAL);
+      ev.phase = nullptr;
+      ev.active_idx = nullptr;
+      ev.active_count = nullptr;
+      ev.num_chains = P.cfg.num_chains;
+      ev.ldc = P.cfg.ldc;
+      pot(ev, c);
+    }
+    fused_step<1, false>(P, lds);
+  }
 }
 
 // ---- wide schedule -----------------------------------------------------------------------
@@ -1256,6 +1296,39 @@ extern "C" int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* st
   hipLaunchKernelGGL(k_nuts_resume, dim3((cfg->ldc + 63) / 64), dim3(64), 0, (hipStream_t)stream,
                      a, *cfg);
   return nmx_check_launch("k_nuts_resume");
+}
+
+extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                                  const int8_t* transform, int model, const float* p0, const float* p1, int n,
+                                  int max_steps, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
+  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+    return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
+  if (tpc_for_dim(cfg->dim) != 1 || num_slices(cfg->dim) != 0)
+    return nmx_fail(NMX_ERR_INVALID, "run_small: dim %d is not a one-wave model (dim < 16)", cfg->dim);
+  if (cfg->sync_chains) return nmx_fail(NMX_ERR_INVALID, "run_small: the persistent schedule is per-chain async");
+  if (!p0 || !p1 || max_steps <= 0) return nmx_fail(NMX_ERR_INVALID, "run_small: bad model parameters");
+  StepArgs args;
+  args.a = arena_of(cfg, arena);
+  args.cfg = *cfg;
+  args.samples = samples;
+  args.fields = fields;
+  args.transform = transform;
+  const dim3 grid((cfg->num_chains + 63) / 64), blk(64);
+  hipStream_t s = (hipStream_t)stream;
+  if (model == NMX_SMALL_DIAG_NORMAL) {
+    if (n != cfg->dim) return nmx_fail(NMX_ERR_INVALID, "run_small: diag_normal needs n == dim");
+    hipLaunchKernelGGL(k_nuts_persistent<NmxDiagNormal>, grid, blk, 0, s, args, NmxDiagNormal{p0, p1, n}, max_steps);
+  } else if (model == NMX_SMALL_EIGHT_SCHOOLS) {
+    if (n + 2 != cfg->dim) return nmx_fail(NMX_ERR_INVALID, "run_small: eight_schools needs dim == J + 2");
+    hipLaunchKernelGGL(k_nuts_persistent<NmxEightSchools>, grid, blk, 0, s, args, NmxEightSchools{p0, p1, n},
+                       max_steps);
+  } else {
+    return nmx_fail(NMX_ERR_INVALID, "run_small: unknown model %d", model);
+  }
+  return nmx_check_launch("k_nuts_persistent");
 }
 
 extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,

@@ -340,6 +340,16 @@ class Engine:
             self._reexpress(cov, mean, s)
         return launches
 
+    def _persistent_model(self):
+        """(model id, p0, p1, n) when the run can use the one-launch persistent schedule
+        (nmx_nuts_run_small: one-wave model with an inline potential, per-chain async)."""
+        import os
+
+        if self.sync_chains or self.D >= 16 or os.environ.get("NMX_PERSISTENT", "1") == "0":
+            return None
+        fn = getattr(self.potential, "small_model", None)
+        return fn() if fn is not None else None
+
     def _run_segment(self, a, b, seed, cstart, thinning, S, samples, fields, poll_every, s, max_launches):
         """Transitions [a, b) of every chain; collection slots per (cstart, thinning, S)."""
         self._fill_cfg(a, b, self.num_warmup, seed, cstart, thinning, S)
@@ -347,6 +357,22 @@ class Engine:
         arena = ptr(self.arena)
         tr = self.potential.transform_codes()
         check(lib().nmx_nuts_resume(cfgp, arena, s), "nmx_nuts_resume")
+        small = self._persistent_model()
+        if small is not None:
+            # one launch normally covers the segment (NUTS: <= 2^depth + 2 steps per
+            # transition); HMC trajectories (ceil(L / step) leapfrogs) may need more: the
+            # kernel resumes from the arena, so relaunch until every chain is DONE
+            model, p0, p1, n = small
+            max_steps = (b - a) * ((1 << self.md) + 2) + 16
+            launches = 0
+            while True:
+                check(lib().nmx_nuts_run_small(cfgp, arena, ptr(samples), ptr(fields), ptr(tr), model, ptr(p0),
+                                               ptr(p1), n, max_steps, s), "nmx_nuts_run_small")
+                launches += 1
+                if int(self.view("counters")[0].item()) >= self.C:
+                    return launches
+                if max_launches is not None and launches * max_steps >= max_launches:
+                    raise RuntimeError(f"chains did not finish within {max_launches} leapfrog steps")
         done = self.view("counters")[0:1]
         host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         ev = torch.cuda.Event()

@@ -74,6 +74,9 @@ class NutsConfig(ctypes.Structure):
     ]
 
 
+SMALL_DIAG_NORMAL, SMALL_EIGHT_SCHOOLS = 1, 2  # nmx_nuts_run_small models
+
+
 class EvalBatch(ctypes.Structure):
     """Mirror of nmx_eval_batch."""
 
@@ -101,6 +104,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_nuts_init_from": (c_int, [_cfgp, c_vp, c_vp, c_vp]),
     "nmx_nuts_init_check": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_nuts_resume": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_nuts_run_small": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
     "nmx_nuts_step": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nmx_pe_diag_normal": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),

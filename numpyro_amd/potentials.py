@@ -94,6 +94,10 @@ class DiagNormal(Potential):
         check(lib().nmx_pe_diag_normal(ptr(self.mu), ptr(self.prec), self.dim, ctypes.byref(ev), stream),
               "nmx_pe_diag_normal")
 
+    def small_model(self):
+        """Inline potential of the persistent schedule (nmx_nuts_run_small)."""
+        return native.SMALL_DIAG_NORMAL, self.mu, self.prec, self.dim
+
 
 class EightSchools(Potential):
     """README.md:47-55: mu ~ N(0,5), tau ~ HalfCauchy(5), theta ~ N(mu, tau), y ~ N(theta, sigma)."""
@@ -112,6 +116,10 @@ class EightSchools(Potential):
     def evaluate(self, ev, stream):
         check(lib().nmx_pe_eight_schools(ptr(self.y), ptr(self.sigma), self.J, ctypes.byref(ev), stream),
               "nmx_pe_eight_schools")
+
+    def small_model(self):
+        """Inline potential of the persistent schedule (nmx_nuts_run_small)."""
+        return native.SMALL_EIGHT_SCHOOLS, self.y, self.sigma, self.J
 
 
 class LogisticRegression(Potential):

@@ -193,6 +193,27 @@ def test_num_steps_equals_potential_evaluations(device, model):
     assert evals == int(mcmc.get_extra_fields()["num_steps"].sum().item())
 
 
+@pytest.mark.parametrize("model", ["eight_schools", "diag_normal"])
+def test_persistent_schedule_is_bitwise_the_launched_one(device, model, monkeypatch):
+    """nmx_nuts_run_small (one launch for the whole run, potential inline, SURVEY.md §8f row
+    1) draws bitwise the samples and extra fields of the launched step/potential loop."""
+    if model == "eight_schools":
+        fm, args = P.eight_schools, (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    else:
+        fm, args = P.diag_normal, (np.array([1.0, -2.0, 0.5], np.float32), np.array([1.0, 0.3, 2.0], np.float32))
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NMX_PERSISTENT", mode)
+        mcmc = MCMC(NUTS(fm), num_warmup=150, num_samples=100, num_chains=70)
+        mcmc.run(5, *args, extra_fields=("num_steps", "diverging", "potential_energy", "accept_prob"))
+        out[mode] = (mcmc.get_samples(True), mcmc.get_extra_fields(True), mcmc.last_run_stats["launches"])
+    assert out["1"][2] <= 2 and out["0"][2] > 100
+    for k, v in out["0"][0].items():
+        np.testing.assert_array_equal(out["1"][0][k].cpu().numpy(), v.cpu().numpy(), err_msg=k)
+    for k, v in out["0"][1].items():
+        np.testing.assert_array_equal(out["1"][1][k].cpu().numpy(), v.cpu().numpy(), err_msg=k)
+
+
 def test_sync_and_async_schedules_are_bitwise_identical(device):
     args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
     a, _ = _run_engine(args, P.eight_schools, 64, 50, 30, 99, sync=False)
