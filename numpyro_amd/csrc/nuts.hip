@@ -27,6 +27,8 @@ namespace {
 constexpr int MAXD = NMX_MAX_TREE_DEPTH;
 constexpr int NPART = 2 * MAXD + 3;  // KE, checkpoint dots (2 per level), whole-tree dots
 constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide schedule)
+constexpr int STEP_CPW = 16;         // chains per wave of the fused step (TPC = 8, D >= 16)
+constexpr int SMALL_CPW = 16;        // chains per wave of the one-wave step (D < 16) and persistent kernel
 
 inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
 // NMX_WIDE_MIN_D overrides the threshold (A/B experiments; a function of D alone either way)
@@ -113,6 +115,26 @@ struct StepArgs {
   float* fields;
   const int8_t* transform;
 };
+
+// Fixed-order sum of N partials over the NV "virtual waves" of a block that hold the same
+// chain (virtual wave vw = wave * SUBS + sub, chain slot cl = lane % CPW; all get the total).
+// Must be reached by every thread of the block.
+template <int NV, int CPW, int N>
+__device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, int cl) {
+  if constexpr (NV > 1) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) lds[(i * NV + vw) * CPW + cl] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float s = 0.0f;
+#pragma unroll 4
+      for (int w = 0; w < NV; ++w) s += lds[(i * NV + w) * CPW + cl];
+      v[i] = s;
+    }
+    __syncthreads();
+  }
+}
 
 // Fixed-order sum of N per-thread partials over the TPC waves of a block (all waves get
 // the total).  Must be reached by every thread of the block.
@@ -821,14 +843,25 @@ __device__ __forceinline__ void momentum_block(uint64_t seed, uint32_t gch, int 
 
 // ---- fused schedule ----------------------------------------------------------------------
 // One fused step for the chains of this block (LIST: append the chains whose next leaf is
-// pending to the compacted list; the persistent kernel evaluates inline instead).
-template <int TPC, bool LIST>
-__device__ __forceinline__ void fused_step(const StepArgs& P, float* lds) {
+// pending to the compacted list; the persistent kernel evaluates inline instead).  A block
+// holds CPW chains; each of its TPC waves splits into SUBS = 64 / CPW sub-waves, so a chain's
+// coordinates spread over NV = TPC * SUBS lanes: fewer rows per lane (the vector phases are a
+// chain of dependent load -> store rounds per row) and C / CPW blocks to spread them over.
+// Every lane of a chain runs the chain's scalar logic; one lane (vw == 0) writes it back.
+// PA: StepArgs by value for the launched kernel (the kernel argument itself: a reference to it
+// made the compiler copy all of it to scratch), a reference to an LDS copy in the persistent
+// loop (by value there, the loop-invariant arguments were hoisted into registers and spilled).
+template <int TPC, int CPW, bool LIST, class PA>
+__device__ __forceinline__ void fused_step(PA P, float* lds) {
+  constexpr int SUBS = 64 / CPW;
+  constexpr int NV = TPC * SUBS;
   const nmx_nuts_config& cfg = P.cfg;
   const Arena& a = P.a;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cl = lane % CPW;
+  const int vw = wv * SUBS + lane / CPW;
+  const int c = blockIdx.x * CPW + cl;
   const int ldc = cfg.ldc;
   const int D = cfg.dim;
   const bool valid = c < cfg.num_chains;
@@ -850,14 +883,14 @@ __device__ __forceinline__ void fused_step(const StepArgs& P, float* lds) {
 #pragma unroll
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
   if (A.leaf) {
-    if (is_nuts) leaf_rows<true, 1>(v, A, seff, wv, D, TPC, c, red);
-    else leaf_rows<false, 1>(v, A, seff, wv, D, TPC, c, red);
+    if (is_nuts) leaf_rows<true, 1>(v, A, seff, vw, D, NV, c, red);
+    else leaf_rows<false, 1>(v, A, seff, vw, D, NV, c, red);
   }
-  block_sum<TPC, NPART>(red, lds);
+  vblock_sum<NV, CPW, NPART>(red, lds, vw, cl);
   leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
   tree_phase(
       cfg, S, A, [&](int i, int side) { return red[1 + 2 * i + side]; },
-      [&](int side) { return red[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, wv == 0);
+      [&](int side) { return red[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, vw == 0);
 
   float ke0[1] = {0.0f};
   const bool vec2 = A.take_leaf || A.done_sub || A.take_biased || A.hmc_accept || A.iter_done || A.start_iter ||
@@ -865,24 +898,24 @@ __device__ __forceinline__ void fused_step(const StepArgs& P, float* lds) {
   if (vec2) {
     float* const samp = A.slot >= 0 ? P.samples + (size_t)A.slot * D * ldc : nullptr;
     const float step_eff = S.step_eff;
-    for (int blk = wv; 4 * blk < D; blk += TPC) {
+    for (int blk = vw; 4 * blk < D; blk += NV) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
       ke0[0] += apply_block<false>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
     }
   }
-  block_sum<TPC, 1>(ke0, lds);
+  vblock_sum<NV, CPW, 1>(ke0, lds, vw, cl);
   if (A.start_iter) {
     S.E0 = S.pe + 0.5f * ke0[0];  // build_tree :1130
     S.energy = S.E0;              // proposal energy of the initial tree (:1137)
   }
-  if (wv == 0) end_step(cfg, a, c, valid, ph_in, S, A, LIST);
+  if (vw == 0) end_step(cfg, a, c, valid, ph_in, S, A, LIST);
 }
 
-template <int TPC>
+template <int TPC, int CPW>
 __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
-  __shared__ float lds[TPC > 1 ? NPART * TPC * 64 : 1];
-  fused_step<TPC, true>(P, lds);
+  __shared__ float lds[TPC * 64 / CPW > 1 ? NPART * TPC * 64 : 1];
+  fused_step<TPC, CPW, true, const StepArgs>(P, lds);
 }
 
 // ---- persistent schedule for tiny models ----------------------------
@@ -893,26 +926,29 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
 // draws are bitwise those of the launched schedule.  Async schedule only (no sync_chains).
 template <class Pot>
 __global__ __launch_bounds__(64) void k_nuts_persistent(StepArgs P, Pot pot, int max_steps) {
-  __shared__ float lds[1];
-  const Arena& a = P.a;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  __shared__ float lds[64 / SMALL_CPW > 1 ? NPART * 64 : 1];
+  __shared__ StepArgs sP;
+  if (threadIdx.x == 0) sP = P;
+  __syncthreads();
+  const int c = blockIdx.x * SMALL_CPW + (threadIdx.x & 63) % SMALL_CPW;
+  const bool evaluator = (threadIdx.x & 63) < SMALL_CPW;  // one lane per chain runs the potential
   const bool valid = c < P.cfg.num_chains;
+  const int* const phase = P.a.is[NMX_F_PHASE - NMX_F_PHASE];
+  nmx_eval_batch ev;
+  ev.z = P.a.v[NMX_F_Z_EVAL - NMX_F_Z];
+  ev.grad = P.a.v[NMX_F_G_EVAL - NMX_F_Z];
+  ev.pe = P.a.fs[NMX_F_PE_EVAL - NMX_F_STEP_SIZE];
+  ev.phase = nullptr;
+  ev.active_idx = nullptr;
+  ev.active_count = nullptr;
+  ev.num_chains = P.cfg.num_chains;
+  ev.ldc = P.cfg.ldc;
   for (int it = 0; it < max_steps; ++it) {
-    const int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+    const int ph = valid ? phase[c] : NMX_PH_DONE;
     if (!__any(ph != NMX_PH_DONE)) break;  // every chain of the wave finished
-    if (ph == NMX_PH_LEAF) {
-      nmx_eval_batch ev;
-      ev.z = AV(NMX_F_Z_EVAL);
-      ev.grad = AV(NMX_F_G_EVAL);
-      ev.pe = AF(NMX_F_PE_EVAL);
-      ev.phase = nullptr;
-      ev.active_idx = nullptr;
-      ev.active_count = nullptr;
-      ev.num_chains = P.cfg.num_chains;
-      ev.ldc = P.cfg.ldc;
-      pot(ev, c);
-    }
-    fused_step<1, false>(P, lds);
+    if (ph == NMX_PH_LEAF && evaluator) pot(ev, c);
+    __syncthreads();  // the evaluator lane's writes are visible to its chain's other lanes
+    fused_step<1, SMALL_CPW, false, const StepArgs&>(sP, lds);
   }
 }
 
@@ -1316,7 +1352,7 @@ extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float
   args.samples = samples;
   args.fields = fields;
   args.transform = transform;
-  const dim3 grid((cfg->num_chains + 63) / 64), blk(64);
+  const dim3 grid((cfg->num_chains + SMALL_CPW - 1) / SMALL_CPW), blk(64);
   hipStream_t s = (hipStream_t)stream;
   if (model == NMX_SMALL_DIAG_NORMAL) {
     if (n != cfg->dim) return nmx_fail(NMX_ERR_INVALID, "run_small: diag_normal needs n == dim");
@@ -1356,7 +1392,9 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
     hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
     return nmx_check_launch("k_nuts_step (wide)");
   }
-  if (tpc_for_dim(cfg->dim) == 1) hipLaunchKernelGGL(k_nuts_step<1>, dim3(grid), dim3(64), 0, s, args);
-  else hipLaunchKernelGGL(k_nuts_step<8>, dim3(grid), dim3(512), 0, s, args);
+  if (tpc_for_dim(cfg->dim) == 1)
+    hipLaunchKernelGGL((k_nuts_step<1, SMALL_CPW>), dim3(cfg->ldc / SMALL_CPW), dim3(64), 0, s, args);
+  else
+    hipLaunchKernelGGL((k_nuts_step<8, STEP_CPW>), dim3(cfg->ldc / STEP_CPW), dim3(512), 0, s, args);
   return nmx_check_launch("k_nuts_step");
 }
