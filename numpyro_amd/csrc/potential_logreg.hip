@@ -862,42 +862,57 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   x3_item<KB, DT, RING, PIPE, SCHED, L2E>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
 }
 
+// Sum of slots sp0 .. sp1-1 at stride st (in slot order; 16 loads issued ahead of their adds)
+template <class T>
+__device__ __forceinline__ T sum_slots(const T* __restrict__ p, size_t st, int sp0, int sp1) {
+  T s = 0;
+  int sp = sp0;
+  for (; sp + 16 <= sp1; sp += 16) {
+    T v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(p + (size_t)(sp + j) * st);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
+  for (; sp < sp1; ++sp) s += p[(size_t)sp * st];
+  return s;
+}
+
+// One workgroup per (64 batch positions, coordinate d or the U row d = D).  Wave w sums the
+// slots [w S / 4, (w + 1) S / 4) in order, then the four are added in wave order: a fixed
+// order that depends on S (a function of n_rows) only, and four independent load streams per
+// output, so the small launches of a NUTS tail are not one long dependent chain of loads.
 // wcol (epilogue_abs variants): U gains the per-chain linear term w . b; pe_shift removes the
 // log(2) terms of the zero rows that pad the split-bf16 tiles
-__global__ void k_logreg_finalize(const float* __restrict__ gpart, const double* __restrict__ pepart, int S,
-                                  int D, nmx_eval_batch ev, const double* __restrict__ wcol, double pe_shift) {
-  const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+constexpr int FIN_WAVES = 4;
+__global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float* __restrict__ gpart,
+                                                                    const double* __restrict__ pepart, int S, int D,
+                                                                    nmx_eval_batch ev,
+                                                                    const double* __restrict__ wcol,
+                                                                    double pe_shift) {
+  __shared__ double part[FIN_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pos = blockIdx.x * 64 + lane;
   const int d = blockIdx.y;
   const int c = nmx_eval_chain(ev, pos);
-  if (c < 0) return;
   const int ldc = ev.ldc;
+  const int sp0 = w * S / FIN_WAVES, sp1 = (w + 1) * S / FIN_WAVES;
+  if (c >= 0) {
+    if (d < D) part[w][lane] = sum_slots(gpart + (size_t)d * ldc + pos, (size_t)D * ldc, sp0, sp1);
+    else part[w][lane] = sum_slots(pepart + pos, (size_t)ldc, sp0, sp1);
+  }
+  __syncthreads();
+  if (w != 0 || c < 0) return;
   if (d < D) {
-    // slabs summed in split order; 16 loads issued ahead of their adds
-    const float* gp = gpart + (size_t)d * ldc + pos;
-    const size_t st = (size_t)D * ldc;
     float s = 0.0f;
-    int sp = 0;
-    for (; sp + 16 <= S; sp += 16) {
-      float v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(gp + (size_t)(sp + j) * st);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) s += v[j];
-    }
-    for (; sp < S; ++sp) s += gp[(size_t)sp * st];
+    for (int i = 0; i < FIN_WAVES; ++i) s += (float)part[i][lane];
     const size_t idx = (size_t)d * ldc + c;
     ev.grad[idx] = s + ev.z[idx];
   } else {
     double s = 0.0;
-    int sp = 0;
-    for (; sp + 16 <= S; sp += 16) {
-      double v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = pepart[(size_t)(sp + j) * ldc + pos];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) s += v[j];
-    }
-    for (; sp < S; ++sp) s += pepart[(size_t)sp * ldc + pos];
+    for (int i = 0; i < FIN_WAVES; ++i) s += part[i][lane];
     double zz = 0.0, wz = 0.0;
     for (int k = 0; k < D; ++k) {
       const double z = ev.z[(size_t)k * ldc + c];
@@ -1044,7 +1059,7 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
     if (int st = nmx_check_launch("k_logreg_x3")) return st;
     const double* wcol = (const double*)((const char*)packed + colterm_offset(n_rows, dim));
     const double shift = -(double)(nt * X3_ROWS - n_rows) * 0.6931471805599453;
-    hipLaunchKernelGGL(k_logreg_finalize, dim3((nb + 63) / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S2, dim,
+    hipLaunchKernelGGL(k_logreg_finalize, dim3((nb + 63) / 64, dim + 1), dim3(64 * FIN_WAVES), 0, s, gpart, pepart, S2, dim,
                        *ev, wcol, shift);
     return nmx_check_launch("k_logreg_finalize");
   }
@@ -1057,7 +1072,7 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   else launch_tiles<32, false>(Xp, n_rows, dim, ev, gpart, pepart, s);
   if (int st = nmx_check_launch("k_logreg_tiles")) return st;
   const double* wcol = epi_abs ? (const double*)((const char*)packed + colterm_offset(n_rows, dim)) : nullptr;
-  hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64), 0, s, gpart, pepart, S, dim, *ev,
+  hipLaunchKernelGGL(k_logreg_finalize, dim3(ev->ldc / 64, dim + 1), dim3(64 * FIN_WAVES), 0, s, gpart, pepart, S, dim, *ev,
                      wcol, 0.0);
   return nmx_check_launch("k_logreg_finalize");
 }
