@@ -30,7 +30,14 @@ constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide
 constexpr int STEP_CPW = 16;         // chains per wave of the fused step (TPC = 8, D >= 16)
 constexpr int SMALL_CPW = 16;        // chains per wave of the one-wave step (D < 16) and persistent kernel
 
-inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
+inline int slice_width(int D) {
+  static const int env = [] {  // NMX_WIDE_SW: A/B experiments (a multiple of 4; fixed per process)
+    const char* e = getenv("NMX_WIDE_SW");
+    return e ? (atoi(e) + 3) / 4 * 4 : 0;
+  }();
+  if (env > 0) return env;
+  return D >= 4096 ? 64 : 32;
+}
 // NMX_WIDE_MIN_D overrides the threshold (A/B experiments; a function of D alone either way)
 inline int wide_min_d() {
   static const int v = [] {
@@ -975,19 +982,29 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   const int s = blockIdx.y;
   const int ldc = cfg.ldc, D = cfg.dim;
   const bool valid = c < cfg.num_chains;
-  const int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  // every per-chain scalar in one round of loads, ahead of the early exit (a block has only
+  // a few rows per wave: a second dependent round was a large share of its time)
+  int ph = NMX_PH_DONE, dir = 0, subn = 0, depth = 0;
+  float seff0 = 0.0f;
+  if (valid) {
+    ph = AI(NMX_F_PHASE)[c];
+    dir = AI(NMX_F_DIR)[c];
+    subn = AI(NMX_F_SUB_N)[c];
+    depth = AI(NMX_F_DEPTH)[c];
+    seff0 = AF(NMX_F_STEP_EFF)[c];
+  }
   if (!__syncthreads_or(ph == NMX_PH_LEAF)) return;
   const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
   Act A{};
   A.leaf = ph == NMX_PH_LEAF;
-  A.dirR = A.leaf ? AI(NMX_F_DIR)[c] : 0;
-  A.k = (A.leaf && is_nuts) ? AI(NMX_F_SUB_N)[c] : 0;
-  A.j = (A.leaf && is_nuts) ? AI(NMX_F_DEPTH)[c] : 0;
+  A.dirR = A.leaf ? dir : 0;
+  A.k = (A.leaf && is_nuts) ? subn : 0;
+  A.j = (A.leaf && is_nuts) ? depth : 0;
   A.imin = 1;
   A.imax = 0;
   if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);
   A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
-  const float seff = A.leaf ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
+  const float seff = A.leaf ? seff0 : 0.0f;
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   float red[NPART];
 #pragma unroll
@@ -1104,7 +1121,16 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   const int s = blockIdx.y;
   const int ldc = cfg.ldc, D = cfg.dim;
   const bool valid = c < cfg.num_chains;
-  const int act = valid ? AI(NMX_F_ACTION)[c] : 0;
+  // all per-chain scalars in one round of loads, ahead of the early exit (as in V1)
+  int act = 0, slot = -1, wfn = 0, it = 0;
+  float step_eff = 0.0f;
+  if (valid) {
+    act = AI(NMX_F_ACTION)[c];
+    slot = AI(NMX_F_SLOT)[c];
+    wfn = AI(NMX_F_ACT_WFN)[c];
+    step_eff = AF(NMX_F_STEP_EFF)[c];
+    it = AI(NMX_F_ITER)[c];
+  }
   constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_START |
                       ACT_PREP;
   if (!__syncthreads_or((act & VEC) != 0)) return;
@@ -1120,10 +1146,8 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   A.prep_leaf = act & ACT_PREP;
   A.dirR = (act & ACT_DIRR) ? 1 : 0;
   A.new_dir = (act & ACT_NEWDIR) ? 1 : 0;
-  A.slot = valid ? AI(NMX_F_SLOT)[c] : -1;
-  A.wfn = valid ? AI(NMX_F_ACT_WFN)[c] : 0;
-  const float step_eff = valid ? AF(NMX_F_STEP_EFF)[c] : 0.0f;
-  const int it = valid ? AI(NMX_F_ITER)[c] : 0;
+  A.slot = slot;
+  A.wfn = wfn;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   float* const samp = (A.iter_done && A.slot >= 0) ? W.p.samples + (size_t)A.slot * D * ldc : nullptr;
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
