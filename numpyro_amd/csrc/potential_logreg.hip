@@ -730,13 +730,13 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
 #pragma unroll
           for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
           float lin = 0.0f, prod = 1.0f;
-          auto epi1 = [&](int r) {
+          auto epi1 = [&](int r) {  // x3_epilogue<L2E>'s row r
             const float l = acc[r];
             const float al = fabsf(l);
-            const float e = __builtin_amdgcn_exp2f(-al * LOG2E);
+            const float e = __builtin_amdgcn_exp2f(L2E ? -al : -al * LOG2E);
             const float ope = 1.0f + e;
             const float inv = __builtin_amdgcn_rcpf(ope);
-            const float num = l >= 0.0f ? 1.0f : e;
+            const float num = (L2E ? l <= 0.0f : l >= 0.0f) ? 1.0f : e;
             res[r] = __builtin_fmaf(num, inv, -y4[r >> 2][r & 3]);
             lin += al;
             prod *= ope;
@@ -772,7 +772,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
               a3 = n3;
             }
           }
-          pe += (double)(0.5f * lin) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+          pe += (double)(0.5f * lin) * (L2E ? (double)LN2 : 1.0) + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
         } else {
           nxt = x3_gemm1<KB>(fa, z1, z2, z3);
           x3_epilogue<L2E>(acc, y4, res, pe);
@@ -923,6 +923,16 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
   }
 }
 
+// Launches over at most this many 128-chain tiles run the hand-interleaved form of the
+// default kernel (NMX_X3_TAIL_GT: A/B override, 0 disables).
+int x3_tail_tiles() {
+  static const int v = [] {
+    const char* e = getenv("NMX_X3_TAIL_GT");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 int check_ev(const nmx_eval_batch* ev) {
   if (!ev || !ev->z || !ev->grad || !ev->pe) return nmx_fail(NMX_ERR_INVALID, "eval batch has NULL pointers");
   if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
@@ -1051,7 +1061,13 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   else if (var == 34) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
   else if (var == 35) hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 2, true, 6>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart); \
   else hipLaunchKernelGGL((k_logreg_x3<kb, dt, 4, 3, true, 0, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart, pepart);
-    if (KB == 4) { NMX_X3(4, 2) }
+    if (KB == 4 && var == 36 && Gt <= x3_tail_tiles()) {
+      // few chain tiles (one or two workgroups per CU, one wave per SIMD): GEMM1(k+1)'s
+      // MFMAs hand-interleaved with tile k's epilogue rows -- the same arithmetic in the same
+      // order as the default (bitwise equal), no other wave on the SIMD to fill the gaps
+      hipLaunchKernelGGL((k_logreg_x3<4, 2, 4, 2, true, 6, true>), grid, blk, lds, s, Xq, nt, dim, S2, Gt, *ev, gpart,
+                         pepart);
+    } else if (KB == 4) { NMX_X3(4, 2) }
     else if (KB == 3) { NMX_X3(3, 2) }
     else if (KB == 2) { NMX_X3(2, 1) }
     else { NMX_X3(1, 1) }
