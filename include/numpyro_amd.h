@@ -301,6 +301,24 @@ int nmx_unpack_columns(const float* in, int ldi, int dim, const int32_t* list, c
 int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const float* neg_prec_mu, int dim,
                const nmx_eval_batch* ev, void* stream);
 
+/* ---- posterior predictive (numpyro/infer/util.py:888-1090 Predictive, :803-885
+ *      _predictive: the model re-run with the latent sites substituted from each posterior
+ *      sample, observed sites sampled).  Samples are constrained values, [num_samples][...]
+ *      row-major; draws are Philox-keyed by (seed, sample, element). ---- */
+/* examples/covtype.py:66-71: obs ~ Bernoulli(logits = X @ coefs); X [n_rows][dim] f32,
+ * coefs [num_samples][dim], out [num_samples][n_rows] int32 0/1. */
+int nmx_predict_logreg(const float* X, int64_t n_rows, int dim, const float* coefs, int num_samples,
+                       uint64_t seed, int32_t* out, void* stream);
+/* README.md:47-55 eight schools: obs ~ Normal(loc, scale); loc [num_samples][n] (theta),
+ * scale [n] (sigma), out [num_samples][n]. */
+int nmx_predict_normal(const float* loc, const float* scale, int n, int num_samples, uint64_t seed,
+                       float* out, void* stream);
+/* examples/bnn.py:43-74: Y ~ Normal(tanh(tanh(X w1) w2) w3, 1/sqrt(prec_obs)); X [n][dx];
+ * samples [num_samples][1 + dx*dh + dh*dh + dh*dy] (prec_obs, w1, w2, w3: sorted sites);
+ * out [num_samples][n][dy]. */
+int nmx_predict_bnn(const float* X, int n, int dx, int dh, int dy, const float* samples, int num_samples,
+                    uint64_t seed, float* out, void* stream);
+
 /* ---- self tests (no reference counterpart; used by tests and smoke()) ---- */
 /* Philox4x32-10 on device: ctr_key is n x {c0,c1,c2,c3,k0,k1}, out is n x 4 words. */
 int nmx_selftest_philox(const uint32_t* ctr_key, uint32_t* out, int n, void* stream);

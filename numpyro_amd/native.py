@@ -105,6 +105,9 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_nuts_init_check": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_nuts_resume": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_nuts_run_small": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
+    "nmx_predict_logreg": (c_int, [c_vp, ctypes.c_int64, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),
+    "nmx_predict_normal": (c_int, [c_vp, c_vp, c_int, c_int, ctypes.c_uint64, c_vp, c_vp]),
+    "nmx_predict_bnn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_nuts_step": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nmx_pe_diag_normal": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),

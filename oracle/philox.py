@@ -27,6 +27,7 @@ EV_BIASED = 3
 EV_LEAF = 4
 EV_INIT = 5
 EV_ACCEPT = 6
+EV_PREDICT = 7
 
 
 def philox4x32_10(ctr, key):
