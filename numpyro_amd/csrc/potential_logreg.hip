@@ -862,17 +862,17 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   x3_item<KB, DT, RING, PIPE, SCHED, L2E>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
 }
 
-// Sum of slots sp0 .. sp1-1 at stride st (in slot order; 16 loads issued ahead of their adds)
+// Sum of slots sp0 .. sp1-1 at stride st (in slot order; 32 loads issued ahead of their adds)
 template <class T>
 __device__ __forceinline__ T sum_slots(const T* __restrict__ p, size_t st, int sp0, int sp1) {
   T s = 0;
   int sp = sp0;
-  for (; sp + 16 <= sp1; sp += 16) {
-    T v[16];
+  for (; sp + 32 <= sp1; sp += 32) {
+    T v[32];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(p + (size_t)(sp + j) * st);
+    for (int j = 0; j < 32; ++j) v[j] = __builtin_nontemporal_load(p + (size_t)(sp + j) * st);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s += v[j];
+    for (int j = 0; j < 32; ++j) s += v[j];
   }
   for (; sp < sp1; ++sp) s += p[(size_t)sp * st];
   return s;
@@ -913,11 +913,18 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < FIN_WAVES; ++i) s += part[i][lane];
+    // every z load in flight at once (D <= 64), then the sums in coordinate order
+    float zf[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) zf[k] = k < D ? ev.z[(size_t)k * ldc + c] : 0.0f;
     double zz = 0.0, wz = 0.0;
-    for (int k = 0; k < D; ++k) {
-      const double z = ev.z[(size_t)k * ldc + c];
-      zz += z * z;
-      if (wcol) wz += wcol[k] * z;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      if (k < D) {
+        const double z = zf[k];
+        zz += z * z;
+        if (wcol) wz += wcol[k] * z;
+      }
     }
     ev.pe[c] = (float)(s + pe_shift + wz + 0.5 * zz + 0.9189385332046727 * D);
   }
