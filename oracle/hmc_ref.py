@@ -12,6 +12,11 @@ Differences from the reference that are deliberate and shared with the engine:
   * potentials are (pe, grad) callables with hand-derived gradients instead of
     jax.value_and_grad (hmc_util.py:242-252), see oracle/potentials.py.
 Arithmetic is done in `dtype` (float32 by default = the reference's x64-off mode).
+
+Decision margins: when `DECISIONS` is a list, every discrete decision of a trajectory
+(transition draws u < p, U-turn angle signs, divergence threshold, HMC accept) appends
+(kind, margin) with a scale-free margin, so a parity test can show that a chain whose path
+left the oracle's did so at a rounding-level tie (tests/test_gpu_nuts.py).
 """
 from __future__ import annotations
 
@@ -21,6 +26,14 @@ from collections import namedtuple
 import numpy as np
 
 from . import philox
+
+DECISIONS = None  # list -> record (kind, margin) of every discrete decision
+
+
+def _log(kind, margin):
+    if DECISIONS is not None:
+        DECISIONS.append((kind, float(margin)))
+
 
 AdaptWindow = namedtuple("AdaptWindow", ["start", "end"])  # hmc_util.py:16
 IntegratorState = namedtuple("IntegratorState", ["z", "r", "potential_energy", "z_grad"])  # :31-33
@@ -297,6 +310,12 @@ def _momentum_angle(inverse_mass_matrix, r_left, r_right, r_sum):
 def _is_turning(inverse_mass_matrix, r_left, r_right, r_sum):
     """hmc_util.py:740-746."""
     left_angle, right_angle = _momentum_angle(inverse_mass_matrix, r_left, r_right, r_sum)
+    if DECISIONS is not None:  # angle relative to the magnitude of its terms
+        v_l = kinetic_grad(inverse_mass_matrix, r_left)
+        v_r = kinetic_grad(inverse_mass_matrix, r_right)
+        rs = np.abs(r_sum - (r_left + r_right) / r_sum.dtype.type(2))
+        _log("turn", min(abs(left_angle) / max(np.dot(np.abs(v_l), rs), 1e-30),
+                         abs(right_angle) / max(np.dot(np.abs(v_r), rs), 1e-30)))
     return bool((left_angle <= 0) | (right_angle <= 0))
 
 
@@ -355,6 +374,8 @@ def _build_basetree(vv_update, kinetic_fn, z, r, z_grad, inverse_mass_matrix, st
         delta_energy = type(delta_energy)(np.inf)
     tree_weight = -delta_energy
     diverging = bool(delta_energy > max_delta_energy)
+    if np.isfinite(delta_energy):
+        _log("diverge", abs(delta_energy - max_delta_energy) / max_delta_energy)
     with np.errstate(over="ignore"):
         accept_prob = min(np.exp(-delta_energy), type(delta_energy)(1.0))
     return TreeInfo(z_new, r_new, z_new_grad, z_new, r_new, z_new_grad, z_new, pe_new, z_new_grad,
@@ -387,6 +408,8 @@ def _combine_tree(current_tree, new_tree, inverse_mass_matrix, going_right, u, b
             transition_prob = dt(1.0) / (dt(1.0) + np.exp(-(new_tree.weight - current_tree.weight)))
         turning = current_tree.turning
     transition = bool(u < transition_prob)
+    if 0.0 < transition_prob < 1.0:
+        _log("transition", abs(u - transition_prob))
     src = new_tree if transition else current_tree
     tree_weight = _logaddexp(current_tree.weight, new_tree.weight)
     return TreeInfo(z_left, r_left, z_left_grad, z_right, r_right, z_right_grad,
@@ -557,6 +580,8 @@ class NUTSOracle:
             accept_prob = min(np.exp(-delta_energy), f(1.0))
         diverging = delta_energy > self.max_delta_energy
         u = philox.uniform(seed, chain, it, philox.EV_ACCEPT, 0, 0)
+        if accept_prob < 1.0:
+            _log("accept", abs(u - accept_prob))
         if u < accept_prob:
             return vv_state_new, energy_new, num_steps, accept_prob, diverging
         return vv_state, energy_old, num_steps, accept_prob, diverging
