@@ -93,10 +93,12 @@ def test_gemm_chains_matches_fp64(device, D, C, tri, split):
 
 @pytest.mark.parametrize("tri", [0, 1, 2])
 @pytest.mark.parametrize("D,C,split", [(3, 64, False), (55, 200, False), (300, 256, False), (1000, 70, False),
-                                       (3000, 130, True), (5038, 64, True)])
+                                       (3000, 130, True), (5038, 64, True), (10000, 256, False)])
 def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
     """Split-bf16 products (nmx_gemm_chains_x3): f32-level error against float64 -- the same
-    bound as the f32-MFMA kernel -- and inactive 64-chain tiles untouched."""
+    bound as the f32-MFMA kernel -- and inactive 64-chain tiles untouched.  D = 10000 is
+    BASELINE config 2 (funnel-10k dense mass) on the default path: no split-K workspace (the
+    x3 kernel splits K only above D = 16384), XCD-aware block order."""
     rs = np.random.RandomState(D + 7)
     lib = native.lib()
     lda = lib.nmx_dense_padded_dim(D)
@@ -125,9 +127,11 @@ def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
                                         native.ptr(ws) if (split and nws) else None, s))
     torch.cuda.synchronize()
     o = out.cpu().numpy().astype(np.float64)
-    A32 = At[:D, :D].T.astype(np.float64)
-    ref = A32 @ In.astype(np.float64) + bias[:, None]
-    bound = 2e-6 * (np.abs(A32) @ np.abs(In.astype(np.float64)) + np.abs(bias)[:, None]) + 1e-6
+    # float64 reference (on the device for the large case: 2.6e10 multiply-adds)
+    A64 = dAt[:D, :D].t().to(torch.float64)
+    In64 = dIn.to(torch.float64)
+    ref = (A64 @ In64 + db.to(torch.float64)[:, None]).cpu().numpy()
+    bound = (2e-6 * (A64.abs() @ In64.abs() + db.to(torch.float64).abs()[:, None]) + 1e-6).cpu().numpy()
     for t in range(ldc // 64):
         cols = slice(64 * t, 64 * t + 64)
         if bool((phase[cols] >= native.PH_LEAF).any()):
@@ -401,3 +405,39 @@ def test_gemm_chains_variants_bitwise(device, variant, tmp_path):
         res[v] = np.load(path)
     for k in res["2"].files:
         np.testing.assert_array_equal(res[variant][k], res["2"][k], err_msg=k)
+
+
+def test_funnel_10k_dense_nuts_runs(device):
+    """BASELINE config 2 shape (examples/funnel.py at dim 10000, dense mass) end to end at
+    reduced chains and iterations: W = 20 (windows [0-2], [3-17], [18-19]: one pooled
+    dense-mass update and re-expression at D = 10000), S = 2.  Every leaf consumes exactly
+    one potential evaluation (the whitened potential's listed-chain count) and the draws are
+    finite."""
+    C = 256
+    mcmc = MCMC(NUTS(P.funnel, dense_mass=True, max_tree_depth=8), num_warmup=20, num_samples=2,
+                num_chains=C)
+    mcmc.warmup(0, 10000)
+    eng = mcmc._engine
+    assert eng.D == 10000 and eng.dense
+    cnt = eng.view("counters")
+    logged = torch.zeros(200000, dtype=torch.int32, device=eng.device)
+    n = [0]
+    orig = eng.potential.evaluate
+
+    def counting(ev, s):
+        p = 0 if ev is eng.eval_lists[0] else 1
+        logged[n[0]] = cnt[2 + p]
+        n[0] += 1
+        orig(ev, s)
+
+    eng.potential.evaluate = counting
+    mcmc.run(1, 10000, extra_fields=("num_steps", "diverging"))
+    eng.potential.evaluate = orig
+    ef = mcmc.get_extra_fields()
+    assert int(logged[:n[0]].sum().item()) == int(ef["num_steps"].sum().item())
+    s = mcmc.get_samples()
+    assert s["x"].shape == (C * 2, 9999) and s["y"].shape == (C * 2,)
+    assert torch.isfinite(s["x"]).all() and torch.isfinite(s["y"]).all()
+    imm = mcmc.post_warmup_state.adapt_state.inverse_mass_matrix
+    assert imm.shape == (10000, 10000) and torch.isfinite(imm).all()
+    assert not torch.equal(imm.cpu(), torch.eye(10000, dtype=imm.dtype))  # the window update happened
