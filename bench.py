@@ -1,12 +1,13 @@
 """Benchmark: NUTS leapfrog steps/s over vectorized chains of the covtype logistic
 regression (BASELINE.json metric), one process per GPU.
 
-A "step" is one MCMC transition of every chain (one NUTS tree each).  Protocol
-(notebooks/source/logistic_regression.ipynb:202-210, NUTS cell: num_warmup=50,
-num_samples=50 -- the defaults here): `--warmup` adaptation transitions
-untimed (mcmc.warmup), then exactly `--steps` sampling transitions timed (mcmc.run),
-bracketed by barrier + synchronize on every rank; value = sum(num_steps) over all chains
-and ranks / max-over-ranks wall time (useful leapfrogs, inputs resident in HBM).
+A "step" is one MCMC transition of every chain (one NUTS tree each).  Protocol (SURVEY.md
+§8d): `--adapt` warmup/adaptation transitions (mcmc.warmup: dual averaging + diagonal mass,
+default 200, untimed setup like data loading), then `--warmup` untimed sampling transitions,
+then exactly `--steps` sampling transitions timed (mcmc.run), bracketed by barrier +
+synchronize on every rank; value = sum(num_steps) over all chains and ranks / max-over-ranks
+wall time (useful leapfrogs, inputs resident in HBM).  Timing adapted chains matters: with
+the step size still at its initial value most trees are one divergent leaf.
 
 Launch for N GPUs:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -33,50 +34,68 @@ SPLIT_PRODUCTS = 6
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # the reference's NUTS timing protocol: num_warmup=50, num_samples=50
-    # (notebooks/source/logistic_regression.ipynb cell 12)
-    p.add_argument("--steps", type=int, default=50, help="timed sampling transitions")
-    p.add_argument("--warmup", type=int, default=50, help="untimed warmup/adaptation transitions")
+    p.add_argument("--steps", type=int, default=100, help="timed sampling transitions")
+    p.add_argument("--warmup", type=int, default=5, help="untimed sampling transitions after adaptation")
+    p.add_argument("--adapt", type=int, default=200, help="untimed adaptation (warmup) transitions")
     p.add_argument("--chains", type=int, default=4096, help="total chains over all GPUs")
     p.add_argument("--rows", type=int, default=581012)
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
+    p.add_argument("--cpu-chains", type=int, default=64, help="chains of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return p.parse_args()
 
 
-def cpu_baseline(X, y, seconds, seed=0):
-    """The oracle's per-chain NUTS (NumPy restatement of numpyro's sample kernel, float32)
-    on the full covtype data, for a bounded number of leapfrogs; returns leapfrogs/s."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds):
+    """Reduced-chain CPU comparator (SURVEY.md §8d CPU side 2): `chains` chains of the oracle's
+    NUTS (oracle/hmc_ref.py, float32) started from the GPU's adapted state of the first chains
+    (z, U, grad, step size, diagonal mass) and the same Philox stream, so they run the timed
+    workload's trees; their potential calls are batched into the OpenMP C restatement of the
+    covtype potential (oracle/c/logreg_batch.c, one X pass per batch: GEMM form).  Runs whole
+    transitions until `seconds` have elapsed; returns leapfrogs/s."""
     import numpy as np
 
+    from oracle import cpu_batched as CB
     from oracle import hmc_ref as H
-    from oracle import philox
-    from oracle import potentials as OP
 
-    pot = OP.LogisticRegression(X, y, dtype=np.float32)
-    count = [0]
-
-    def pe_grad(z):
-        count[0] += 1
-        return pot.pe_grad(z)
-
-    o = H.NUTSOracle(pe_grad, X.shape[1], 1000, max_tree_depth=10)
+    f = CB.LogRegBatch(X, y)
+    D = X.shape[1]
+    cols = lambda t: t[:chains].detach().cpu().numpy()  # noqa: E731
+    z, g, pe = cols(state.z["coefs"]), cols(state.z_grad), cols(state.potential_energy)
+    ss, imm = cols(state.adapt_state.step_size), cols(state.adapt_state.inverse_mass_matrix)
+    oracles, states = [], []
+    for c in range(chains):
+        o = H.NUTSOracle(None, D, num_warmup, step_size=float(ss[c]), inverse_mass_matrix=imm[c])
+        wa = o.wa_init((z[c],), None, np.float32(ss[c]), inverse_mass_matrix=imm[c], mass_matrix_size=D)
+        oracles.append(o)
+        states.append(H.HMCState(it0, z[c].astype(np.float32), g[c].astype(np.float32), np.float32(pe[c]), None,
+                                 None, None, 0, np.float32(0), np.float32(0), False, wa, (seed, c)))
     t0 = time.perf_counter()
-    st = o.init(philox.init_uniform(seed, 0, 0, X.shape[1]), seed, 0)
-    count[0] = 0
-    t0 = time.perf_counter()
-    leap = 0
+    leap, trans = 0, 0
     while time.perf_counter() - t0 < seconds:
-        st = o.sample(st)
-        leap = count[0]
+        states, _, evals, _ = CB.run_chains(f, states, oracles, 1)
+        leap += evals
+        trans += 1
     dt = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": leap / dt, "unit": "leapfrog/s", "cores": threads, "kind": "port",
-            "sample": f"1 chain, full covtype {X.shape[0]}x{X.shape[1]} f32, NumPy oracle NUTS "
-                      f"(oracle/hmc_ref.py), {leap} leapfrogs in {dt:.1f}s, BLAS threads={threads}"}
+    return {"value": leap / dt, "unit": "leapfrog/s", "cores": f.threads(), "kind": "port",
+            "sample": f"reduced C={chains}: {chains} chains of the timed workload (GPU-adapted state, same "
+                      f"stream), {trans} transitions = {leap} leapfrogs in {dt:.1f}s; NumPy oracle NUTS "
+                      f"(oracle/hmc_ref.py) with the potential batched over chains into the OpenMP C "
+                      f"restatement (oracle/c/logreg_batch.c, full {X.shape[0]}x{D} f32 data)",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
 
 
 def main():
@@ -96,17 +115,23 @@ def main():
     from numpyro_amd import datasets
     from numpyro_amd import potentials as P
     from numpyro_amd.infer import MCMC, NUTS, shard_chains
+    from numpyro_amd.random import key_to_seed
 
     X, y = datasets.covtype_synthetic(n_rows=args.rows, seed=0)
     lo, hi = shard_chains(args.chains, rank, world)
     kernel = NUTS(P.logistic_regression)
-    mcmc = MCMC(kernel, num_warmup=args.warmup, num_samples=args.steps, num_chains=hi - lo,
+    mcmc = MCMC(kernel, num_warmup=args.adapt, num_samples=args.warmup, num_chains=hi - lo,
                 chain_offset=lo, chain_method="vectorized", progress_bar=False,
                 sync_chains=args.sync_chains)
     Xd = torch.from_numpy(X).to(device)
     yd = torch.from_numpy(y).to(device)
-    # untimed: init + warmup adaptation
+    # untimed: init + adaptation, then the untimed sampling transitions
     mcmc.warmup(args.seed, Xd, yd)
+    if args.warmup > 0:
+        mcmc.run(args.seed + 1, Xd, yd)
+        mcmc.post_warmup_state = mcmc.last_state
+    start_state = mcmc.post_warmup_state
+    mcmc.num_samples = args.steps
     eng = mcmc._engine
     pot = eng.potential
     # time the potential launches inside the timed region with events on its stream
@@ -128,7 +153,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    mcmc.run(args.seed + 1, Xd, yd, extra_fields=("num_steps",))
+    mcmc.run(args.seed + 2, Xd, yd, extra_fields=("num_steps", "diverging"))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -148,28 +173,30 @@ def main():
     gathered = shard.gather_chains(site)
     torch.cuda.synchronize()
     end_of_run_ms = (time.perf_counter() - te0) * 1e3
-    num_steps = mcmc.get_extra_fields()["num_steps"].to(torch.float64).sum()
+    ef = mcmc.get_extra_fields(group_by_chain=True)
+    ns = ef["num_steps"].to(torch.float64)  # [C_local, steps]
+    num_steps = ns.sum()
     launches = mcmc.last_run_stats["launches"]
     pot_ms = sum(a.elapsed_time(b) for a, b in evs)
-    stats = torch.tensor([num_steps.item(), elapsed, pot_ms, float(len(evs)), float(launches)],
-                         dtype=torch.float64, device=device)
+    stats = torch.tensor([num_steps.item(), elapsed, pot_ms, float(len(evs)), float(launches),
+                          float(ef["diverging"].sum().item())], dtype=torch.float64, device=device)
+    tree_max = ns.max(0).values.to(device)  # per timed transition: the largest tree of the shard
     if world > 1:
         tot = stats.clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        useful, elapsed = tot[0].item(), mx[1].item()
+        dist.all_reduce(tree_max, op=dist.ReduceOp.MAX)
+        useful, elapsed, divergent = tot[0].item(), mx[1].item(), tot[5].item()
     else:
-        useful = stats[0].item()
+        useful, divergent = stats[0].item(), stats[5].item()
     value = useful / elapsed
     # dominant kernel: fused logreg potential (two f32 MFMA GEMMs), algorithmic FLOPs per
     # chain-leapfrog = 4 N D; one launch evaluates every LEAF chain.
     local_useful = stats[0].item()
     flop = 4.0 * args.rows * X.shape[1] * local_useful
     achieved = flop / (pot_ms * 1e-3) / 1e12 if pot_ms > 0 else 0.0
-    variant = int(os.environ.get("NMX_LOGREG_VARIANT", "36"))
-    split = 30 <= variant <= 36
-    peak = MI355X_BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS if split else MI355X_FP32_MFMA_PEAK_TFLOPS
+    peak = MI355X_BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
     traffic = None
     try:
         with open(args.traffic_json) as f:
@@ -192,18 +219,22 @@ def main():
             "data": "synthetic covtype (581012x54 N(0,1) standardized + intercept, y~Bernoulli(sigmoid(X@ref_coefs)))",
             "config": {"workload": "covtype logistic regression NUTS, diag mass, max_tree_depth 10",
                        "num_chains": args.chains, "rows": args.rows, "dim": int(X.shape[1]),
+                       "adapt_transitions": args.adapt,
                        "parallelism": f"chains sharded {world}-way (no data-path collective)",
                        "schedule": "lockstep" if args.sync_chains else "per-chain async"},
             "useful_leapfrogs": useful,
+            "mean_tree_size": useful / (args.chains * args.steps),
+            "divergent_frac": divergent / (args.chains * args.steps),
+            "lockstep_equivalent_leapfrogs": float(tree_max.sum().item()) * args.chains,
+            "evaluated_leapfrogs": useful,
             "leapfrog_launches": launches,
+            "chain_slot_occupancy": local_useful / max(1, launches * (hi - lo)),
             "potential_ms_per_launch": pot_ms / max(1, len(evs)),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
                          "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
-                         "kernel": f"k_logreg_x3 (variant {variant}) + k_logreg_finalize" if split
-                         else f"f32 MFMA logreg (variant {variant}) + k_logreg_finalize",
+                         "kernel": "k_logreg_x3 + k_logreg_finalize",
                          "peak_basis": ("bf16 MFMA 2500 TF/s / 6 split products (f32 operands as three bf16 terms, "
-                                        "f32 accumulation); achieved = algorithmic 4*N*D f32 FLOP per chain-leapfrog")
-                         if split else "f32 MFMA 157.3 TF/s",
+                                        "f32 accumulation); achieved = algorithmic 4*N*D f32 FLOP per chain-leapfrog"),
                          "frac_of_f32_mfma_peak": achieved / MI355X_FP32_MFMA_PEAK_TFLOPS},
             "cpu_baseline": None,
             "end_of_run": {"ms": end_of_run_ms, "gathered_chains": int(gathered.shape[0]),
@@ -212,7 +243,9 @@ def main():
                            "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(X, y, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2),
+                                               args.adapt + args.warmup, args.adapt, args.cpu_chains,
+                                               args.cpu_seconds)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

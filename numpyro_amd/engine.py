@@ -22,6 +22,8 @@ from .native import NutsConfig, EvalBatch, check, lib, ptr, stream_ptr
 
 INIT_ATTEMPTS = 100  # find_valid_initial_params (numpyro/infer/util.py:386-388)
 
+_generations = iter(range(1, 1 << 62))  # ids of arena contents (Engine.generation)
+
 
 def build_adaptation_schedule(num_steps):
     """Stan windows, numpyro/infer/hmc_util.py:387-436 (host-side; sent to the device)."""
@@ -91,6 +93,10 @@ class Engine:
         self._views = {}
         self.iteration = 0  # transitions completed by every chain
         self.num_warmup = 0
+        # id of the arena's current contents: a state snapshot taken at this generation can
+        # be resumed without copying the arena back (MCMC.run after warmup, kernel.sample)
+        self.generation = 0
+        self._pool = None  # dense pooled adaptation: (window, PooledCovariance) across run() calls
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
 
@@ -207,8 +213,10 @@ class Engine:
                 raise RuntimeError("Cannot find valid initial parameters. Please check your model "
                                    "again.")  # infer/util.py:795-797
         self.iteration = 0
+        self._pool = None
         if self.dense and imm is not None:
             self._reexpress(imm, None, s)
+        self.generation = next(_generations)
 
     # ------------------------------------------------------------------ dense mass
     def _reexpress(self, inverse_mass_matrix, mu, s):
@@ -241,8 +249,9 @@ class Engine:
                 samples[k][pos] = torch.exp(samples[k][pos])
 
     def _dense_segments(self, it0, it1):
-        """Split [it0, it1) at the ends of middle adaptation windows; yields
-        (a, b, window_is_middle)."""
+        """Split [it0, it1) at the bounds of the middle adaptation windows; yields
+        (a, b, window) with window = (start, end + 1) of the middle window holding [a, b), or
+        None outside them."""
         bounds = []
         if self.opts.adapt_mass_matrix and self.num_warmup > 0:
             sched = build_adaptation_schedule(self.num_warmup)
@@ -254,13 +263,13 @@ class Engine:
             if we1 <= a or ws >= it1:
                 continue
             if ws > a:
-                segs.append((a, ws, False))
+                segs.append((a, ws, None))
                 a = ws
             b = min(we1, it1)
-            segs.append((a, b, b == we1 and a == ws))
+            segs.append((a, b, (ws, we1)))
             a = b
         if a < it1:
-            segs.append((a, it1, False))
+            segs.append((a, it1, None))
         return segs
 
     def run(self, num_iters: int, seed: int, collect_begin: int = 0, collection_size: int | None = None,
@@ -278,9 +287,13 @@ class Engine:
         if self.sync_chains and num_iters > self.iter_capacity:
             self._grow_finished(num_iters)
         S = max(int(collection_size), 0)
-        samples = torch.empty((max(S, 1), self.D, self.ldc), dtype=torch.float32, device=self.device)
-        fields = torch.zeros((max(S, 1), len(native.COLLECT), self.ldc), dtype=torch.float32,
-                             device=self.device)
+        if S > 0:
+            samples = torch.empty((S, self.D, self.ldc), dtype=torch.float32, device=self.device)
+            fields = torch.zeros((S, len(native.COLLECT), self.ldc), dtype=torch.float32, device=self.device)
+        else:  # nothing is collected: the device writes no slot (collection_size 0)
+            samples = torch.empty((0, self.D, self.ldc), dtype=torch.float32, device=self.device)
+            fields = torch.empty((0, len(native.COLLECT), self.ldc), dtype=torch.float32, device=self.device)
+        self.generation = next(_generations)
         cstart = it0 + start_idx
         if not self.dense:
             launches = self._run_segment(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
@@ -289,7 +302,8 @@ class Engine:
             launches = self._run_dense(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
                                        poll_every, s, max_launches)
         self.iteration = it0 + num_iters
-        return samples[:S], fields[:S], launches
+        self.generation = next(_generations)
+        return samples, fields, launches
 
     @staticmethod
     def _slot_of(i, cstart, thinning, S):
@@ -305,19 +319,25 @@ class Engine:
         return [k for k in (self._slot_of(i, cstart, thinning, S) for i in range(a, b)) if k >= 0]
 
     def _run_dense(self, it0, it1, seed, cstart, thinning, S, samples, fields, poll_every, s, max_launches):
+        """Dense mass: segments outside the middle windows run as they are; inside one, every
+        transition's draws (model space) join the window's pool, which persists across run()
+        calls (a kernel stepped one transition at a time pools the same draws), and the window's
+        last transition finalizes it and re-expresses every chain."""
         from .dense import PooledCovariance
         budget = int(float(__import__("os").environ.get("NMX_DENSE_ADAPT_BYTES", 4 << 30)))
         chunk = max(1, budget // (4 * self.D * self.ldc))
         wt = self.potential.whitening
         pos = self.model_potential.transform_codes().to(torch.bool)
         launches = 0
-        for a, b, middle in self._dense_segments(it0, it1):
-            if not middle:
+        for a, b, win in self._dense_segments(it0, it1):
+            if win is None:
                 launches += self._run_segment(a, b, seed, cstart, thinning, S, samples, fields, poll_every, s,
                                               max_launches)
                 self._convert_slots(samples, self._slots_in(a, b, cstart, thinning, S), s)
                 continue
-            pool = PooledCovariance(self.D, self.device, wt.mu)
+            if self._pool is None or self._pool[0] != win:
+                self._pool = (win, PooledCovariance(self.D, self.device, wt.mu))
+            pool = self._pool[1]
             zbuf = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
             for ca in range(a, b, chunk):
                 cb = min(b, ca + chunk)
@@ -335,9 +355,11 @@ class Engine:
                             samples[slot][pos] = torch.exp(samples[slot][pos])
                         fields[slot].copy_(afld[k])
                 del abuf, afld
-            pool.all_reduce()
-            cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
-            self._reexpress(cov, mean, s)
+            if b == win[1]:
+                pool.all_reduce()
+                cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
+                self._pool = None
+                self._reexpress(cov, mean, s)
         return launches
 
     def _persistent_model(self):

@@ -32,6 +32,57 @@ HMCAdaptState = namedtuple(  # hmc_util.py:18-30
      "mm_state", "window_idx", "rng_key"])
 
 
+def snapshot_state(eng, seed, keep_arena=True):
+    """HMCState of every chain of `eng` after its last transition (hmc.py:31-48 fields, chains
+    first).  `keep_arena` copies the device state so the snapshot can be resumed later
+    (MCMC.post_warmup_state / last_state); without it the state is resumable only while the
+    engine has not moved on (MCMCKernel.sample's in-place stepping)."""
+    C = eng.C
+    z_flat, zgrad = eng.model_state()
+    pot = eng.potential
+    z = pot.unflatten(z_flat) if len(pot.sites) else z_flat
+    imm, msq, msq_inv = eng.mass_state()
+    adapt = HMCAdaptState(
+        eng.chain_state("step_size").clone(), imm, msq, msq_inv,
+        (eng.chain_state("da_xt").clone(), eng.chain_state("da_xavg").clone(),
+         eng.chain_state("da_gavg").clone(), eng.chain_state("da_t").clone(),
+         eng.chain_state("da_prox").clone()),
+        (eng.chain_state("wf_mean").clone(), eng.chain_state("wf_m2").clone(),
+         eng.chain_state("wf_n").clone()),
+        eng.chain_state("window_idx").clone(), seed)
+    st = HMCState(
+        eng.chain_state("iter").clone(), z, zgrad,
+        eng.chain_state("pe").clone(), eng.chain_state("energy").clone(), None,
+        eng.opts.trajectory_length, eng.chain_state("last_nsteps").clone(),
+        eng.chain_state("last_acc").clone(), eng.chain_state("mean_acc").clone(),
+        eng.chain_state("last_div").clone().bool(), adapt, seed)
+    st._arena = eng.arena.clone() if keep_arena else None
+    st._whitening = eng.whitening_state()
+    st._iteration = eng.iteration
+    st._num_warmup = eng.num_warmup
+    st._generation = eng.generation
+    st._engine = eng
+    assert C == st.i.shape[0]
+    return st
+
+
+def restore_state(eng, state):
+    """Make `state` the engine's current state (no copy when it already is)."""
+    if getattr(state, "_engine", None) is not eng:
+        raise ValueError("the state belongs to a different model/data binding")
+    if eng.generation == state._generation:
+        return
+    if state._arena is None:
+        raise ValueError("this state was advanced in place by a later sample() call and holds no device "
+                         "copy; pass the state returned by the most recent sample()")
+    eng.arena.copy_(state._arena)
+    eng.set_whitening_state(state._whitening)
+    eng.iteration = state._iteration
+    eng.num_warmup = state._num_warmup
+    eng._pool = None
+    eng.generation = state._generation
+
+
 class MCMCKernel:
     """Interface of numpyro/infer/mcmc.py:32-158."""
 
@@ -157,15 +208,84 @@ class HMC(MCMCKernel):
         return Engine(self.potential(model_args, model_kwargs), num_chains, self.options(), device=device,
                       chain_offset=chain_offset, sync_chains=sync_chains)
 
-    def init(self, rng_key, num_warmup, init_params=None, model_args=(), model_kwargs={}):
-        raise NotImplementedError("drive the device engine through numpyro_amd.infer.MCMC")
+    def init(self, rng_key, num_warmup, init_params=None, model_args=(), model_kwargs={}, *,
+             num_chains=None, chain_offset=0, device=None):
+        """HMC.init (hmc.py:740-822), vectorized: initialises `num_chains` chains on the device
+        (init_to_uniform with retries, or `init_params`) and returns their HMCState.
 
-    def sample(self, state, model_args, model_kwargs):
-        raise NotImplementedError("drive the device engine through numpyro_amd.infer.MCMC")
+        The chain count is `num_chains`, else the leading dimension of a batch of keys
+        (`random.split(key, C)`, as MCMC's vectorized path passes them) or of `init_params`,
+        else 1.  Chain c draws from the Philox stream (seed of the first key, chain_offset + c),
+        so a loop of `sample` calls reproduces `MCMC.run` with the same key bitwise."""
+        import numpy as np
+        import torch
+
+        from ..random import key_to_seed
+
+        keys = np.asarray(rng_key.cpu().numpy() if hasattr(rng_key, "cpu") else rng_key)
+        if num_chains is None:
+            if keys.ndim == 2:
+                num_chains = keys.shape[0]
+            elif init_params is not None and not isinstance(init_params, dict) and np.ndim(init_params) == 2:
+                num_chains = int(np.shape(init_params)[0])
+            elif isinstance(init_params, dict):
+                num_chains = int(np.shape(next(iter(init_params.values())))[0])
+            else:
+                num_chains = 1
+        seed = key_to_seed(keys)
+        eng = self.make_engine(int(num_chains), model_args, model_kwargs, device=device,
+                               chain_offset=chain_offset)
+        ip = None
+        if init_params is not None:
+            ip = eng.potential.flatten(init_params) if isinstance(init_params, dict) else init_params
+            ip = torch.as_tensor(ip, dtype=torch.float32)
+            if ip.dim() == 1:
+                ip = ip[None, :].expand(eng.C, -1)
+        with torch.cuda.device(eng.device):
+            eng.initialize(seed, int(num_warmup), init_params=ip, radius=self.init_radius())
+        self._engine, self._seed = eng, seed
+        self._sample_fn = self.sample
+        return snapshot_state(eng, seed, keep_arena=False)
+
+    def sample(self, state, model_args=(), model_kwargs=None):
+        """One transition of every chain (sample_kernel, hmc.py:459-530) on the device; returns
+        the new HMCState.  The engine advances in place: the returned state is current, the
+        argument becomes a plain record (resuming from it needs a state with a device copy,
+        e.g. MCMC.post_warmup_state)."""
+        import torch
+
+        eng = getattr(state, "_engine", None)
+        if eng is None:
+            raise ValueError("state must come from init() or sample() of this kernel")
+        with torch.cuda.device(eng.device):
+            restore_state(eng, state)
+            eng.run(1, state.adapt_state.rng_key, collection_size=0)
+        return snapshot_state(eng, state.adapt_state.rng_key, keep_arena=False)
+
+    def postprocess_fn(self, model_args=(), model_kwargs=None):
+        """Unconstrained site values -> constrained ones plus deterministic sites
+        (infer/util.py:176-190 constrain_fn)."""
+        import torch
+
+        from ..potentials import POSITIVE
+
+        pot = self.potential(model_args, model_kwargs)
+
+        def fn(z):
+            if not isinstance(z, dict):
+                z = pot.unflatten(z)
+            out = {}
+            for name, _, tr in pot.sites:
+                out[name] = torch.exp(z[name]) if tr == POSITIVE else z[name]
+            out.update(pot.deterministic(out))
+            return out
+
+        return fn
 
     def __getstate__(self):
         state = self.__dict__.copy()
         state["_sample_fn"] = None
+        state["_engine"] = None
         return state
 
 

@@ -17,7 +17,7 @@ import torch
 
 from .. import diagnostics, native, shard
 from ..random import key_to_seed
-from .hmc import HMCAdaptState, HMCState
+from .hmc import restore_state, snapshot_state
 
 _FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
 
@@ -91,40 +91,10 @@ class MCMC:
         return self._last_state
 
     def _snapshot(self, eng, seed):
-        C = eng.C
-        z_flat, zgrad = eng.model_state()
-        pot = eng.potential
-        z = pot.unflatten(z_flat) if len(pot.sites) else z_flat
-        imm, msq, msq_inv = eng.mass_state()
-        adapt = HMCAdaptState(
-            eng.chain_state("step_size").clone(), imm, msq, msq_inv,
-            (eng.chain_state("da_xt").clone(), eng.chain_state("da_xavg").clone(),
-             eng.chain_state("da_gavg").clone(), eng.chain_state("da_t").clone(),
-             eng.chain_state("da_prox").clone()),
-            (eng.chain_state("wf_mean").clone(), eng.chain_state("wf_m2").clone(),
-             eng.chain_state("wf_n").clone()),
-            eng.chain_state("window_idx").clone(), seed)
-        st = HMCState(
-            eng.chain_state("iter").clone(), z, zgrad,
-            eng.chain_state("pe").clone(), eng.chain_state("energy").clone(), None,
-            eng.opts.trajectory_length, eng.chain_state("last_nsteps").clone(),
-            eng.chain_state("last_acc").clone(), eng.chain_state("mean_acc").clone(),
-            eng.chain_state("last_div").clone().bool(), adapt, seed)
-        st._arena = eng.arena.clone()
-        st._whitening = eng.whitening_state()
-        st._iteration = eng.iteration
-        st._num_warmup = eng.num_warmup
-        st._engine = eng
-        assert C == st.i.shape[0]
-        return st
+        return snapshot_state(eng, seed, keep_arena=True)
 
     def _restore(self, eng, state):
-        if getattr(state, "_engine", None) is not eng:
-            raise ValueError("post_warmup_state belongs to a different model/data binding")
-        eng.arena.copy_(state._arena)
-        eng.set_whitening_state(state._whitening)
-        eng.iteration = state._iteration
-        eng.num_warmup = state._num_warmup
+        restore_state(eng, state)
 
     # ------------------------------------------------------------------ run
     def warmup(self, rng_key, *args, extra_fields=(), collect_warmup=False, init_params=None, **kwargs):

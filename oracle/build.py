@@ -1,0 +1,31 @@
+"""ORACLE build (test infrastructure only): compiles the C restatements under oracle/c/ into
+oracle/_lib/*.so with gcc.  Called by __graft_entry__.build(); only bench.py's cpu_baseline
+leg and tests load the result.  Built for x86-64-v3 (AVX2 + FMA) so the library built here
+also runs on the GPU box's host CPU."""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "_lib")
+FLAGS = ["-O3", "-march=x86-64-v3", "-ffast-math", "-fopenmp", "-fPIC", "-shared", "-std=c11", "-Wall"]
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(LIB_DIR, f"lib{name}.so")
+
+
+def build(verbose: bool = False) -> None:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    for src in sorted(glob.glob(os.path.join(HERE, "c", "*.c"))):
+        name = os.path.splitext(os.path.basename(src))[0]
+        out = lib_path(name)
+        if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+            continue
+        r = subprocess.run(["gcc", *FLAGS, src, "-o", out, "-lm"], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"gcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print("built", os.path.relpath(out, os.path.dirname(HERE)))

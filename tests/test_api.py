@@ -103,12 +103,16 @@ def test_dense_segments_split_at_middle_window_ends():
     segs = Engine._dense_segments(Fake(), 0, 2000)
     sched = build_adaptation_schedule(1000)
     middle = [(a, b + 1) for a, b in sched[1:-1]]
-    assert [(a, b) for a, b, m in segs if m] == middle
-    assert segs[0] == (0, 75, False) and segs[-1] == (950, 2000, False)
+    assert [(a, b) for a, b, w in segs if w] == middle
+    assert all(w == (a, b) for a, b, w in segs if w)
+    assert segs[0] == (0, 75, None) and segs[-1] == (950, 2000, None)
     # contiguous cover
     assert all(segs[i][1] == segs[i + 1][0] for i in range(len(segs) - 1))
+    # a run that starts or ends inside a middle window gets the partial piece with its window
+    part = Engine._dense_segments(Fake(), 80, 120)
+    assert part == [(80, 100, (75, 100)), (100, 120, (100, 150))]
     Fake.opts.adapt_mass_matrix = False
-    assert Engine._dense_segments(Fake(), 0, 2000) == [(0, 2000, False)]
+    assert Engine._dense_segments(Fake(), 0, 2000) == [(0, 2000, None)]
 
 
 def test_host_diagnostics_known_values():

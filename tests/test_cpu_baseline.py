@@ -1,0 +1,59 @@
+"""The CPU comparator of bench.py (CPU side 2): the batched C restatement of
+the covtype potential (oracle/c/logreg_batch.c) against the float64 oracle, and the batched
+multi-chain driver (oracle/cpu_batched.py) against independent oracle chains, bitwise."""
+import numpy as np
+
+from oracle import cpu_batched as CB
+from oracle import hmc_ref as H
+from oracle import philox
+from oracle import potentials as OP
+
+
+def _data(N=3000, D=55, seed=0):
+    rs = np.random.RandomState(seed)
+    X = rs.randn(N, D).astype(np.float32)
+    beta = rs.randn(D) * 0.3
+    y = (rs.rand(N) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
+    return X, y
+
+
+def test_logreg_batch_matches_fp64():
+    X, y = _data()
+    Z = (0.2 * np.random.RandomState(1).randn(37, X.shape[1])).astype(np.float32)
+    pe, g = CB.LogRegBatch(X, y)(Z)
+    pe_r, g_r = OP.LogisticRegression(X, y).pe_grad_batch(Z)
+    np.testing.assert_allclose(pe, pe_r, rtol=1e-5)
+    scale = np.abs(X).T @ np.ones(X.shape[0]) + np.abs(Z)  # |X|^T |sigmoid - y| bound
+    assert np.all(np.abs(g - g_r) <= 1e-5 * scale)
+
+
+def test_batched_chains_are_the_oracle_chains():
+    """Batching the potential calls of 6 chains changes nothing: each chain's states equal an
+    independent oracle run (per-row evaluation with the oracle's own f32 potential)."""
+    X, y = _data(N=200, D=5, seed=2)
+    ref = OP.LogisticRegression(X, y, dtype=np.float32)
+
+    def rowwise(Z):
+        out = [ref.pe_grad(z) for z in Z]
+        return np.array([o[0] for o in out], np.float32), np.stack([o[1] for o in out])
+
+    seed, n, W, T = 5, 6, 10, 14
+    oracles, states, indep = [], [], []
+    for c in range(n):
+        o = H.NUTSOracle(ref.pe_grad, 5, W)
+        states.append(o.init(philox.init_uniform(seed, c, 0, 5), seed, c))
+        oracles.append(H.NUTSOracle(None, 5, W))
+        s = states[-1]
+        hist = []
+        for _ in range(T):
+            s = o.sample(s)
+            hist.append(s)
+        indep.append(hist)
+    _, hist, evals, calls = CB.run_chains(rowwise, states, oracles, T)
+    assert evals == sum(s.num_steps for h in indep for s in h)
+    assert calls < evals
+    for c in range(n):
+        for a, b in zip(hist[c], indep[c]):
+            assert a.num_steps == b.num_steps
+            np.testing.assert_array_equal(a.z, b.z)
+            assert a.adapt_state.step_size == b.adapt_state.step_size

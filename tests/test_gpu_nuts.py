@@ -522,3 +522,43 @@ def test_bnn_fits_data(device, dense):
     r2 = 1 - ((Y[:, 0] - yhat) ** 2).mean() / Y[:, 0].var()
     assert r2 > 0.8, r2
     assert np.median(s["prec_obs"]) > 5.0
+
+
+@pytest.mark.parametrize("model,dense", [("logreg", False), ("diag_normal", False), ("mvn", True)])
+def test_kernel_init_sample_loop_matches_mcmc_run(device, model, dense):
+    """MCMCKernel plug-in surface (mcmc.py:90-120, hmc.py:740-822): a caller that drives the
+    kernel itself -- init, then one sample() per transition, as _single_chain_mcmc's
+    fori_collect loop does (mcmc.py:461-513) -- gets bitwise the draws, tree sizes and step
+    sizes of MCMC.run with the same key (fused, wide and dense pooled-adaptation paths; the
+    dense window's pool persists across sample() calls)."""
+    rs = np.random.RandomState(11)
+    if model == "mvn":
+        D = 6
+        a = rs.randn(D, D)
+        args, fm, site = (np.zeros(D), a @ a.T + 0.5 * np.eye(D)), P.multivariate_normal, "x"
+    else:
+        dim = 40 if model == "logreg" else 300
+        args, fm, _, site, *_ = _fixed_step_case(model, dim, rs)
+    C, W, S, seed = 40, 30, 12, 7
+    kern = NUTS(fm, dense_mass=dense)
+    st = kern.init(seed, W, model_args=args, num_chains=C)
+    zs, ns, ss = [], [], []
+    for i in range(W + S):
+        st = kern.sample(st, args, {})
+        if i >= W:
+            zs.append(st.z[site].clone())
+            ns.append(st.num_steps.clone())
+            ss.append(st.adapt_state.step_size.clone())
+    post = kern.postprocess_fn(args, {})(st.z)
+    assert set(post) >= {site}
+    mcmc = MCMC(NUTS(fm, dense_mass=dense), num_warmup=W, num_samples=S, num_chains=C)
+    mcmc.run(seed, *args, extra_fields=("num_steps", "adapt_state.step_size"))
+    ref = mcmc.get_samples(group_by_chain=True)[site]
+    ef = mcmc.get_extra_fields(group_by_chain=True)
+    torch.testing.assert_close(torch.stack(zs, 1), ref, rtol=0, atol=0)
+    torch.testing.assert_close(torch.stack(ns, 1), ef["num_steps"], rtol=0, atol=0)
+    torch.testing.assert_close(torch.stack(ss, 1), ef["adapt_state.step_size"], rtol=0, atol=0)
+    # a state the engine has moved past holds no device copy: resuming from it is refused
+    kern.sample(st, args, {})
+    with pytest.raises(ValueError):
+        kern.sample(st, args, {})
