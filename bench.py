@@ -25,9 +25,8 @@ sys.path.insert(0, ROOT)
 MI355X_FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, Peak FP32 (matrix), dense
 MI355X_BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
 MI355X_HBM_PEAK_GBS = 8000.0
-# The default covtype kernel (NMX_LOGREG_VARIANT 30-36, potential_logreg.hip) runs each f32
-# product as six bf16 MFMA products of three-term splits: its f32-equivalent ceiling is the
-# bf16 MFMA peak / 6.  The f32-MFMA kernels (variants < 30) are bounded by the f32 matrix peak.
+# The covtype kernel (k_logreg_x3, potential_logreg.hip) runs each f32 product as six bf16
+# MFMA products of three-term splits: its f32-equivalent ceiling is the bf16 MFMA peak / 6.
 SPLIT_PRODUCTS = 6
 
 

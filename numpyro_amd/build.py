@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnumpyro_amd.so")
-ARCH = os.environ.get("NMX_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 COMMON_FLAGS = [

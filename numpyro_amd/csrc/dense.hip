@@ -267,116 +267,6 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ p
   }
 }
 
-// Wide-tile version (opt-in: NMX_GEMM_VARIANT=1): 128 rows x 128 chains per workgroup
-// (wave w: rows 32w.., four 32x32 accumulators), halving the A (T) re-reads per chain, and
-// an XCD-aware block order: blocks of one XCD (b % 8) take consecutive chain tiles of the
-// SAME row tile, so the A K-stages they share are served by that XCD's L2.  Measured
-// (profiles/r01): +10% at D=10000, C=4096 all chains; slower at D=5038, C=2048 and in
-// compacted runs (half as many blocks: wave-quantization tail), hence not the default.
-constexpr int TN2 = 128;
-
-__global__ __launch_bounds__(256, 2) void k_gemm_chains_w(const float* __restrict__ At, int lda, int D,
-                                                          const float* __restrict__ In, float* __restrict__ Out,
-                                                          const float* __restrict__ bias, int triangle, int ldc,
-                                                          const int32_t* __restrict__ phase,
-                                                          const int32_t* __restrict__ count, int C, int n_rt,
-                                                          int n_ct) {
-  __shared__ __attribute__((aligned(16))) float As[2][BK * TM];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * TN2];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
-  const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-  const int rt = (q / n_ct) * 8 + xcd;
-  const int ct = q % n_ct;
-  if (rt >= n_rt) return;
-  const int i0 = rt * TM;
-  const int c0 = ct * TN2;
-  // which 64-chain halves hold an evaluated chain (outputs are written per half, the
-  // same 64-chain granularity as k_gemm_chains)
-  bool half_on[2] = {true, true};
-  if (count) {
-    if (c0 >= *count) return;
-  } else {
-    const int ca = c0 + lane, cb = c0 + 64 + lane;
-    half_on[0] = __any(ca < C && (phase == nullptr || phase[ca] >= NMX_PH_LEAF));
-    half_on[1] = __any(cb < C && (phase == nullptr || phase[cb] >= NMX_PH_LEAF));
-    if (!half_on[0] && !half_on[1]) return;
-  }
-  const int kt_begin = triangle == 1 ? i0 / BK : 0;
-  const int nk = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
-
-  auto load_a = [&](int kt, int buf) {
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int inst = w * 4 + qq;
-      const int row = inst * 2 + (lane >> 5);
-      const int col = (lane & 31) * 4;
-      const float* src = At + (size_t)(kt * BK + row) * lda + i0 + col;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                       (void __attribute__((address_space(3)))*)(&As[buf][inst * 256]), 16, 0, 0);
-    }
-  };
-  auto load_b = [&](int kt, float4 (&reg)[4]) {
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int e = qq * 256 + tid;  // float4 index in the 32 x 128 tile
-      const int row = e >> 5;        // 32 float4 per row
-      const int col = (e & 31) * 4;
-      const int k = kt * BK + row;
-      const int c = c0 + col;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < D && c < ldc) v = *reinterpret_cast<const float4*>(In + (size_t)k * ldc + c);
-      reg[qq] = v;
-    }
-  };
-  auto store_b = [&](int buf, const float4 (&reg)[4]) {
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) reinterpret_cast<float4*>(Bs[buf])[qq * 256 + tid] = reg[qq];
-  };
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-  float4 breg[4];
-  load_a(kt_begin, 0);
-  load_b(kt_begin, breg);
-  store_b(0, breg);
-  __syncthreads();
-  for (int kt = kt_begin; kt < nk; ++kt) {
-    const int buf = (kt - kt_begin) & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_a(kt + 1, buf ^ 1);
-      load_b(kt + 1, breg);
-    }
-    const float* as = As[buf];
-    const float* bs = Bs[buf];
-#pragma unroll
-    for (int s2 = 0; s2 < BK / 2; ++s2) {
-      const int k = 2 * s2 + h;
-      const float a = as[k * TM + w * 32 + l31];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bs[k * TN2 + 32 * j + l31], acc[j], 0, 0, 0);
-    }
-    if (more) store_b(buf ^ 1, breg);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = i0 + w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (i < D) {
-      const float bi = bias ? bias[i] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c0 + 32 * j + l31;
-        if (c < ldc && half_on[j >> 1]) Out[(size_t)i * ldc + c] = acc[j][r] + bi;
-      }
-    }
-  }
-}
-
 // pe[c] = 0.5 sum_d (z[d][c] - mu[d]) * g[d][c] for evaluated chains; 4 waves split d,
 // partials combined in fixed order.
 __global__ __launch_bounds__(256) void k_quad_pe(const float* __restrict__ mu, int D, nmx_eval_batch ev) {
@@ -634,14 +524,7 @@ extern "C" int nmx_unpack_columns(const float* in, int ldi, int dim, const int32
 extern "C" int nmx_dense_padded_dim(int D) { return (D + TM - 1) / TM * TM; }
 
 // K-splits of the chain products: a function of D only (results never depend on C).
-static int ksplit_for(int D) {
-  static const int forced = [] {
-    const char* e = getenv("NMX_GEMM_KSPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced > 0) return forced;
-  return D <= 2048 ? 1 : (D + 2559) / 2560;
-}
+static int ksplit_for(int D) { return D <= 2048 ? 1 : (D + 2559) / 2560; }
 
 extern "C" size_t nmx_gemm_chains_workspace_bytes(int dim, int ldc) {
   const int ks = ksplit_for(dim);
@@ -658,39 +541,19 @@ extern "C" int nmx_gemm_chains(const float* At, int lda, int D, const float* In,
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains: lda must be a multiple of %d >= padded D", TM);
   if (In == Out) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: In and Out must not alias");
   if (triangle < 0 || triangle > 2) return nmx_fail(NMX_ERR_INVALID, "gemm_chains: triangle must be 0, 1 or 2");
-  // 2 (default): k_gemm_chains2<32>; 3: k_gemm_chains2<16>; 0: k_gemm_chains (register-
-  // staged B); 1: k_gemm_chains_w (128-chain tiles).  0, 2, 3 give bitwise equal products.
-  static const int wide = [] {
-    const char* e = getenv("NMX_GEMM_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  if (wide == 1 && ldc >= TN2) {
-    const int n_rt = lda / TM, n_ct = (ldc + TN2 - 1) / TN2;
-    const int nb = (n_rt + 7) / 8 * 8 * n_ct;
-    hipLaunchKernelGGL(k_gemm_chains_w, dim3(nb), dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias,
-                       triangle, ldc, phase, active_count, num_chains, n_rt, n_ct);
-    return nmx_check_launch("k_gemm_chains_w");
-  }
+  // k_gemm_chains2 (LDS-DMA staged); operands past 2 GiB (lda > 23170) take the register-
+  // staged k_gemm_chains (64-bit offsets).  Both give bitwise equal products.
   const int ks = workspace ? ksplit_for(D) : 1;
   // block order only permutes blocks (results identical): XCD-aware sweep measured +20-30%
   // on the triangular products at D=5038 (BNN), neutral at D=10000 (profiles/r01)
-  static const int forced_order = [] {
-    const char* e = getenv("NMX_GEMM_ORDER");
-    return e ? atoi(e) : -1;
-  }();
   const int n_rt = lda / TM, n_ct = ldc / TN;
-  const int order = forced_order >= 0 ? forced_order : (n_rt <= 48 ? 1 : 0);
+  const int order = n_rt <= 48 ? 1 : 0;
   dim3 grid = order ? dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks) : dim3(n_rt, n_ct, ks);
   const bool fits32 = (int64_t)lda * lda * 4 < 0x7fffffff && (int64_t)D * ldc * 4 < 0x7fffffff;
-  if (wide >= 2 && fits32) {
-    const int bk = wide == 3 ? 16 : 32;
-    const size_t lds = 2 * (size_t)bk * (TM + TN) * sizeof(float);
-    if (bk == 16)
-      hipLaunchKernelGGL(k_gemm_chains2<16>, grid, dim3(256), lds, (hipStream_t)stream, At, lda, D, In, Out, bias,
-                         triangle, ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
-    else
-      hipLaunchKernelGGL(k_gemm_chains2<32>, grid, dim3(256), lds, (hipStream_t)stream, At, lda, D, In, Out, bias,
-                         triangle, ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
+  if (fits32) {
+    const size_t lds = 2 * (size_t)BK * (TM + TN) * sizeof(float);
+    hipLaunchKernelGGL(k_gemm_chains2<BK>, grid, dim3(256), lds, (hipStream_t)stream, At, lda, D, In, Out, bias,
+                       triangle, ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
   } else {
     hipLaunchKernelGGL(k_gemm_chains, grid, dim3(256), 0, (hipStream_t)stream, At, lda, D, In, Out, bias, triangle,
                        ldc, phase, active_count, num_chains, (float*)workspace, ks, order, n_rt, n_ct);
@@ -738,23 +601,14 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
   // K-splits: a function of D only (never of C), at most ksplit_for(D) (the workspace size);
   // measured at D = 10000 (profiles/r01): no split is fastest all-active (2.2 vs 2.4 ms per
   // triangular product at C = 4096), 2 splits at C = 512 (0.33 vs 0.37)
-  static const int forced_ks = [] {
-    const char* e = getenv("NMX_GEMM_KSPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  const int ks = workspace ? (forced_ks > 0 ? forced_ks : (D <= 16384 ? 1 : (D + 8191) / 8192)) : 1;
+  const int ks = workspace ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
   // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
   // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
-  static const int forced_order = [] {
-    const char* e = getenv("NMX_GEMM_ORDER");
-    return e ? atoi(e) : -1;
-  }();
   const int n_rt = lda / TM, n_ct = ldc / TN;
-  const int order = forced_order >= 0 ? forced_order : 1;
-  dim3 grid = order ? dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks) : dim3(n_rt, n_ct, ks);
+  dim3 grid = dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
   hipLaunchKernelGGL(k_gemm_x3, grid, dim3(256), (size_t)2 * X3_PIECES * 1024, s, (const char*)Ap, lda, D,
                      (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
-                     ks, order, n_rt, n_ct);
+                     ks, 1, n_rt, n_ct);
   if (ks > 1)
     hipLaunchKernelGGL(k_gemm_reduce, dim3((D + 15) / 16, ldc / TN), dim3(256), 0, s, (const float*)workspace, ks,
                        D, ldc, Out, bias, phase, active_count, num_chains);

@@ -30,23 +30,9 @@ constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide
 constexpr int STEP_CPW = 16;        // chains per wave of the fused step (TPC = 8, D >= 16)
 constexpr int SMALL_CPW = 16;        // chains per wave of the one-wave step (D < 16) and persistent kernel
 
-inline int slice_width(int D) {
-  static const int env = [] {  // NMX_WIDE_SW: A/B experiments (a multiple of 4; fixed per process)
-    const char* e = getenv("NMX_WIDE_SW");
-    return e ? (atoi(e) + 3) / 4 * 4 : 0;
-  }();
-  if (env > 0) return env;
-  return D >= 4096 ? 64 : 32;
-}
-// NMX_WIDE_MIN_D overrides the threshold (A/B experiments; a function of D alone either way)
-inline int wide_min_d() {
-  static const int v = [] {
-    const char* e = getenv("NMX_WIDE_MIN_D");
-    return e ? atoi(e) : WIDE_MIN_D;
-  }();
-  return v;
-}
-inline int num_slices(int D) { return D >= wide_min_d() ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
+// slice width of the wide schedule: 32 (D < 4096) and 64 measured best over 16-256
+inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
+inline int num_slices(int D) { return D >= WIDE_MIN_D ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
 constexpr size_t ALIGN = 256;
 
 inline size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }

@@ -35,17 +35,12 @@ from .potentials import REAL, Potential
 DENSE, UPPER, LOWER = 0, 1, 2  # nmx_gemm_chains `triangle` (shape of A in Out = A In)
 
 
-def _use_x3():
-    """Split-bf16 products (nmx_gemm_chains_x3, default) or f32 MFMA (NMX_GEMM_X3=0)."""
-    import os
-
-    return os.environ.get("NMX_GEMM_X3", "1") != "0"
-
-
 class Whitening:
     """z = mu + T w, T T^T = M^-1.  Holds the two padded At operands of nmx_gemm_chains."""
 
-    def __init__(self, dim: int, device):
+    def __init__(self, dim: int, device, x3: bool = True):
+        """x3: split-bf16 products (nmx_gemm_chains_x3, the default) or the f32-MFMA kernel
+        (nmx_gemm_chains, kept for comparison in tests)."""
         self.D = int(dim)
         self.device = torch.device(device)
         self.lda = int(lib().nmx_dense_padded_dim(self.D))
@@ -54,7 +49,7 @@ class Whitening:
         self.mu = torch.zeros(self.D, dtype=torch.float32, device=self.device)
         self._ws = {}
         self._split = {}
-        self.x3 = _use_x3()
+        self.x3 = bool(x3)
         if self.x3:  # MFMA-fragment packs of T^T and T (nmx_gemm_x3_pack_a)
             nb = lib().nmx_gemm_x3_packed_a_bytes(self.lda)
             self.fwd_p = torch.empty(nb, dtype=torch.uint8, device=self.device)

@@ -65,10 +65,16 @@ class SamplerOptions:
     regularize_mass_matrix: bool = True
     max_delta_energy: float = 1000.0
     inverse_mass_matrix: object = None  # diag [D] or None
+    # dense pooled adaptation: bytes of window draws buffered per chunk
+    dense_adapt_bytes: int = 4 << 30
 
 
 class Engine:
     """Chains of one device: arena + potential + launch loop."""
+
+    # one-launch persistent schedule for one-wave models (False: the launched loop; tests
+    # compare the two)
+    persistent = True
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
@@ -324,8 +330,7 @@ class Engine:
         calls (a kernel stepped one transition at a time pools the same draws), and the window's
         last transition finalizes it and re-expresses every chain."""
         from .dense import PooledCovariance
-        budget = int(float(__import__("os").environ.get("NMX_DENSE_ADAPT_BYTES", 4 << 30)))
-        chunk = max(1, budget // (4 * self.D * self.ldc))
+        chunk = max(1, int(self.opts.dense_adapt_bytes) // (4 * self.D * self.ldc))
         wt = self.potential.whitening
         pos = self.model_potential.transform_codes().to(torch.bool)
         launches = 0
@@ -365,9 +370,7 @@ class Engine:
     def _persistent_model(self):
         """(model id, p0, p1, n) when the run can use the one-launch persistent schedule
         (nmx_nuts_run_small: one-wave model with an inline potential, per-chain async)."""
-        import os
-
-        if self.sync_chains or self.D >= 16 or os.environ.get("NMX_PERSISTENT", "1") == "0":
+        if self.sync_chains or self.D >= 16 or not self.persistent:
             return None
         fn = getattr(self.potential, "small_model", None)
         return fn() if fn is not None else None

@@ -15,7 +15,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NMX_LIB", os.path.join(_HERE, "_lib", "libnumpyro_amd.so"))
+LIB_PATH = os.path.join(_HERE, "_lib", "libnumpyro_amd.so")
 
 _lib = None
 

@@ -122,10 +122,8 @@ def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None,
     if flops_per_leapfrog:
         tf = flops_per_leapfrog * ns / (pot_ms * 1e-3) / 1e12
         peak = PEAK_F32_TFLOPS
-        if name == "covtype" and 30 <= int(os.environ.get("NMX_LOGREG_VARIANT", "36")) <= 36:
-            peak = 2500.0 / 6  # split-bf16 kernel: bf16 MFMA peak / 6 products (bench.py)
-        if eng.dense and os.environ.get("NMX_GEMM_X3", "1") != "0":
-            peak = 2500.0 / 6  # split-bf16 chain products (nmx_gemm_chains_x3)
+        if name == "covtype" or eng.dense:
+            peak = 2500.0 / 6  # split-bf16 products: bf16 MFMA peak / 6 (bench.py)
         out["roofline"] = {"bound": "mfma", "achieved_tflops": round(tf, 2), "peak": round(peak, 1),
                            "frac": round(tf / peak, 3)}
     if bytes_per_leapfrog:

@@ -10,8 +10,10 @@ from numpyro_amd.infer import MCMC, NUTS
 
 W, S, C = (int(a) for a in (sys.argv[1:4] + ["1000", "1000", "4"][len(sys.argv[1:4]):]))
 args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+from numpyro_amd.engine import Engine
+
 for mode in ("1", "0", "1"):
-    os.environ["NMX_PERSISTENT"] = mode
+    Engine.persistent = mode == "1"
     mcmc = MCMC(NUTS(P.eight_schools), num_warmup=W, num_samples=S, num_chains=C, progress_bar=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

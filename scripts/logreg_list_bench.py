@@ -1,14 +1,13 @@
 """Potential launch time with a compacted active list inside a wide batch (ldc = 4096), as in
 the tail of a NUTS run, vs a dense batch of the same chains.
-usage: python scripts/logreg_list_bench.py variant [counts]"""
+usage: python scripts/logreg_list_bench.py [counts]"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from numpyro_amd import datasets, native
 from numpyro_amd.potentials import LogisticRegression
 
-os.environ["NMX_LOGREG_VARIANT"] = sys.argv[1] if len(sys.argv) > 1 else "30"
-counts = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "1,32,69,128,256,512").split(",")]
+counts = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "1,32,69,128,256,512").split(",")]
 X, y = datasets.covtype_synthetic(seed=0)
 N, D = X.shape
 dev = torch.device("cuda:0")
@@ -37,5 +36,5 @@ for n in counts:
         pot.evaluate(ev, s)
     b.record(); b.synchronize()
     ms = a.elapsed_time(b) / 20
-    print(f"variant {os.environ['NMX_LOGREG_VARIANT']} active {n} of ldc {LDC}: {ms:.3f} ms/eval, "
+    print(f"active {n} of ldc {LDC}: {ms:.3f} ms/eval, "
           f"{4.0 * N * D * n / (ms * 1e-3) / 1e12:.1f} TFLOP/s", flush=True)

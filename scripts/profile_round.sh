@@ -13,7 +13,7 @@ step() { echo "== $1" >> "$O/steps.log"; shift; "$@"; rc=$?; echo "rc=$rc" >> "$
 if [ "$part" != b ]; then
 step fetch timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o p -- python3 scripts/bench_potential.py d 4096
 step write timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o p -- python3 scripts/bench_potential.py d 4096
-step traffic python3 scripts/traffic_json.py "$O/pmc_fetch" "$O/pmc_write" "$O/traffic.json" "k_logreg_x3 (NMX_LOGREG_VARIANT default 36), C=4096 all active"
+step traffic python3 scripts/traffic_json.py "$O/pmc_fetch" "$O/pmc_write" "$O/traffic.json" "k_logreg_x3, C=4096 all active"
 # the bench line reports this round's PMC traffic (bench.py --traffic-json)
 step bench timeout -k 10 600 bash -c "python bench.py --traffic-json $O/traffic.json > $O/bench_line.json 2> $O/bench.err"
 step ktrace timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace" -o bench -- python3 bench.py --no-cpu-baseline --traffic-json $O/traffic.json

@@ -346,67 +346,6 @@ def test_whitened_packed_list_matches_dense_batch(device):
     assert np.all(np.isnan(pe_l[others])) and np.all(np.isnan(g_l[:, others]))
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "3"])
-def test_gemm_chains_variant_subprocess(device, variant):
-    """The non-default NMX_GEMM_VARIANTs -- 0 (register-staged B), 1 (128 x 128 tiles,
-    XCD-aware order), 3 (LDS-DMA stages, BK 16) -- pass the same checks as the default (2);
-    the variant is latched per process, hence a child process."""
-    import subprocess
-    import sys
-
-    env = dict(__import__("os").environ, NMX_GEMM_VARIANT=variant)
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", __file__,
-                        "-k", "gemm_chains_matches_fp64 or packed_list"], env=env, capture_output=True, text=True,
-                       timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-_GEMM_DUMP = r"""
-import sys, numpy as np, torch
-from numpyro_amd import native
-lib = native.lib()
-dev = torch.device("cuda:0")
-out = []
-for D, C, tri, ks in ((300, 192, 0, 1), (300, 192, 1, 1), (1000, 128, 2, 1), (5038, 256, 1, 2), (5038, 256, 0, 2)):
-    g = torch.Generator().manual_seed(D + tri)
-    lda = lib.nmx_dense_padded_dim(D)
-    ldc = (C + 63) // 64 * 64
-    A = torch.randn(D, D, generator=g)
-    A = {0: A, 1: torch.triu(A), 2: torch.tril(A)}[tri]
-    At = torch.zeros(lda, lda); At[:D, :D] = A.t()
-    x = torch.randn(D, ldc, generator=g)
-    At, x = At.to(dev), x.to(dev)
-    y = torch.full((D, ldc), float("nan"), device=dev)
-    nws = lib.nmx_gemm_chains_workspace_bytes(D, ldc)
-    ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=dev)
-    native.check(lib.nmx_gemm_chains(native.ptr(At), lda, D, native.ptr(x), native.ptr(y), None, tri, ldc, None,
-                                     None, C, native.ptr(ws) if nws else None, native.stream_ptr()))
-    torch.cuda.synchronize()
-    out.append(y.cpu().numpy())
-np.savez(sys.argv[1], *out)
-"""
-
-
-@pytest.mark.parametrize("variant", ["0", "3"])
-def test_gemm_chains_variants_bitwise(device, variant, tmp_path):
-    """GEMM variants 0 and 3 run the same MFMA sequence per output as the default (2):
-    bitwise equal products (plain, upper, lower, split-K)."""
-    import os
-    import subprocess
-    import sys
-
-    res = {}
-    for v in ("2", variant):
-        path = str(tmp_path / f"g{v}.npz")
-        env = dict(os.environ, NMX_GEMM_VARIANT=v)
-        r = subprocess.run([sys.executable, "-c", _GEMM_DUMP, path], env=env, capture_output=True, text=True,
-                           timeout=600, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        res[v] = np.load(path)
-    for k in res["2"].files:
-        np.testing.assert_array_equal(res[variant][k], res["2"][k], err_msg=k)
-
-
 def test_funnel_10k_dense_nuts_runs(device):
     """BASELINE config 2 shape (examples/funnel.py at dim 10000, dense mass) end to end at
     reduced chains and iterations: W = 20 (windows [0-2], [3-17], [18-19]: one pooled

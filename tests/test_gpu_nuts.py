@@ -353,8 +353,10 @@ def test_persistent_schedule_is_bitwise_the_launched_one(device, model, monkeypa
     else:
         fm, args = P.diag_normal, (np.array([1.0, -2.0, 0.5], np.float32), np.array([1.0, 0.3, 2.0], np.float32))
     out = {}
+    from numpyro_amd.engine import Engine
+
     for mode in ("0", "1"):
-        monkeypatch.setenv("NMX_PERSISTENT", mode)
+        monkeypatch.setattr(Engine, "persistent", mode == "1")
         mcmc = MCMC(NUTS(fm), num_warmup=150, num_samples=100, num_chains=70)
         mcmc.run(5, *args, extra_fields=("num_steps", "diverging", "potential_energy", "accept_prob"))
         out[mode] = (mcmc.get_samples(True), mcmc.get_extra_fields(True), mcmc.last_run_stats["launches"])

@@ -253,30 +253,11 @@ def test_bnn_skips_inactive_and_list(device):
     assert np.all(np.isnan(pe[phase == 0])) and np.all(np.isfinite(pe[phase == 3]))
 
 
-def test_logreg_kernel_variants_agree(device, monkeypatch):
-    """The f32-MFMA A/B kernels (NMX_LOGREG_VARIANT 22 = row lanes, 0 = generic tiles) and the
-    split-bf16 default agree to f32 accumulation level on the same inputs."""
-    from numpyro_amd.potentials import LogisticRegression
-
-    rs = np.random.RandomState(11)
-    N, D, C = 5000, 55, 96
-    X = rs.randn(N, D).astype(np.float32)
-    y = (rs.rand(N) < 0.3).astype(np.float32)
-    Z = (rs.randn(C, D) * 0.2).astype(np.float32)
-    out = {}
-    for v in ("22", "0", "36"):
-        monkeypatch.setenv("NMX_LOGREG_VARIANT", v)
-        out[v] = _eval(LogisticRegression(X, y), Z, device)
-    for v in ("0", "36"):
-        np.testing.assert_allclose(out[v][0], out["22"][0], rtol=1e-6, err_msg=v)
-        np.testing.assert_allclose(out[v][1], out["22"][1], rtol=1e-5, atol=1e-3, err_msg=v)
-
-def test_logreg_split_bf16_matches_f32_accuracy(device, monkeypatch):
-    """The split-bf16 kernels (NMX_LOGREG_VARIANT 30-36: every f32 operand as three bf16
-    terms, six bf16 MFMA products per k-step, f32 accumulation) carry f32-level error: against
-    a float64 evaluation their U and gradient errors stay within 3x those of the f32-MFMA
-    kernel (variant 22) and below 3e-6 of max|grad| per chain.  The schedules 30-35 (2- and
-    3-slot ring, software-pipelined with one ring or split rings, hand-interleaved) run the same arithmetic in the same order: bitwise equal."""
+def test_logreg_split_bf16_matches_f32_accuracy(device):
+    """The split-bf16 kernel (every f32 operand as three bf16 terms, six bf16 MFMA products
+    per k-step, f32 accumulation) carries f32-level error: against a float64 evaluation its U
+    and gradient errors stay within 3x those of a plain float32 evaluation of the same
+    formulas (NumPy, the oracle in float32) and below 3e-6 of max|grad| per chain."""
     from numpyro_amd.potentials import LogisticRegression
 
     X, y = datasets.covtype_synthetic(seed=0)
@@ -285,18 +266,16 @@ def test_logreg_split_bf16_matches_f32_accuracy(device, monkeypatch):
     C, D = 160, X.shape[1]
     Z = (datasets.COVTYPE_REF_COEFS[None, :] + 0.05 * rs.randn(C, D)).astype(np.float32)
     pe_r, g_r = OP.LogisticRegression(X.astype(np.float64), y.astype(np.float64)).pe_grad_batch(Z.astype(np.float64))
-    out = {}
-    for v in ("22", "30", "31", "32", "33", "34", "35", "36"):
-        monkeypatch.setenv("NMX_LOGREG_VARIANT", v)
-        out[v] = _eval(LogisticRegression(X, y), Z, device)
+    f32 = OP.LogisticRegression(X, y, dtype=np.float32)
+    o32 = [f32.pe_grad(z) for z in Z]
+    pe32 = np.array([o[0] for o in o32], np.float64)
+    g32 = np.stack([o[1] for o in o32]).astype(np.float64)
+    pe, g = _eval(LogisticRegression(X, y), Z, device)
     gscale = np.abs(g_r).max(1)
-    err = {v: (np.abs(out[v][0] - pe_r) / np.abs(pe_r), np.abs(out[v][1] - g_r).max(1) / gscale) for v in out}
-    for v in ("31", "32", "33", "34", "35"):
-        np.testing.assert_array_equal(out[v][0], out["30"][0], err_msg=v)
-        np.testing.assert_array_equal(out[v][1], out["30"][1], err_msg=v)
-    # 36 (the default): Z pre-scaled by -log2(e) before the split -- rounds differently, same
-    # error level
-    for v in ("30", "36"):
-        assert err[v][0].max() <= max(3 * err["22"][0].max(), 2e-7), (v, err[v][0].max(), err["22"][0].max())
-        assert err[v][1].max() <= 3e-6, (v, err[v][1].max())
-        assert np.median(err[v][1]) <= 3 * np.median(err["22"][1]), (v, np.median(err[v][1]), np.median(err["22"][1]))
+    e_pe, e_g = np.abs(pe - pe_r) / np.abs(pe_r), np.abs(g - g_r).max(1) / gscale
+    r_pe, r_g = np.abs(pe32 - pe_r) / np.abs(pe_r), np.abs(g32 - g_r).max(1) / gscale
+    print(f"split-bf16 vs fp64: U {e_pe.max():.2e} grad {e_g.max():.2e} (median {np.median(e_g):.2e}); "
+          f"NumPy float32: U {r_pe.max():.2e} grad {r_g.max():.2e} (median {np.median(r_g):.2e})")
+    assert e_pe.max() <= max(3 * r_pe.max(), 2e-7)
+    assert e_g.max() <= 3e-6
+    assert np.median(e_g) <= 3 * max(np.median(r_g), 1e-7)
