@@ -66,12 +66,14 @@ enum nmx_field {
   NMX_F_PHASE = 0, NMX_F_ITER, NMX_F_DEPTH, NMX_F_SUB_N, NMX_F_DIR, NMX_F_TREE_N,
   NMX_F_WINDOW_IDX, NMX_F_DA_T, NMX_F_WF_N, NMX_F_TURNING, NMX_F_TREE_DIV, NMX_F_SUB_DIV,
   NMX_F_HMC_K, NMX_F_HMC_N, NMX_F_LAST_NSTEPS, NMX_F_LAST_DIV, NMX_F_MAXDEPTH_CUR,
+  NMX_F_HS_K, NMX_F_HS_DIR, NMX_F_HS_LAST,
   /* decisions of the last step, consumed by the wide (D-split) vector kernels */
   NMX_F_ACTION, NMX_F_SLOT, NMX_F_ACT_WFN,
   /* per-chain float scalars */
   NMX_F_STEP_SIZE, NMX_F_E0, NMX_F_PE, NMX_F_ENERGY, NMX_F_TREE_W, NMX_F_TREE_ACC,
   NMX_F_SUB_W, NMX_F_SUB_ACC, NMX_F_PE_SUB, NMX_F_E_SUB, NMX_F_DA_XT, NMX_F_DA_XAVG,
-  NMX_F_DA_GAVG, NMX_F_DA_PROX, NMX_F_MEAN_ACC, NMX_F_LAST_ACC, NMX_F_STEP_EFF, NMX_F_PE_EVAL,
+  NMX_F_DA_GAVG, NMX_F_DA_PROX, NMX_F_MEAN_ACC, NMX_F_LAST_ACC, NMX_F_STEP_EFF, NMX_F_HS_STEP,
+  NMX_F_HS_E0, NMX_F_PE_EVAL,
   /* per-chain vectors [D][ldc] */
   NMX_F_Z, NMX_F_ZGRAD, NMX_F_ZL, NMX_F_RL, NMX_F_GL, NMX_F_ZR, NMX_F_RR, NMX_F_GR,
   NMX_F_ZSUB, NMX_F_GSUB, NMX_F_RSUM, NMX_F_RSUM_SUB, NMX_F_INV_MASS, NMX_F_MASS_SQRT,
@@ -161,6 +163,17 @@ int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void* stream);
 /* Set every non-DONE chain with a stored state to START and extend iter_end; used when a
  * run continues from post_warmup_state / last_state (mcmc.py:664-670). */
 int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream);
+/* find_reasonable_step_size (numpyro/infer/hmc_util.py:314-384), run by warmup_adapter at
+ * init (:573-576) and at the end of every middle adaptation window (:619-626) when
+ * find_heuristic_step_size (hmc.py:320-331): begin resets every chain's search; each round is
+ * propose (step *= 2^direction, momentum r = M^-1 eps as the reference draws it, first half
+ * step -> z_eval; searching chains listed in active list 0, count in counters[2]) -> the
+ * model's potential on that list -> finish (second half step, dE, new direction; a chain that
+ * stops stores its step size and restarts dual averaging there, at_init selecting
+ * log(10 step) or log(10) + log(step)).  counters[1] = chains still searching. */
+int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void* stream);
+int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream);
+int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, void* stream);
 /* One lockstep step of the per-chain NUTS/HMC state machine (sample_kernel hmc.py:459-530
  * with build_tree hmc_util.py:1088-1180 unrolled into leaves): consumes the potential at
  * z_eval for LEAF chains, advances trees / transitions / adaptation / collection, and

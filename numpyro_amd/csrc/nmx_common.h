@@ -22,6 +22,7 @@ enum nmx_rng_event : uint32_t {
   NMX_EV_LEAF = 4u,       // leaf-level (uniform) transition, word3 = leaf index
   NMX_EV_INIT = 5u,       // init_to_uniform draw, word3 = attempt
   NMX_EV_ACCEPT = 6u,     // HMC Metropolis accept
+  NMX_EV_HEURISTIC = 8u,  // find_reasonable_step_size momentum, word2 = block, word3 = attempt
 };
 
 struct nmx_u4 { uint32_t x, y, z, w; };

@@ -1240,6 +1240,106 @@ __global__ void k_nuts_resume(Arena a, nmx_nuts_config cfg) {
   if (ph == NMX_PH_DONE || ph == NMX_PH_WAIT || ph == NMX_PH_START) AI(NMX_F_PHASE)[c] = NMX_PH_START;
 }
 
+// ---- find_reasonable_step_size (hmc_util.py:314-384) ----------------------------------
+// Per chain, from its stored state (z, U, grad): repeat { step *= 2^direction; r = momentum;
+// one velocity_verlet step; direction' = log(0.8) < -dE ? 1 : -1 } while the direction keeps
+// its sign and the step stays within (tiny, max).  The reference draws the momentum as
+// momentum_generator(z, inverse_mass_matrix, key) (hmc_util.py:359), i.e. r = M^-1 eps (the
+// inverse mass where momentum_generator expects its square root); reproduced as is.
+// HS_K = attempt count (-1: search finished), HS_DIR / HS_LAST = direction / last direction,
+// HS_STEP = step, HS_E0 = energy of the attempt's start; RL holds r(n+1/2) of the attempt.
+__global__ void k_heur_begin(Arena a, nmx_nuts_config cfg) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[1] = 0;
+  if (c >= cfg.num_chains) return;
+  AI(NMX_F_HS_K)[c] = 0;
+  AI(NMX_F_HS_DIR)[c] = 0;
+  AI(NMX_F_HS_LAST)[c] = 0;
+  AF(NMX_F_HS_STEP)[c] = AF(NMX_F_STEP_SIZE)[c];
+}
+
+// step update, momentum, first half step and z_eval; lists the searching chains (list 0)
+__global__ void k_heur_propose(Arena a, nmx_nuts_config cfg) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = c < cfg.num_chains ? AI(NMX_F_HS_K)[c] : -1;
+  const bool act = k >= 0;
+  if (act) {
+    const int dir = AI(NMX_F_HS_DIR)[c];
+    const float step = AF(NMX_F_HS_STEP)[c] * (dir > 0 ? 2.0f : (dir < 0 ? 0.5f : 1.0f));
+    AF(NMX_F_HS_STEP)[c] = step;
+    const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+    const int it = AI(NMX_F_ITER)[c];
+    const int ldc = cfg.ldc;
+    float ke = 0.0f;
+    for (int blk = 0; 4 * blk < cfg.dim; ++blk) {
+      const nmx_u4 x = nmx_rng(cfg.seed, gch, (uint32_t)it, NMX_EV_HEURISTIC, blk, (uint32_t)k);
+      float n[4];
+      nmx_box_muller(x.x, x.y, n[0], n[1]);
+      nmx_box_muller(x.z, x.w, n[2], n[3]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * blk + q;
+        if (d < cfg.dim) {
+          const size_t idx = (size_t)d * ldc + c;
+          const float im = cfg.unit_mass ? 1.0f : AV(NMX_F_INV_MASS)[idx];
+          const float r = im * n[q];
+          ke += (im * r) * r;
+          const float rh = r - (0.5f * step) * AV(NMX_F_ZGRAD)[idx];
+          AV(NMX_F_RL)[idx] = rh;
+          AV(NMX_F_Z_EVAL)[idx] = AV(NMX_F_Z)[idx] + step * (im * rh);
+        }
+      }
+    }
+    AF(NMX_F_HS_E0)[c] = 0.5f * ke + AF(NMX_F_PE)[c];  // kinetic_fn(imm, r) + potential_energy
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(act);
+  if (m) {
+    int base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(&a.counters[2], __builtin_popcountll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (act) a.active_idx[base + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = c;
+  }
+}
+
+// second half step, energy change, new direction; a chain whose search ends stores its step
+// size and restarts dual averaging at it (warmup_adapter :573-576 at init, :619-626 at window
+// ends); counters[1] = chains still searching
+__global__ void k_heur_finish(Arena a, nmx_nuts_config cfg, int at_init) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.counters[2]) return;
+  const int c = a.active_idx[p];
+  const int ldc = cfg.ldc;
+  const float step = AF(NMX_F_HS_STEP)[c];
+  float ke = 0.0f;
+  for (int d = 0; d < cfg.dim; ++d) {
+    const size_t idx = (size_t)d * ldc + c;
+    const float im = cfg.unit_mass ? 1.0f : AV(NMX_F_INV_MASS)[idx];
+    const float r = AV(NMX_F_RL)[idx] - (0.5f * step) * AV(NMX_F_G_EVAL)[idx];
+    ke += (im * r) * r;
+  }
+  const float dE = (0.5f * ke + AF(NMX_F_PE_EVAL)[c]) - AF(NMX_F_HS_E0)[c];
+  const int dir_new = logf(0.8f) < -dE ? 1 : -1;  // NaN dE -> -1
+  const int last = AI(NMX_F_HS_DIR)[c];
+  AI(NMX_F_HS_LAST)[c] = last;
+  AI(NMX_F_HS_DIR)[c] = dir_new;
+  const bool not_small = step > 1.17549435e-38f || dir_new >= 0;
+  const bool not_large = step < 3.40282347e+38f || dir_new <= 0;
+  if (not_small && not_large && (last == 0 || dir_new == last)) {
+    AI(NMX_F_HS_K)[c] = AI(NMX_F_HS_K)[c] + 1;
+    atomicAdd(&a.counters[1], 1);
+  } else {
+    AI(NMX_F_HS_K)[c] = -1;
+    AF(NMX_F_STEP_SIZE)[c] = step;
+    AF(NMX_F_STEP_EFF)[c] = step;
+    AF(NMX_F_DA_PROX)[c] = at_init ? logf(10.0f * step) : logf(10.0f) + logf(step);
+    AF(NMX_F_DA_XT)[c] = 0.0f;
+    AF(NMX_F_DA_XAVG)[c] = 0.0f;
+    AF(NMX_F_DA_GAVG)[c] = 0.0f;
+    AI(NMX_F_DA_T)[c] = 0;
+  }
+}
+
 int validate(const nmx_nuts_config* cfg) {
   if (!cfg) return nmx_fail(NMX_ERR_INVALID, "config is NULL");
   if (cfg->num_chains <= 0 || cfg->dim <= 0) return nmx_fail(NMX_ERR_INVALID, "num_chains and dim must be positive");
@@ -1333,6 +1433,36 @@ extern "C" int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void
   hipLaunchKernelGGL(k_nuts_init_check, dim3((cfg->num_chains + 63) / 64), dim3(64), 0,
                      (hipStream_t)stream, a, *cfg);
   return nmx_check_launch("k_nuts_init_check");
+}
+
+extern "C" int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  hipLaunchKernelGGL(k_heur_begin, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a, *cfg);
+  return nmx_check_launch("k_heur_begin");
+}
+
+extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  if (hipMemsetAsync(a.counters + 2, 0, 4, (hipStream_t)stream) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
+  hipLaunchKernelGGL(k_heur_propose, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a,
+                     *cfg);
+  return nmx_check_launch("k_heur_propose");
+}
+
+extern "C" int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  Arena a = arena_of(cfg, arena);
+  if (hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
+  hipLaunchKernelGGL(k_heur_finish, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a,
+                     *cfg, at_init);
+  return nmx_check_launch("k_heur_finish");
 }
 
 extern "C" int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream) {

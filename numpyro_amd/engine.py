@@ -67,6 +67,7 @@ class SamplerOptions:
     inverse_mass_matrix: object = None  # diag [D] or None
     # dense pooled adaptation: bytes of window draws buffered per chunk
     dense_adapt_bytes: int = 4 << 30
+    find_heuristic_step_size: bool = False
 
 
 class Engine:
@@ -222,9 +223,38 @@ class Engine:
         self._pool = None
         if self.dense and imm is not None:
             self._reexpress(imm, None, s)
+        if self._heuristic():
+            self._find_step_size(True, s)
         self.generation = next(_generations)
 
     # ------------------------------------------------------------------ dense mass
+    def _heuristic(self):
+        o = self.opts
+        return bool(o.find_heuristic_step_size) and bool(o.adapt_step_size) and self.num_warmup > 0
+
+    def _find_step_size(self, at_init, s):
+        """find_reasonable_step_size for every chain from its stored state (warmup_adapter at
+        init, hmc_util.py:573-576, and at middle-window ends, :619-626): rounds of propose ->
+        potential on the searching chains -> finish until no chain searches."""
+        L = lib()
+        cfgp = ctypes.byref(self.cfg)
+        arena = ptr(self.arena)
+        ev = self.eval_lists[0]
+        ev.num_chains = self.C
+        check(L.nmx_heuristic_begin(cfgp, arena, s), "nmx_heuristic_begin")
+        for _ in range(600):  # the step doubles or halves each round: <= 2 x 254 rounds to an extreme
+            check(L.nmx_heuristic_propose(cfgp, arena, s), "nmx_heuristic_propose")
+            self.potential.evaluate(ev, s)
+            check(L.nmx_heuristic_finish(cfgp, arena, int(at_init), s), "nmx_heuristic_finish")
+            if int(self.view("counters")[1].item()) == 0:
+                return
+        raise RuntimeError("find_reasonable_step_size did not terminate")
+
+    def _window_ends(self):
+        """First transition index after each middle adaptation window (hmc_util.py:596-635)."""
+        sched = build_adaptation_schedule(self.num_warmup)
+        return [we + 1 for i, (_, we) in enumerate(sched) if 0 < i < len(sched) - 1]
+
     def _reexpress(self, inverse_mass_matrix, mu, s):
         """Change the whitening of every chain (at an iteration boundary): z is kept,
         w = T_new^-1 (z - mu_new), and U, grad_w are re-evaluated at the new w."""
@@ -302,8 +332,21 @@ class Engine:
         self.generation = next(_generations)
         cstart = it0 + start_idx
         if not self.dense:
-            launches = self._run_segment(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
-                                         poll_every, s, max_launches)
+            # with the step-size search, stop at every middle-window end it runs at
+            cuts = [e for e in self._window_ends() if it0 < e <= it0 + num_iters] if self._heuristic() else []
+            launches, a = 0, it0
+            for b in cuts + [it0 + num_iters]:
+                if b > a:
+                    launches += self._run_segment(a, b, seed, cstart, thinning, S, samples, fields, poll_every, s,
+                                                  max_launches)
+                if b in cuts:
+                    self._find_step_size(False, s)
+                    # the transition that ended the window reports the searched step size, as
+                    # its adapt_state does in the reference (update_fn returns it, :700-705)
+                    slot = self._slot_of(b - 1, cstart, thinning, S)
+                    if slot >= 0:
+                        fields[slot, native.COLLECT.index("step_size"), :self.C] = self.view("step_size")[:self.C]
+                a = b
         else:
             launches = self._run_dense(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
                                        poll_every, s, max_launches)

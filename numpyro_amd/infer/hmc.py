@@ -137,8 +137,9 @@ class HMC(MCMCKernel):
                               "can't be adapted", stacklevel=2)
         if kinetic_fn is not None:
             raise NotImplementedError("custom kinetic_fn: the engine uses the Euclidean kinetic energy")
-        if find_heuristic_step_size:
-            raise NotImplementedError("find_heuristic_step_size=True is not supported yet")
+        if find_heuristic_step_size and dense_mass:
+            raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
+                                      "coordinates, the dense engine in whitened ones")
         if isinstance(dense_mass, (list, tuple)) and len(dense_mass) > 0:
             raise NotImplementedError("structured dense_mass (list of site groups) is not supported; "
                                       "use dense_mass=True for a full dense mass matrix")
@@ -160,6 +161,7 @@ class HMC(MCMCKernel):
         self._max_tree_depth = 10
         self._init_strategy = init_strategy
         self._regularize_mass_matrix = regularize_mass_matrix
+        self._find_heuristic_step_size = bool(find_heuristic_step_size)
         self._potential = potential_fn
         self._sample_fn = None
 
@@ -188,7 +190,8 @@ class HMC(MCMCKernel):
             target_accept_prob=self._target_accept_prob, max_tree_depth=md,
             trajectory_length=self._trajectory_length, num_steps=self._num_steps,
             regularize_mass_matrix=self._regularize_mass_matrix,
-            inverse_mass_matrix=self._inverse_mass_matrix)
+            inverse_mass_matrix=self._inverse_mass_matrix,
+            find_heuristic_step_size=self._find_heuristic_step_size)
 
     def potential(self, model_args=(), model_kwargs=None) -> Potential:
         if self._model is not None:

@@ -37,9 +37,11 @@ PH_DONE, PH_WAIT, PH_START, PH_LEAF, PH_INITEVAL, PH_NEEDINIT = range(6)
 FIELDS = [
     "phase", "iter", "depth", "sub_n", "dir", "tree_n", "window_idx", "da_t", "wf_n", "turning",
     "tree_div", "sub_div", "hmc_k", "hmc_n", "last_nsteps", "last_div", "maxdepth_cur",
+    "hs_k", "hs_dir", "hs_last",
     "action", "slot", "act_wfn",
     "step_size", "e0", "pe", "energy", "tree_w", "tree_acc", "sub_w", "sub_acc", "pe_sub", "e_sub",
-    "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "pe_eval",
+    "da_xt", "da_xavg", "da_gavg", "da_prox", "mean_acc", "last_acc", "step_eff", "hs_step",
+    "hs_e0", "pe_eval",
     "z", "zgrad", "zl", "rl", "gl", "zr", "rr", "gr", "zsub", "gsub", "rsum", "rsum_sub",
     "inv_mass", "mass_sqrt", "wf_mean", "wf_m2", "z_eval", "g_eval",
     "ckpt_r", "ckpt_rsum", "active_idx", "counters", "finished", "part", "part0", "tot",
@@ -104,6 +106,9 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_nuts_init_from": (c_int, [_cfgp, c_vp, c_vp, c_vp]),
     "nmx_nuts_init_check": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_nuts_resume": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_heuristic_begin": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_heuristic_propose": (c_int, [_cfgp, c_vp, c_vp]),
+    "nmx_heuristic_finish": (c_int, [_cfgp, c_vp, c_int, c_vp]),
     "nmx_nuts_run_small": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
     "nmx_predict_logreg": (c_int, [c_vp, ctypes.c_int64, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_predict_normal": (c_int, [c_vp, c_vp, c_int, c_int, ctypes.c_uint64, c_vp, c_vp]),

@@ -205,7 +205,9 @@ def warmup_adapter(num_adapt_steps, find_reasonable_step_size=None, adapt_step_s
 
     def update_fn(t, accept_prob, z_info, state):  # :637-705
         step_size, imm, mm_sqrt, mm_sqrt_inv, ss_state, mm_state, window_idx, rng_key = state
-        rng_key_ss = rng_key
+        # a window-end search draws with the next transition's index (device: the chain's
+        # iteration counter after transition t)
+        rng_key_ss = (rng_key[0], rng_key[1], t + 1) if isinstance(rng_key, tuple) else rng_key
         if adapt_step_size:
             ss_state = ss_update(f(target_accept_prob) - f(accept_prob), ss_state)
             log_step_size, log_step_size_avg = ss_state[0], ss_state[1]
@@ -268,8 +270,10 @@ def velocity_verlet(pe_grad, kinetic_fn=euclidean_kinetic_energy, kinetic_grad_f
 
 def find_reasonable_step_size(pe_grad, kinetic_fn, momentum_generator, init_step_size,
                               inverse_mass_matrix, z_info, rng_key):
-    """hmc_util.py:314-384; `rng_key` is an iterator of momentum keys here."""
-    target_accept_prob = np.log(0.8)
+    """hmc_util.py:314-384; `momentum_generator(z, inverse_mass_matrix, k)` draws the k-th
+    attempt's momentum (the reference passes the inverse mass matrix where
+    momentum_generator expects its square root, hmc_util.py:359; kept)."""
+    target_accept_prob = np.float32(np.log(np.float32(0.8)))  # jnp.log(0.8) in float32
     _, vv_update = velocity_verlet(pe_grad, kinetic_fn)
     z, _, potential_energy, z_grad = z_info
     if potential_energy is None or z_grad is None:
@@ -496,7 +500,7 @@ class NUTSOracle:
                  adapt_step_size=True, adapt_mass_matrix=True, dense_mass=False,
                  target_accept_prob=0.8, max_tree_depth=10, trajectory_length=2 * math.pi,
                  num_steps=None, regularize_mass_matrix=True, max_delta_energy=1000.0,
-                 inverse_mass_matrix=None, dtype=np.float32):
+                 inverse_mass_matrix=None, find_heuristic_step_size=False, dtype=np.float32):
         self.pe_grad, self.dim, self.num_warmup, self.algo = pe_grad, dim, num_warmup, algo
         self.dtype = dtype
         self.max_delta_energy = max_delta_energy
@@ -504,10 +508,24 @@ class NUTSOracle:
                               else (max_tree_depth, max_tree_depth))
         self.trajectory_length = trajectory_length
         self.fixed_num_steps = num_steps
+        frs = None
+        if find_heuristic_step_size:
+            def frs(step_size, inverse_mass_matrix, z_info, rng_key):
+                # rng_key = (seed, chain, transition index): attempt k draws Philox event
+                # EV_HEURISTIC (csrc/nuts.hip k_heur_propose)
+                seed, chain, it = rng_key
+
+                def momentum(z, imm, k):
+                    eps = philox.heuristic_normals(seed, chain, it, k, self.dim).astype(dtype)
+                    return momentum_generator(np.asarray(imm, dtype), eps).astype(dtype)
+
+                return dtype(find_reasonable_step_size(self.pe_grad, euclidean_kinetic_energy, momentum,
+                                                       dtype(step_size), inverse_mass_matrix, z_info, None))
         self.wa_init, self.wa_update = warmup_adapter(
-            num_warmup, adapt_step_size=adapt_step_size, adapt_mass_matrix=adapt_mass_matrix,
-            dense_mass=dense_mass, target_accept_prob=target_accept_prob,
-            regularize_mass_matrix=regularize_mass_matrix, dtype=dtype)
+            num_warmup, find_reasonable_step_size=frs, adapt_step_size=adapt_step_size,
+            adapt_mass_matrix=adapt_mass_matrix, dense_mass=dense_mass,
+            target_accept_prob=target_accept_prob, regularize_mass_matrix=regularize_mass_matrix,
+            dtype=dtype)
         self.step_size = step_size
         self.inverse_mass_matrix = inverse_mass_matrix
         self.vv_init, self.vv_update = velocity_verlet(pe_grad)
@@ -517,7 +535,7 @@ class NUTSOracle:
         f = self.dtype
         z = np.asarray(z, f)
         pe, z_grad = self.pe_grad(z)
-        wa_state = self.wa_init((z, None, pe, z_grad), None, f(self.step_size),
+        wa_state = self.wa_init((z, None, pe, z_grad), (seed, chain, 0), f(self.step_size),
                                 inverse_mass_matrix=self.inverse_mass_matrix,
                                 mass_matrix_size=self.dim)
         return HMCState(0, z, z_grad, pe, None, None, self.trajectory_length, 0, f(0), f(0), False,

@@ -28,6 +28,7 @@ EV_LEAF = 4
 EV_INIT = 5
 EV_ACCEPT = 6
 EV_PREDICT = 7
+EV_HEURISTIC = 8
 
 
 def philox4x32_10(ctr, key):
@@ -94,6 +95,15 @@ def normals(seed, chain, it, dim):
     n2, n3 = box_muller(out[:, 2], out[:, 3])
     eps = np.stack([n0, n1, n2, n3], axis=-1).reshape(-1)[:dim]
     return eps
+
+
+def heuristic_normals(seed, chain, it, attempt, dim):
+    """find_reasonable_step_size momentum noise of one attempt (csrc/nuts.hip k_heur_propose)."""
+    nblk = (dim + 3) // 4
+    out = rng(seed, chain, it, EV_HEURISTIC, np.arange(nblk), attempt)
+    n0, n1 = box_muller(out[:, 0], out[:, 1])
+    n2, n3 = box_muller(out[:, 2], out[:, 3])
+    return np.stack([n0, n1, n2, n3], axis=-1).reshape(-1)[:dim]
 
 
 def uniform(seed, chain, it, event, idx=0, sub=0):

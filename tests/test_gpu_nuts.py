@@ -564,3 +564,40 @@ def test_kernel_init_sample_loop_matches_mcmc_run(device, model, dense):
     kern.sample(st, args, {})
     with pytest.raises(ValueError):
         kern.sample(st, args, {})
+
+
+@pytest.mark.parametrize("model,dim", [("diag_normal", 40), ("logreg", 55), ("diag_normal", 300)])
+def test_find_heuristic_step_size_matches_oracle(device, model, dim):
+    """find_heuristic_step_size=True (hmc.py:320-331): find_reasonable_step_size
+    (hmc_util.py:314-384) at init and at the middle window end of W = 150 ([75-99]).  The
+    oracle's adapter with the same search (same Philox momentum per attempt), fed the device's
+    accept probabilities and draws, must reproduce the device's step size after every
+    transition: the initial search from each chain's initial point, and the window-end search
+    from its draw at t = 99 (rtol 1e-5; the search's result is a power-of-two multiple of its
+    start, so a mismatch would be a whole factor 2)."""
+    seed, C, W = 31, 64, 150
+    rs = np.random.RandomState(dim)
+    args, fm, ref, *_ = _fixed_step_case(model, dim, rs)
+    eng = NUTS(fm, find_heuristic_step_size=True).make_engine(C, args)
+    eng.initialize(seed, W)
+    ss0 = eng.chain_state("step_size").cpu().numpy().copy()
+    z0 = eng.chain_state("z").cpu().numpy().copy()
+    samples, fields, _ = eng.run(W, seed)
+    acc = fields[:, native.COLLECT.index("accept_prob"), :C].cpu().numpy().T
+    ss = fields[:, native.COLLECT.index("step_size"), :C].cpu().numpy().T
+    draws = samples[:, :, :C].cpu().numpy().transpose(2, 0, 1)
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    moved = 0
+    for c in range(C):
+        o = H.NUTSOracle(pe_grad, dim, W, find_heuristic_step_size=True)
+        st = o.init(z0[c], seed, c)
+        np.testing.assert_allclose(ss0[c], st.adapt_state.step_size, rtol=1e-6, err_msg=f"chain {c} initial search")
+        wa = st.adapt_state
+        for t in range(W):
+            z = draws[c, t].astype(np.float32)
+            pe, g = pe_grad(z)
+            wa = o.wa_update(t, np.float32(acc[c, t]), H.IntegratorState(z, None, pe, g), wa)
+            np.testing.assert_allclose(ss[c, t], wa.step_size, rtol=1e-5, err_msg=f"chain {c} after transition {t}")
+        moved += int(ss0[c] != 1.0)
+    assert moved > 0  # the search changed the initial step size of at least some chains
