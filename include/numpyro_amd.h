@@ -308,6 +308,18 @@ int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, con
                      int ldo, void* stream);
 int nmx_unpack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
                        int ldo, const float* pe_in, float* pe_out, void* stream);
+/* Per-chain dense mass matrices (the reference's per-chain adaptation, hmc.py:790-798 vmapped
+ * init_kernel; hmc_util.py:133-239 welford_covariance(diagonal=False)), dim <= 256.
+ * nmx_chain_matvec: out[a][c] = sum_b M[c][b][a] in[b][c] for the listed chains (list/count),
+ * or the chains with phase >= LEAF (list NULL; phase NULL = every chain < num_chains);
+ * M [C][dim][dim] f32: T_c^T row-major gives z = T_c w, T_c row-major gives g_w = T_c^T g_z.
+ * nmx_chain_welford: welford update_fn (:172-196) of every chain with its draw z [dim][ldc],
+ * n = the count after this draw; mean [C][dim], m2 [C][dim][dim] (row a = delta_post[a] *
+ * delta_pre). */
+int nmx_chain_matvec(const float* M, int dim, const float* in, float* out, int ldc, const int32_t* list,
+                     const int32_t* count, const int32_t* phase, int num_chains, void* stream);
+int nmx_chain_welford(const float* z, int dim, int ldc, int num_chains, int n, float* mean, float* m2,
+                      void* stream);
 /* Multivariate normal, U = 0.5 (z-mu)^T P (z-mu), grad = P z - P mu (one nmx_gemm_chains
  * with At = P^T, bias = -P mu) then the per-chain quadratic form: the dense-mass test
  * targets of test/infer/test_mcmc.py:73-100 and :313-343. */

@@ -619,8 +619,12 @@ extern "C" int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const f
                           const nmx_eval_batch* ev, void* stream) {
   if (!ev || !ev->z || !ev->grad || !ev->pe || !mu || !neg_prec_mu)
     return nmx_fail(NMX_ERR_INVALID, "mvn: NULL operand");
-  if (int st = nmx_gemm_chains(prec_t, lda, dim, ev->z, ev->grad, neg_prec_mu, 0, ev->ldc, ev->phase, nullptr,
-                               ev->num_chains, nullptr, stream))
+  // the product selects chains by phase over chain indices; with a compacted list of chain
+  // indices, ev->num_chains bounds the list count, not the indices (a listed chain can sit
+  // anywhere below ldc), so the index range is the whole batch then
+  const int nc = (ev->active_idx && ev->phase) ? ev->ldc : ev->num_chains;
+  if (int st = nmx_gemm_chains(prec_t, lda, dim, ev->z, ev->grad, neg_prec_mu, 0, ev->ldc, ev->phase, nullptr, nc,
+                               nullptr, stream))
     return st;
   hipLaunchKernelGGL(k_quad_pe, dim3(ev->ldc / 64), dim3(256), 0, (hipStream_t)stream, mu, dim, *ev);
   return nmx_check_launch("k_quad_pe");

@@ -241,3 +241,130 @@ class PooledCovariance:
             cov = (n / (n + 5.0)) * cov + 1e-3 * (5.0 / (n + 5.0)) * torch.eye(self.D, dtype=cov.dtype,
                                                                               device=cov.device)
         return cov, mean_y + self.shift
+
+
+# --------------------------------------------------------------------------------------- per chain
+CHAIN_DENSE_MAX_D = 256
+
+
+def chain_dense_bytes(dim, num_chains):
+    """Device bytes of per-chain dense mass state: T^T and T (f32), Welford m2 (f32), the
+    float64 matrices held for HMCAdaptState / re-expression (inverse mass, T)."""
+    return int(num_chains) * int(dim) * int(dim) * (3 * 4 + 2 * 8)
+
+
+class ChainWhitening:
+    """Per-chain z_c = T_c w_c with T_c T_c^T = M_c^-1 (T_c = tril_inv_c^T, hmc_util.py:224-231),
+    every chain its own matrix as in the reference's vmapped adaptation (hmc.py:790-798).
+    Holds T_c^T and T_c row-major for nmx_chain_matvec (forward / backward)."""
+
+    def __init__(self, dim: int, num_chains: int, device):
+        self.D, self.C = int(dim), int(num_chains)
+        self.device = torch.device(device)
+        self.fwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T^T
+        self.bwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T
+        eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
+        self.set(eye.expand(self.C, self.D, self.D))
+
+    def set(self, inverse_mass_matrix, mu=None):
+        """inverse_mass_matrix [C, D, D] or a shared [D, D] / diagonal [D]; mu must be None
+        (per-chain whitening is linear, z = T w)."""
+        imm = torch.as_tensor(inverse_mass_matrix, dtype=torch.float64).to(self.device)
+        if imm.dim() == 1:
+            imm = torch.diag(imm)
+        if imm.dim() == 2:
+            imm = imm.expand(self.C, self.D, self.D)
+        if imm.shape != (self.C, self.D, self.D):
+            raise ValueError(f"inverse_mass_matrix must be [{self.C}, {self.D}, {self.D}]")
+        T = torch.linalg.cholesky(imm.flip(-2, -1)).flip(-2, -1)  # upper, T T^T = imm
+        self.inverse_mass_matrix = imm.contiguous()
+        self.T = T
+        self.fwd.copy_(T.transpose(-1, -2))
+        self.bwd.copy_(T)
+
+    def mass_matrix_sqrt_inv(self):
+        return self.T.transpose(-1, -2)  # tril_inv
+
+    def mass_matrix_sqrt(self):
+        # tril_inv^-1 per chain (hmc_util.py:226-231 cov_inv_sqrt)
+        eye = torch.eye(self.D, dtype=torch.float64, device=self.device).expand(self.C, self.D, self.D)
+        return torch.linalg.solve_triangular(self.T.transpose(-1, -2), eye, upper=False)
+
+    def to_model(self, w, out, phase=None, num_chains=None, stream=0):
+        """out[:, c] = T_c w[:, c] for [D, ldc] buffers (chains < C)."""
+        check(lib().nmx_chain_matvec(ptr(self.fwd), self.D, ptr(w), ptr(out), w.shape[-1], None, None, ptr(phase),
+                                     int(num_chains or self.C), stream), "nmx_chain_matvec")
+
+    def to_whitened(self, z):
+        """w_c = T_c^-1 z_c for z [D, C]."""
+        zc = z.to(torch.float64).t().unsqueeze(-1)  # [C, D, 1]
+        return torch.linalg.solve_triangular(self.T, zc, upper=True).squeeze(-1).t().to(torch.float32)
+
+    def grad_to_model(self, g_w):
+        """g_z = T_c^-T g_w for g_w [D, C]."""
+        gc = g_w.to(torch.float64).t().unsqueeze(-1)
+        return torch.linalg.solve_triangular(self.T.transpose(-1, -2), gc, upper=False).squeeze(-1).t().to(
+            torch.float32)
+
+
+class ChainWhitenedPotential(Potential):
+    """U_w(w) = U(T_c w), grad_w = T_c^T grad U, per chain (nmx_chain_matvec around the model)."""
+
+    def __init__(self, base: Potential):
+        self.base = base
+        self.dim = base.dim
+        self.sites = [(n, s, REAL) for n, s, _ in base.sites]
+        self.whitening = None
+
+    def _bind(self, C, ldc, device):
+        self.base.bind(C, ldc, device)
+        if self.whitening is None or self.whitening.device != device or self.whitening.C != C:
+            self.whitening = ChainWhitening(self.dim, C, device)
+        self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
+        self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
+        self._batches = {}
+
+    def evaluate(self, ev, stream):
+        wt = self.whitening
+        L = lib()
+        key = (ev.active_idx, ev.active_count, ev.pe, ev.phase, ev.num_chains)
+        b = self._batches.get(key)
+        if b is None:
+            b = EvalBatch(z=ptr(self.zb), grad=ptr(self.gb), pe=ev.pe, phase=ev.phase, active_idx=ev.active_idx,
+                          active_count=ev.active_count, num_chains=ev.num_chains, ldc=ev.ldc)
+            self._batches[key] = b
+        b.num_chains = ev.num_chains
+        check(L.nmx_chain_matvec(ptr(wt.fwd), self.dim, ev.z, ptr(self.zb), ev.ldc, ev.active_idx, ev.active_count,
+                                 ev.phase, ev.num_chains, stream), "nmx_chain_matvec")
+        self.base.evaluate(b, stream)
+        check(L.nmx_chain_matvec(ptr(wt.bwd), self.dim, ptr(self.gb), ev.grad, ev.ldc, ev.active_idx,
+                                 ev.active_count, ev.phase, ev.num_chains, stream), "nmx_chain_matvec")
+
+
+class ChainWelford:
+    """welford_covariance(diagonal=False) of every chain (hmc_util.py:133-239), f32 on the
+    device (nmx_chain_welford); final_fn per chain with the reference's regulariser."""
+
+    def __init__(self, dim, num_chains, device):
+        self.D, self.C = int(dim), int(num_chains)
+        self.mean = torch.zeros(self.C, self.D, dtype=torch.float32, device=device)
+        self.m2 = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=device)
+        self.n = 0
+
+    def add(self, z, stream=0):
+        """z: [D, ldc] model-space draws of every chain."""
+        self.n += 1
+        check(lib().nmx_chain_welford(ptr(z), self.D, z.shape[-1], self.C, self.n, ptr(self.mean), ptr(self.m2),
+                                      stream), "nmx_chain_welford")
+
+    def finalize(self, regularize=True):
+        """final_fn (hmc_util.py:198-237) per chain: cov [C, D, D] float64."""
+        n = self.n
+        if n < 2:
+            raise RuntimeError("dense adaptation needs at least 2 draws per window")
+        cov = self.m2.to(torch.float64) / (n - 1)
+        if regularize:
+            cov = (n / (n + 5.0)) * cov + 1e-3 * (5.0 / (n + 5.0)) * torch.eye(self.D, dtype=cov.dtype,
+                                                                              device=cov.device)
+        # jnp.linalg.cholesky symmetrizes its input (symmetrize_input=True)
+        return 0.5 * (cov + cov.transpose(-1, -2))

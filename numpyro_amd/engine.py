@@ -67,6 +67,8 @@ class SamplerOptions:
     inverse_mass_matrix: object = None  # diag [D] or None
     # dense pooled adaptation: bytes of window draws buffered per chunk
     dense_adapt_bytes: int = 4 << 30
+    # per-chain dense mass: device bytes allowed for the matrices (dense.chain_dense_bytes)
+    chain_dense_bytes: int = 64 << 30
     find_heuristic_step_size: bool = False
 
 
@@ -81,7 +83,20 @@ class Engine:
                  chain_offset: int = 0, sync_chains: bool = False):
         self.dense = bool(opts.dense_mass)
         self.model_potential = potential
-        if self.dense:
+        # dense mass: per-chain matrices (the reference's semantics) when they are adapted and
+        # fit, one pooled matrix when asked for ("pooled"), one shared whitening when the
+        # matrix is given and not adapted (every chain holds the same one: same semantics)
+        self.chain_dense = self.dense and opts.dense_mass != "pooled" and bool(opts.adapt_mass_matrix)
+        if self.chain_dense:
+            from .dense import CHAIN_DENSE_MAX_D, ChainWhitenedPotential, chain_dense_bytes
+            need = chain_dense_bytes(potential.dim, num_chains)
+            if potential.dim > CHAIN_DENSE_MAX_D or need > opts.chain_dense_bytes:
+                raise ValueError(
+                    f"per-chain dense mass matrices for {num_chains} chains of dimension {potential.dim} need "
+                    f"{need / 2**30:.1f} GiB (limit {opts.chain_dense_bytes / 2**30:.0f} GiB, dim <= "
+                    f"{CHAIN_DENSE_MAX_D}); use dense_mass='pooled' for one matrix adapted over all chains")
+            potential = ChainWhitenedPotential(potential)
+        elif self.dense:
             from .dense import WhitenedPotential
             potential = WhitenedPotential(potential)
         self.potential = potential
@@ -189,7 +204,8 @@ class Engine:
         imm_t = None
         if self.dense:
             # chains are initialised in model coordinates (w = z), then re-expressed
-            self.potential.whitening.set(torch.eye(self.D, dtype=torch.float64), torch.zeros(self.D))
+            self.potential.whitening.set(torch.eye(self.D, dtype=torch.float64),
+                                         None if self.chain_dense else torch.zeros(self.D))
         elif imm is not None:
             imm_t = torch.as_tensor(imm, dtype=torch.float32, device=self.device).reshape(-1)
             if imm_t.numel() != self.D:
@@ -372,7 +388,7 @@ class Engine:
         transition's draws (model space) join the window's pool, which persists across run()
         calls (a kernel stepped one transition at a time pools the same draws), and the window's
         last transition finalizes it and re-expresses every chain."""
-        from .dense import PooledCovariance
+        from .dense import ChainWelford, PooledCovariance
         chunk = max(1, int(self.opts.dense_adapt_bytes) // (4 * self.D * self.ldc))
         wt = self.potential.whitening
         pos = self.model_potential.transform_codes().to(torch.bool)
@@ -384,7 +400,8 @@ class Engine:
                 self._convert_slots(samples, self._slots_in(a, b, cstart, thinning, S), s)
                 continue
             if self._pool is None or self._pool[0] != win:
-                self._pool = (win, PooledCovariance(self.D, self.device, wt.mu))
+                self._pool = (win, ChainWelford(self.D, self.C, self.device) if self.chain_dense
+                              else PooledCovariance(self.D, self.device, wt.mu))
             pool = self._pool[1]
             zbuf = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
             for ca in range(a, b, chunk):
@@ -395,7 +412,10 @@ class Engine:
                 launches += self._run_segment(ca, cb, seed, ca, 1, n, abuf, afld, poll_every, s, max_launches)
                 for k in range(n):
                     wt.to_model(abuf[k], zbuf, stream=s)
-                    pool.add(zbuf[:, :self.C])
+                    if self.chain_dense:
+                        pool.add(zbuf, stream=s)
+                    else:
+                        pool.add(zbuf[:, :self.C])
                     slot = self._slot_of(ca + k, cstart, thinning, S)
                     if slot >= 0:
                         samples[slot].copy_(zbuf)
@@ -404,8 +424,11 @@ class Engine:
                         fields[slot].copy_(afld[k])
                 del abuf, afld
             if b == win[1]:
-                pool.all_reduce()
-                cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
+                if self.chain_dense:
+                    cov, mean = pool.finalize(self.opts.regularize_mass_matrix), None
+                else:
+                    pool.all_reduce()
+                    cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
                 self._pool = None
                 self._reexpress(cov, mean, s)
         return launches
@@ -502,7 +525,8 @@ class Engine:
 
     def mass_state(self):
         """(inverse_mass_matrix, mass_matrix_sqrt, mass_matrix_sqrt_inv) as HMCAdaptState holds
-        them: per-chain diagonals [C, D], or the pooled dense matrices [D, D]."""
+        them: per-chain diagonals [C, D], per-chain dense matrices [C, D, D], or the pooled /
+        shared dense matrices [D, D]."""
         if self.dense:
             wt = self.potential.whitening
             return (wt.inverse_mass_matrix.to(torch.float32).clone(), wt.mass_matrix_sqrt().to(torch.float32),
@@ -514,7 +538,7 @@ class Engine:
         if not self.dense:
             return None
         wt = self.potential.whitening
-        return (wt.inverse_mass_matrix.clone(), wt.mu.clone())
+        return (wt.inverse_mass_matrix.clone(), None if self.chain_dense else wt.mu.clone())
 
     def set_whitening_state(self, st):
         if st is not None:

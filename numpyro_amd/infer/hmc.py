@@ -140,6 +140,11 @@ class HMC(MCMCKernel):
         if find_heuristic_step_size and dense_mass:
             raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
                                       "coordinates, the dense engine in whitened ones")
+        if isinstance(dense_mass, str):
+            if dense_mass != "pooled":
+                raise ValueError("dense_mass must be a bool, 'pooled' or a list of site groups")
+            warnings.warn("dense_mass='pooled': one dense mass matrix is adapted from the draws of all chains "
+                          "(not per chain as in numpyro); chains share it", stacklevel=2)
         if isinstance(dense_mass, (list, tuple)) and len(dense_mass) > 0:
             raise NotImplementedError("structured dense_mass (list of site groups) is not supported; "
                                       "use dense_mass=True for a full dense mass matrix")
@@ -186,7 +191,8 @@ class HMC(MCMCKernel):
         md = tuple(md) if isinstance(md, (tuple, list)) else (int(md), int(md))
         return SamplerOptions(
             algo=self._algo, step_size=self._step_size, adapt_step_size=self._adapt_step_size,
-            adapt_mass_matrix=self._adapt_mass_matrix, dense_mass=bool(self._dense_mass),
+            adapt_mass_matrix=self._adapt_mass_matrix,
+            dense_mass=self._dense_mass if self._dense_mass == "pooled" else bool(self._dense_mass),
             target_accept_prob=self._target_accept_prob, max_tree_depth=md,
             trajectory_length=self._trajectory_length, num_steps=self._num_steps,
             regularize_mass_matrix=self._regularize_mass_matrix,

@@ -157,7 +157,7 @@ def main():
         run_model("funnel", P.funnel, (D,), a.chains or 4096, a.warmup, a.steps,
                   flops_per_leapfrog=2.0 * D * D if a.dense else None,
                   bytes_per_leapfrog=None if a.dense else 2 * D * 4,
-                  dense_mass=bool(a.dense), max_tree_depth=a.max_tree_depth)
+                  dense_mass="pooled" if a.dense else False, max_tree_depth=a.max_tree_depth)
     elif a.what == "sv":
         r = datasets.sp500_synthetic()
         D = r.size + 2
@@ -170,7 +170,7 @@ def main():
         model_flops = 6.0 * 100 * H * H + 6.0 * 100 * 3 * H
         run_model("bnn", P.bnn, (X, Y, H), a.chains or 2048, a.warmup, a.steps,
                   flops_per_leapfrog=(2.0 * D * D if a.dense else 0.0) + model_flops,
-                  dense_mass=bool(a.dense), max_tree_depth=a.max_tree_depth)
+                  dense_mass="pooled" if a.dense else False, max_tree_depth=a.max_tree_depth)
     elif a.what == "covtype":
         X, y = datasets.covtype_synthetic(seed=0)
         dev = torch.device("cuda:0")

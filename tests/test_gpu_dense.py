@@ -165,6 +165,36 @@ def test_mvn_potential_matches_oracle(device, D):
         np.testing.assert_allclose(pe[c], pr, rtol=1e-4, atol=1e-4)
 
 
+def test_mvn_potential_compacted_list_high_indices(device):
+    """A compacted list whose count bound (num_chains = C - finished, as in a run's tail) is
+    below the listed chains' indices: every listed chain is still evaluated."""
+    D, C, ldc = 7, 200, 256
+    cov = _corr_cov(D, 4) + 0.1 * np.eye(D)
+    pot = P.MultivariateNormal(np.zeros(D), cov)
+    pot.bind(C, ldc, device)
+    rs = np.random.RandomState(2)
+    Z = rs.randn(C, D).astype(np.float32)
+    z = torch.zeros(D, ldc, device=device)
+    z[:, :C] = torch.from_numpy(Z.T.copy()).to(device)
+    g = torch.full((D, ldc), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    chosen = np.array([199, 180, 150, 3], np.int32)
+    ph = torch.zeros(ldc, dtype=torch.int32, device=device)
+    ph[torch.from_numpy(chosen.astype(np.int64)).to(device)] = native.PH_LEAF
+    idx = torch.zeros(ldc, dtype=torch.int32, device=device)
+    idx[:4] = torch.from_numpy(chosen).to(device)
+    cnt = torch.tensor([4], dtype=torch.int32, device=device)
+    ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), phase=native.ptr(ph),
+                          active_idx=native.ptr(idx), active_count=native.ptr(cnt), num_chains=8, ldc=ldc)
+    pot.evaluate(ev, native.stream_ptr())
+    torch.cuda.synchronize()
+    ref = OP.MVN(np.linalg.inv(cov))
+    for c in chosen:
+        pr, gr = ref.pe_grad(Z[c].astype(np.float64))
+        np.testing.assert_allclose(pe[c].item(), pr, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(g[:, c].cpu().numpy(), gr, rtol=1e-4, atol=1e-4)
+
+
 def test_whitened_potential_matches_oracle(device):
     D = 12
     cov = _corr_cov(D, 3) + 0.05 * np.eye(D)
@@ -246,17 +276,30 @@ def test_dense_fixed_mass_matches_oracle(device, algo, model):
     np.testing.assert_allclose(msq @ msq.T, np.linalg.inv(imm), rtol=1e-3, atol=1e-3)
 
 
+def _kernel(cls, *args, dense_mass, **kw):
+    if dense_mass == "pooled":
+        with pytest.warns(UserWarning, match="pooled"):
+            return cls(*args, dense_mass=dense_mass, **kw)
+    return cls(*args, dense_mass=dense_mass, **kw)
+
+
+@pytest.mark.parametrize("mode", [True, "pooled"])
 @pytest.mark.parametrize("kernel_cls", [NUTS, HMC])
 @pytest.mark.parametrize("rho", [-0.7, 0.8])
-def test_dense_mass_pooled_adaptation(device, kernel_cls, rho):
+def test_dense_mass_adaptation(device, kernel_cls, rho, mode):
     """test/infer/test_mcmc.py:313-343 (2-d MVN, trajectory_length=2): the adapted dense
-    mass recovers the target covariance (rtol 0.10) and the sample moments match."""
+    mass recovers the target covariance (rtol 0.10; per-chain matrices: their mean) and the
+    sample moments match.  dense_mass=True adapts one matrix per chain (the reference's
+    semantics), 'pooled' one matrix from every chain's draws."""
     true_cov = np.array([[10.0, rho], [rho, 0.1]])
-    kernel = kernel_cls(P.multivariate_normal, trajectory_length=2.0, dense_mass=True)
+    kernel = _kernel(kernel_cls, P.multivariate_normal, trajectory_length=2.0, dense_mass=mode)
     mcmc = MCMC(kernel, num_warmup=1000, num_samples=1000, num_chains=64, progress_bar=False)
     mcmc.run(0, None, true_cov)
     msq = mcmc.last_state.adapt_state.mass_matrix_sqrt.cpu().numpy().astype(np.float64)
-    est_cov = np.linalg.inv(msq @ msq.T)
+    assert msq.shape == ((64, 2, 2) if mode is True else (2, 2))
+    est_cov = np.linalg.inv(msq @ np.swapaxes(msq, -1, -2))
+    if mode is True:
+        est_cov = est_cov.mean(0)
     np.testing.assert_allclose(est_cov, true_cov, rtol=0.10)
     x = mcmc.get_samples()["x"].cpu().numpy().astype(np.float64)
     np.testing.assert_allclose(x[:, 0].mean(), 0.0, atol=0.50)
@@ -265,12 +308,13 @@ def test_dense_mass_pooled_adaptation(device, kernel_cls, rho):
     np.testing.assert_allclose(x.var(0), [10.0, 0.1], rtol=0.20)
 
 
+@pytest.mark.parametrize("mode", [True, "pooled"])
 @pytest.mark.parametrize("regularize", [True, False])
-def test_correlated_mvn(device, regularize):
+def test_correlated_mvn(device, regularize, mode):
     """test/infer/test_mcmc.py:75-100 (D = 5, dense NUTS from zeros)."""
     D = 5
     true_cov = _corr_cov(D, 0)
-    kernel = NUTS(P.multivariate_normal, dense_mass=True, regularize_mass_matrix=regularize)
+    kernel = _kernel(NUTS, P.multivariate_normal, dense_mass=mode, regularize_mass_matrix=regularize)
     C = 64
     mcmc = MCMC(kernel, num_warmup=1000, num_samples=1000, num_chains=C, progress_bar=False)
     mcmc.run(0, None, None, np.linalg.inv(true_cov), init_params=torch.zeros(C, D))
@@ -279,9 +323,11 @@ def test_correlated_mvn(device, regularize):
     assert np.sum(np.abs(np.cov(x.T) - true_cov)) / D ** 2 < 0.02
 
 
-def test_dense_resume_from_post_warmup_state(device):
+@pytest.mark.parametrize("mode", [True, "pooled"])
+def test_dense_resume_from_post_warmup_state(device, mode):
     cov = _corr_cov(4, 5) + 0.1 * np.eye(4)
-    mcmc = MCMC(NUTS(P.multivariate_normal, dense_mass=True), num_warmup=200, num_samples=50, num_chains=64)
+    mcmc = MCMC(_kernel(NUTS, P.multivariate_normal, dense_mass=mode), num_warmup=200, num_samples=50,
+                num_chains=64)
     mcmc.warmup(1, None, cov)
     st = mcmc.post_warmup_state
     mcmc.run(2, None, cov)
@@ -289,7 +335,7 @@ def test_dense_resume_from_post_warmup_state(device):
     mcmc.post_warmup_state = st
     mcmc.run(2, None, cov)
     np.testing.assert_array_equal(a, mcmc.get_samples()["x"].cpu().numpy())
-    assert st.adapt_state.inverse_mass_matrix.shape == (4, 4)
+    assert st.adapt_state.inverse_mass_matrix.shape == ((64, 4, 4) if mode is True else (4, 4))
 
 
 def test_whitening_roundtrip(device):
@@ -353,7 +399,7 @@ def test_funnel_10k_dense_nuts_runs(device):
     one potential evaluation (the whitened potential's listed-chain count) and the draws are
     finite."""
     C = 256
-    mcmc = MCMC(NUTS(P.funnel, dense_mass=True, max_tree_depth=8), num_warmup=20, num_samples=2,
+    mcmc = MCMC(_kernel(NUTS, P.funnel, dense_mass="pooled", max_tree_depth=8), num_warmup=20, num_samples=2,
                 num_chains=C)
     mcmc.warmup(0, 10000)
     eng = mcmc._engine
@@ -380,3 +426,117 @@ def test_funnel_10k_dense_nuts_runs(device):
     imm = mcmc.post_warmup_state.adapt_state.inverse_mass_matrix
     assert imm.shape == (10000, 10000) and torch.isfinite(imm).all()
     assert not torch.equal(imm.cpu(), torch.eye(10000, dtype=imm.dtype))  # the window update happened
+
+
+def test_per_chain_dense_needs_pooled_when_too_large(device):
+    """Per-chain dense matrices at D = 10000 (C2) do not fit: the error names dense_mass='pooled'."""
+    mcmc = MCMC(NUTS(P.funnel, dense_mass=True), num_warmup=10, num_samples=1, num_chains=64)
+    with pytest.raises(ValueError, match="pooled"):
+        mcmc.run(0, 10000)
+
+
+@pytest.mark.parametrize("D,C", [(3, 64), (55, 130), (256, 70)])
+def test_chain_matvec_matches_fp64(device, D, C):
+    """nmx_chain_matvec: out[a][c] = sum_b M[c][b][a] in[b][c] for listed chains (others
+    untouched) and for the phase-selected dense batch; f32 fma-chain error bound."""
+    lib = native.lib()
+    rs = np.random.RandomState(D)
+    ldc = (C + 63) // 64 * 64
+    M = rs.randn(C, D, D).astype(np.float32)
+    x = rs.randn(D, ldc).astype(np.float32)
+    dM, dx = torch.from_numpy(M).to(device), torch.from_numpy(x).to(device)
+    ref = np.einsum("cba,bc->ac", M.astype(np.float64), x[:, :C].astype(np.float64))
+    bound = 1e-6 * np.einsum("cba,bc->ac", np.abs(M).astype(np.float64), np.abs(x[:, :C]).astype(np.float64)) + 1e-6
+    chosen = np.sort(rs.choice(C, C // 3, replace=False)).astype(np.int32)[::-1].copy()
+    idx = torch.zeros(ldc, dtype=torch.int32, device=device)
+    idx[:len(chosen)] = torch.from_numpy(chosen).to(device)
+    cnt = torch.tensor([len(chosen)], dtype=torch.int32, device=device)
+    out = torch.full((D, ldc), float("nan"), device=device)
+    native.check(lib.nmx_chain_matvec(native.ptr(dM), D, native.ptr(dx), native.ptr(out), ldc, native.ptr(idx),
+                                      native.ptr(cnt), None, C, native.stream_ptr()))
+    o = out.cpu().numpy().astype(np.float64)
+    assert np.all(np.abs(o[:, chosen] - ref[:, chosen]) <= bound[:, chosen])
+    others = np.setdiff1d(np.arange(ldc), chosen)
+    assert np.all(np.isnan(o[:, others]))
+    phase = torch.full((ldc,), native.PH_DONE, dtype=torch.int32, device=device)
+    phase[:C:2] = native.PH_LEAF
+    out.fill_(float("nan"))
+    native.check(lib.nmx_chain_matvec(native.ptr(dM), D, native.ptr(dx), native.ptr(out), ldc, None, None,
+                                      native.ptr(phase), C, native.stream_ptr()))
+    o = out.cpu().numpy().astype(np.float64)
+    assert np.all(np.abs(o[:, :C:2] - ref[:, ::2]) <= bound[:, ::2]) and np.all(np.isnan(o[:, 1:C:2]))
+
+
+@pytest.mark.parametrize("model", ["mvn", "logreg"])
+def test_per_chain_dense_adaptation_matches_oracle(device, model):
+    """Per-chain dense adaptation (hmc.py:790-798: each chain its own welford_covariance
+    (diagonal=False), hmc_util.py:133-239) over W = 150 (one middle window, [75-99]):
+    (1) teacher-forced -- the oracle's dense Welford + final_fn fed each chain's device draws of
+    the window reproduces the chain's adapted inverse mass matrix (rtol 1e-4: the same f32
+    updates; the device's Cholesky is float64); (2) from each chain's post-warmup state the
+    oracle's dense-mass NUTS (mass_matrix_sqrt @ eps momentum, M^-1 r in the leapfrog and the
+    U-turn dots, hmc_util.py:1183-1220) takes the device's next three trees and draws (>= 95%
+    of chains, every mismatch at a rounding-level decision tie)."""
+    from test_gpu_nuts import _explain_mismatches, _first_split, _tie_score
+
+    seed, C, W, D = 17, 64, 150, 6
+    rs = np.random.RandomState(3)
+    if model == "mvn":
+        cov = _corr_cov(D, 21) + 0.1 * np.eye(D)
+        args, fm, site = (None, cov), P.multivariate_normal, "x"
+        ref = OP.MVN(np.linalg.inv(cov))
+    else:
+        X = rs.randn(500, D).astype(np.float32)
+        X[:, 1] = X[:, 0] + 0.3 * X[:, 1]  # correlated posterior
+        beta = rs.randn(D) * 0.3
+        y = (rs.rand(500) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
+        args, fm, site = (X, y), P.logistic_regression, "coefs"
+        ref = OP.LogisticRegression(X, y, dtype=np.float32)
+    mcmc = MCMC(NUTS(fm, dense_mass=True), num_warmup=W, num_samples=3, num_chains=C)
+    mcmc.warmup(seed, *args, collect_warmup=True)
+    draws = mcmc.get_samples(group_by_chain=True)[site].cpu().numpy().reshape(C, W, D)
+    st = mcmc.post_warmup_state
+    imm = st.adapt_state.inverse_mass_matrix.cpu().numpy().astype(np.float64)
+    assert imm.shape == (C, D, D)
+    _, upd, fin = H.welford_covariance(diagonal=False)
+    for c in range(C):
+        wst = (np.zeros(D, np.float32), np.zeros((D, D), np.float32), 0)
+        for t in range(75, 100):
+            wst = upd(draws[c, t], wst)
+        cov_o = fin(wst, regularize=True)[0]
+        np.testing.assert_allclose(imm[c], cov_o, rtol=1e-4, atol=1e-7, err_msg=f"chain {c}")
+    # (2) sampling transitions from the post-warmup state
+    mcmc.run(seed, *args, extra_fields=("num_steps",))
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
+    zs = mcmc.get_samples(True)[site].cpu().numpy()
+    z0 = st.z[site].cpu().numpy()
+    g0 = st.z_grad.cpu().numpy()
+    pe0 = st.potential_energy.cpu().numpy()
+    ss = st.adapt_state.step_size.cpu().numpy()
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    match, mism = 0, []
+    for c in range(C):
+        o = H.NUTSOracle(pe_grad, D, W, step_size=float(ss[c]), adapt_step_size=False, adapt_mass_matrix=False,
+                         dense_mass=True, inverse_mass_matrix=imm[c].astype(np.float32))
+        wa = o.wa_init((z0[c],), None, np.float32(ss[c]), inverse_mass_matrix=imm[c].astype(np.float32),
+                       mass_matrix_size=D)
+        s = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
+                       0, np.float32(0), np.float32(0), False, wa, (seed, c))
+        ok, margins = [], []
+        for t in range(3):
+            H.DECISIONS = []
+            try:
+                s = o.sample(s)
+            finally:
+                d, H.DECISIONS = H.DECISIONS, None
+            margins.append(min(d, key=_tie_score) if d else ("none", np.inf))
+            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
+        t = _first_split(ok)
+        if t < 0:
+            match += 1
+        else:
+            mism.append((c, t, margins[t]))
+    print(f"[per-chain dense {model}] {match}/{C} chains reproduce the oracle's dense-mass transitions")
+    _explain_mismatches(mism, f"per-chain dense {model}")
+    assert match >= int(0.95 * C)

@@ -511,7 +511,8 @@ def test_funnel_reparam_non_centered(device, capsys):
 @pytest.mark.parametrize("dense", [False, True])
 def test_bnn_fits_data(device, dense):
     """examples/bnn.py (small H): the posterior-mean network fits the training data and
-    prec_obs is of the order of the noise level (Y is standardized, sigma_obs 0.05 before)."""
+    prec_obs is of the order of the noise level (Y is standardized, sigma_obs 0.05 before).
+    dense=True: per-chain dense matrices (D = 61)."""
     X, Y = datasets.bnn_data(N=60, D_X=3)
     H = 6
     mcmc = MCMC(NUTS(P.bnn, dense_mass=dense), num_warmup=300, num_samples=100, num_chains=64)
