@@ -160,7 +160,8 @@ __global__ void k_logreg_pack_x3(const float* __restrict__ X, const float* __res
       v[j] = (row < n && d < D) ? X[row * D + d] : 0.0f;
     }
   } else {
-    // labels as floats: lane L < 8 holds y[h = L/4][i = 4 (L%4) .. +3] (bytes 16 L .. 16 L + 15)
+    // labels as y - 1/2 (x3_epi_pair): lane L < 8 holds row labels [h = L/4][i = 4 (L%4) .. +3]
+    // (bytes 16 L .. 16 L + 15); padded rows 0 (their X is zero)
     float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (lane < 8) {
       const int hh = lane >> 2;
@@ -168,7 +169,7 @@ __global__ void k_logreg_pack_x3(const float* __restrict__ X, const float* __res
       for (int k = 0; k < 4; ++k) {
         const int ii = 4 * (lane & 3) + k;
         const int64_t row = r0 + (ii & 3) + 8 * (ii >> 2) + 4 * hh;
-        f[k] = row < n ? y[row] : 0.0f;
+        f[k] = row < n ? y[row] - 0.5f : 0.0f;
       }
     }
     float4* o = reinterpret_cast<float4*>(out + i);
@@ -226,29 +227,55 @@ __device__ __forceinline__ void x3_labels_wait(f32x4 (&y4)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y4[0]), "+v"(y4[1]), "+v"(y4[2]), "+v"(y4[3]));
 }
 
-// Bernoulli-logits epilogue (epilogue_abs arithmetic; no row mask: padded rows have l = 0):
-// acc -> sigmoid(l) - y, U terms into pe
-// The accumulator holds m = -l log2(e) (Z pre-scaled by -log2 e before its split), so
-// e = 2^-|m| needs no multiply and sum |l| = ln 2 sum |m|
-__device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&y4)[4], float (&res)[16], double& pe) {
-  float lin = 0.0f, prod = 1.0f;
+// Bernoulli-logits epilogue on the GEMM1 accumulator, rows 2p and 2p+1 (no row mask: padded
+// rows have l = 0 and zero X).  The accumulator holds m = -l log2(e) (Z pre-scaled by -log2 e
+// before its split), so e = 2^-|m| needs no multiply and sum |l| = ln 2 sum |m|.
+//   U terms:   |l|/2 + log1p(e)   (the linear part (1/2 - y) l is the per-chain w . b of the
+//              finalize), log1p summed as log of the product of the factors 1 + e
+//   residual:  R' = y - sigmoid(l) = (y - 1/2) + copysign(1/(1+e) - 1/2, m)
+//              (sigmoid(l) - 1/2 = copysign(1/(1+e) - 1/2, l), sign(l) = -sign(m)); GEMM2
+//              accumulates X^T R' = -X^T (sigmoid(l) - y) and the finalize subtracts it.
+// Labels come as y - 1/2.  Per value: exp and rcp, 1/2 of a packed add (1 + e), 1/2 packed
+// mul (product), 1/2 packed add (- 1/2), one bitfield insert (copysign), 1/2 packed add
+// (+ label), one add (|m|): the even and odd rows keep separate products (each <= 2^8).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void x3_epi_pair(const f32x16& acc, const f32x4 (&yh4)[4], int p, float (&res)[16],
+                                            float& lin, f32x2& prod) {
+  const int r0 = 2 * p, r1 = 2 * p + 1;
+  const float m0 = acc[r0], m1 = acc[r1];
+  f32x2 e;
+  e.x = __builtin_amdgcn_exp2f(-fabsf(m0));
+  e.y = __builtin_amdgcn_exp2f(-fabsf(m1));
+  const f32x2 ope = e + 1.0f;
+  prod = prod * ope;
+  f32x2 inv;
+  inv.x = __builtin_amdgcn_rcpf(ope.x);
+  inv.y = __builtin_amdgcn_rcpf(ope.y);
+  const f32x2 hh = inv - 0.5f;
+  constexpr unsigned SB = 0x80000000u;
+  f32x2 sg;
+  sg.x = __uint_as_float((__float_as_uint(m0) & SB) | (__float_as_uint(hh.x) & ~SB));
+  sg.y = __uint_as_float((__float_as_uint(m1) & SB) | (__float_as_uint(hh.y) & ~SB));
+  f32x2 yh;
+  yh.x = yh4[r0 >> 2][r0 & 3];
+  yh.y = yh4[r1 >> 2][r1 & 3];
+  const f32x2 rr = sg + yh;
+  res[r0] = rr.x;
+  res[r1] = rr.y;
+  lin += fabsf(m0);
+  lin += fabsf(m1);
+}
+
+__device__ __forceinline__ void x3_epi_finish(float lin, f32x2 prod, double& pe) {
+  pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod.x * prod.y) * (double)LN2;
+}
+
+__device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&yh4)[4], float (&res)[16], double& pe) {
+  float lin = 0.0f;
+  f32x2 prod = {1.0f, 1.0f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int r = 4 * q + u;
-      const float l = acc[r];
-      const float al = fabsf(l);
-      const float e = __builtin_amdgcn_exp2f(-al);
-      const float ope = 1.0f + e;
-      const float inv = __builtin_amdgcn_rcpf(ope);
-      const float num = l <= 0.0f ? 1.0f : e;
-      res[r] = __builtin_fmaf(num, inv, -y4[q][u]);
-      lin += al;
-      prod *= ope;
-    }
-  }
-  pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+  for (int p = 0; p < 8; ++p) x3_epi_pair(acc, yh4, p, res, lin, prod);
+  x3_epi_finish(lin, prod, pe);
 }
 
 // GEMM2 of one tile: G += X^T . R, R split into three bf16 terms (k-step s = registers 8s..8s+7)
@@ -361,16 +388,18 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
       asm volatile("s_barrier" ::: "memory");  // A(0) is in
       if (nt > 1) issue_a(1);
       issue_b(0);
-      f32x16 acc;
-      if (active) acc = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
-      for (int k = 0; k < nt; ++k) {
+      f32x16 accA, accB;
+      if (active) accA = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      // one tile: epilogue + GEMM2 of tile k on `acc`, GEMM1 of tile k+1 into `nxt`; the loop
+      // below alternates the two accumulators (no register copy between tiles)
+      auto step = [&](int k, const f32x16& acc, f32x16& nxt) {
         // A(k+1) and B(k) have landed in every wave; A slot k&1 (GEMM1(k)) and B slot
         // (k+1)&1 (GEMM2(k-1)) were last read in iteration k-1
         x3_wait_vm<0>();
         asm volatile("s_barrier" ::: "memory");
         if (k + 2 < nt) issue_a(k + 2);
         if (k + 1 < nt) issue_b(k + 1);
-        if (!active) continue;
+        if (!active) return;
         const char* bs = bring + (k & 1) * NBP * 1024;
         f32x4 y4[4];
         x3_labels(bs + (NBP - 1) * 1024, h, y4);
@@ -379,26 +408,15 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         // the epilogue of tile k
         const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) & 1) * NA * 1024) + lane;
         float res[16];
-        f32x16 nxt;
-        if constexpr (SCHED && KB == 4) {
-          // Hand-interleaved (in-order issue within a wave): each GEMM1(k+1) MFMA is followed
-          // by one row's epilogue of tile k, which fills the MFMA's dependency stall; the first
-          // split half then rides on the last k-block.  sched_barrier(0) pins the order; the
-          // operations and their per-value order equal x3_gemm1 / x3_epilogue / x3_gemm2.
+        if constexpr (SCHED == 6 && KB == 4) {
+          // Hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with
+          // row pairs of tile k's epilogue, which fill the MFMAs' dependency stalls.
+          // sched_barrier(0) pins the order; the operations and their per-value order equal
+          // x3_gemm1 / x3_epilogue (bitwise equal results).
 #pragma unroll
           for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
-          float lin = 0.0f, prod = 1.0f;
-          auto epi1 = [&](int r) {  // x3_epilogue's row r
-            const float l = acc[r];
-            const float al = fabsf(l);
-            const float e = __builtin_amdgcn_exp2f(-al);
-            const float ope = 1.0f + e;
-            const float inv = __builtin_amdgcn_rcpf(ope);
-            const float num = l <= 0.0f ? 1.0f : e;
-            res[r] = __builtin_fmaf(num, inv, -y4[r >> 2][r & 3]);
-            lin += al;
-            prod *= ope;
-          };
+          float lin = 0.0f;
+          f32x2 prod = {1.0f, 1.0f};
           bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
 #pragma unroll
           for (int kb = 0; kb < KB; ++kb) {
@@ -409,16 +427,14 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
               n3 = fa[(2 * KB + kb + 1) * 64];
             }
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
-            epi1(4 * kb + 0);
+            x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
             __builtin_amdgcn_sched_barrier(0);
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
-            epi1(4 * kb + 1);
             __builtin_amdgcn_sched_barrier(0);
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
-            epi1(4 * kb + 2);
+            x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
             __builtin_amdgcn_sched_barrier(0);
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
-            epi1(4 * kb + 3);
             __builtin_amdgcn_sched_barrier(0);
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
@@ -430,13 +446,33 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
               a3 = n3;
             }
           }
-          pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod) * (double)LN2;
+          x3_epi_finish(lin, prod, pe);
         } else {
           nxt = x3_gemm1<KB>(fa, z1, z2, z3);
           x3_epilogue(acc, y4, res, pe);
         }
         x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
-        acc = nxt;
+        if constexpr (SCHED == 0) {
+          // scheduling hints (LLVM igrouplp): each GEMM1(k+1) MFMA followed by 5 VALU (tile k's
+          // epilogue and the first split half), each GEMM2(k) MFMA by 3 (the second split half),
+          // so one wave's MFMA dependency stalls are filled with its own vector work.  Measured
+          // (scripts/ab_logreg.py, C = 4096 all active): 2.74 vs 2.85 ms without the hints; 4-7
+          // and 1-3 VALU per group all within 1.5%.
+#pragma unroll
+          for (int i = 0; i < 6 * KB; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU
+          }
+#pragma unroll
+          for (int i = 0; i < 12 * DT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+          }
+        }
+      };
+      for (int k = 0; k < nt; k += 2) {
+        step(k, accA, accB);
+        if (k + 1 < nt) step(k + 1, accB, accA);
       }
     }
   }
@@ -514,7 +550,7 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
 #pragma unroll
     for (int i = 0; i < FIN_WAVES; ++i) s += (float)part[i][lane];
     const size_t idx = (size_t)d * ldc + c;
-    ev.grad[idx] = s + ev.z[idx];
+    ev.grad[idx] = ev.z[idx] - s;  // the partials hold X^T (y - sigmoid(l)) (x3_epi_pair)
   } else {
     double s = 0.0;
 #pragma unroll
