@@ -4,11 +4,17 @@
 // z = (log prec_obs, w1, w2, w3) row-major (ravel_pytree of the sorted sites).
 //
 // U and dU per chain with the hand-derived adjoint (oracle
-// BNN.pe_grad).  One workgroup (256 threads) owns one evaluated chain: its weights, both
-// activation layers and the adjoints live in LDS (N=100, H=69: 78 KB), the three
-// N x H x H products run as 4x4 register-blocked FMA loops.  The model is ~3 MFLOP per
-// chain-leapfrog -- ~3% of the dense-mass products it runs between (dense.hip), so it is
-// written for clarity and LDS residency rather than MFMA.  The chain-major columns of the
+// BNN.pe_grad).  One workgroup (8 waves) owns one evaluated chain: its weights, both
+// activation layers and the adjoints live in LDS (N=100, H=69: 78 KB, two workgroups per
+// CU).  The three N x H x H products -- h1 W2 (forward), h1^T ga2 (grad W2) and ga2 W2^T
+// (back to layer 1), ~2.9 MFLOP of the ~3 per chain-evaluation -- run on the matrix cores as
+// 32 x 32 output tiles of v_mfma_f32_32x32x2_f32 (f32 operands, f32 accumulation in k order:
+// bitwise the sequential FMA chain), the tiles of a product spread over the waves, operands
+// read from LDS with the padding rows / columns masked to zero.  gfx950's f32 matrix peak
+// equals its f32 vector peak (157 TF/s), so the gain over register-blocked FMA loops is the
+// freed VALU (measured 0.30 vs 0.34 ms at 2048 chains, scripts/ab_bnn.py); the rest of a
+// chain's evaluation is latency-bound serial phases (tanh layers, reductions, 20 KB of
+// parameters in and gradient out).  The chain-major columns of the
 // evaluated chains are first transposed to rows (k_cols_to_rows, 64x64 LDS tiles, both
 // sides coalesced) so each workgroup reads its chain's 20 KB parameter vector and writes
 // its gradient contiguously; k_rows_to_cols scatters the gradients back.
@@ -19,10 +25,27 @@
 
 namespace {
 
-#ifndef NMX_BNN_THREADS
-#define NMX_BNN_THREADS 512
-#endif
-constexpr int THREADS = NMX_BNN_THREADS;
+constexpr int THREADS = 512;
+constexpr int NWAVES = THREADS / 64;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// One 32 x 32 output tile: acc[r] = sum_k A(row, k) B(k, col) over k < K (K steps of 2), with
+// lane l supplying A(l & 31, 2s + (l >> 5)) and B(2s + (l >> 5), l & 31); register r of lane l
+// holds row (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31.
+template <class FA, class FB>
+__device__ __forceinline__ f32x16 mfma_tile(int K, FA fa, FB fb) {
+  const int lane = threadIdx.x & 63, l31 = lane & 31, kh = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll 4
+  for (int k0 = 0; k0 < K; k0 += 2) {
+    const int k = k0 + kh;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa(l31, k), fb(k, l31), acc, 0, 0, 0);
+  }
+  return acc;
+}
+__device__ __forceinline__ int tile_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 
 struct BnnDims {
   int N, Dx, H;
@@ -121,11 +144,14 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   const float u = z[0];
   const float p = expf(u);
   float wsq = 0.0f;
+  // unrolled so that a thread's loads are in flight together (a rolled loop waits on each)
+#pragma unroll 4
   for (int i = t; i < Dx * H; i += THREADS) {
     const float v = z[dm.o_w1 + i];
     W1[i] = v;
     wsq += v * v;
   }
+#pragma unroll 20
   for (int i = t; i < H * H; i += THREADS) {
     const float v = z[dm.o_w2 + i];
     W2[i] = v;
@@ -136,6 +162,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     w3[i] = v;
     wsq += v * v;
   }
+#pragma unroll 4
   for (int i = t; i < N * Dx; i += THREADS) Xs[i] = X[i];
   for (int i = t; i < N; i += THREADS) Ys[i] = Y[i];
   __syncthreads();
@@ -149,28 +176,20 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
   __syncthreads();
 
-  // h2 = tanh(h1 W2): 4x4 blocks over (n, j)
-  const int nbn = (N + 3) / 4, nbh = (H + 3) / 4;
-  for (int blk = t; blk < nbn * nbh; blk += THREADS) {
-    const int n0 = (blk / nbh) * 4, j0 = (blk % nbh) * 4;
-    float acc[4][4] = {};
-    for (int i = 0; i < H; ++i) {
-      float a[4], w[4];
+  // h2 = tanh(h1 W2): 32 x 32 tiles over (n, j), K = i
+  const int wv = t >> 6, l31 = t & 31;
+  const int ntn = (N + 31) / 32, nth = (H + 31) / 32;
+  for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
+    const int n0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
+    const f32x16 acc = mfma_tile(
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[k * H + j0 + c] : 0.0f; });
+    const int j = j0 + l31;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = n0 + q < N ? h1[(n0 + q) * H + i] : 0.0f;
-        w[q] = j0 + q < H ? W2[i * H + j0 + q] : 0.0f;
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + tile_row(r);
+      if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
     }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-        if (n0 + x < N && j0 + y < H) h2[(n0 + x) * H + j0 + y] = tanhf(acc[x][y]);
   }
   __syncthreads();
 
@@ -200,59 +219,38 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
   __syncthreads();
 
-  // grad W2 = W2 + h1^T ga2: 4x4 blocks over (i, j)
-  for (int blk = t; blk < nbh * nbh; blk += THREADS) {
-    const int i0 = (blk / nbh) * 4, j0 = (blk % nbh) * 4;
-    float acc[4][4] = {};
-    for (int n = 0; n < N; ++n) {
-      float a[4], w[4];
+  // grad W2 = W2 + h1^T ga2: 32 x 32 tiles over (i, j), K = n
+  for (int tile = wv; tile < nth * nth; tile += NWAVES) {
+    const int i0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
+    const f32x16 acc = mfma_tile(
+        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[k * H + i0 + m] : 0.0f; },
+        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[k * H + j0 + c] : 0.0f; });
+    const int j = j0 + l31;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = i0 + q < H ? h1[n * H + i0 + q] : 0.0f;
-        w[q] = j0 + q < H ? h2[n * H + j0 + q] : 0.0f;
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
+    for (int r = 0; r < 16; ++r) {
+      const int i = i0 + tile_row(r);
+      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
     }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-        if (i0 + x < H && j0 + y < H) {
-          const int ij = (i0 + x) * H + j0 + y;
-          g[dm.o_w2 + ij] = W2[ij] + acc[x][y];
-        }
   }
   __syncthreads();
 
-  // ga1 = (ga2 W2^T) * (1 - h1^2): 4x4 blocks over (n, i), in place of h1 (a block reads
-  // h1 only at its own elements; grad W2 above finished reading h1 at the barrier)
-  for (int blk = t; blk < nbn * nbh; blk += THREADS) {
-    const int n0 = (blk / nbh) * 4, i0 = (blk % nbh) * 4;
-    float acc[4][4] = {};
-    for (int j = 0; j < H; ++j) {
-      float a[4], w[4];
+  // ga1 = (ga2 W2^T) * (1 - h1^2): 32 x 32 tiles over (n, i), K = j, in place of h1 (a tile
+  // reads h1 only at its own elements; grad W2 above finished reading h1 at the barrier)
+  for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
+    const int n0 = (tile / nth) * 32, i0 = (tile % nth) * 32;
+    const f32x16 acc = mfma_tile(
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[(i0 + c) * H + k] : 0.0f; });
+    const int i = i0 + l31;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = n0 + q < N ? h2[(n0 + q) * H + j] : 0.0f;
-        w[q] = i0 + q < H ? W2[(i0 + q) * H + j] : 0.0f;
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + tile_row(r);
+      if (n < N && i < H) {
+        float* hp = &h1[n * H + i];
+        const float hv = *hp;
+        *hp = acc[r] * (1.0f - hv * hv);
       }
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] += a[x] * w[y];
     }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int y = 0; y < 4; ++y)
-        if (n0 + x < N && i0 + y < H) {
-          float* hp = &h1[(n0 + x) * H + i0 + y];
-          const float hv = *hp;
-          *hp = acc[x][y] * (1.0f - hv * hv);
-        }
   }
   __syncthreads();
 
