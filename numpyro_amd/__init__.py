@@ -7,3 +7,6 @@ as a device state machine (csrc/nuts.hip) driving fused potential+gradient HIP k
 __version__ = "0.1.0"
 
 from . import diagnostics, random  # noqa: F401,E402
+from . import distributions, jnp  # noqa: F401,E402
+from .frontend import LocScaleReparam, reparam  # noqa: F401,E402
+from .primitives import deterministic, plate, sample  # noqa: F401,E402

@@ -148,9 +148,9 @@ class HMC(MCMCKernel):
         if isinstance(dense_mass, (list, tuple)) and len(dense_mass) > 0:
             raise NotImplementedError("structured dense_mass (list of site groups) is not supported; "
                                       "use dense_mass=True for a full dense mass matrix")
-        if model is not None and not isinstance(model, FusedModel):
-            raise TypeError("`model` must be a fused model (numpyro_amd.potentials.*); arbitrary "
-                            "Python models cannot run on the device engine")
+        if model is not None and not (isinstance(model, FusedModel) or callable(model)):
+            raise TypeError("`model` must be a model function (numpyro_amd.sample / plate / distributions, "
+                            "mapped onto a fused kernel by numpyro_amd.frontend) or a fused model")
         if potential_fn is not None and not isinstance(potential_fn, Potential):
             raise TypeError("`potential_fn` must be a numpyro_amd.potentials.Potential")
         self._model = model
@@ -200,8 +200,14 @@ class HMC(MCMCKernel):
             find_heuristic_step_size=self._find_heuristic_step_size)
 
     def potential(self, model_args=(), model_kwargs=None) -> Potential:
-        if self._model is not None:
+        if isinstance(self._model, FusedModel):
             self._potential = self._model.potential(*model_args, **(model_kwargs or {}))
+        elif self._model is not None:
+            # model front end: trace the model and map it onto its fused kernel
+            # (initialize_model, numpyro/infer/util.py:632-800)
+            from ..frontend import potential_from_model
+
+            self._potential = potential_from_model(self._model, model_args, model_kwargs)
         return self._potential
 
     def init_radius(self):

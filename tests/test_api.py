@@ -22,7 +22,9 @@ def test_kernel_argument_validation():
     with pytest.raises(ValueError):
         HMC(P.eight_schools, num_steps=None, trajectory_length=None)
     with pytest.raises(TypeError):
-        NUTS(lambda: None)  # arbitrary Python models cannot run on the device engine
+        NUTS(3.0)  # a model is a function (front end) or a fused model
+    with pytest.raises(NotImplementedError):
+        NUTS(lambda: None).potential()  # no sample sites: no fused kernel for this structure
     with pytest.raises(TypeError):
         NUTS(potential_fn=lambda z: z)
     with pytest.raises(NotImplementedError):

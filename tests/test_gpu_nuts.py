@@ -602,3 +602,34 @@ def test_find_heuristic_step_size_matches_oracle(device, model, dim):
             np.testing.assert_allclose(ss[c, t], wa.step_size, rtol=1e-5, err_msg=f"chain {c} after transition {t}")
         moved += int(ss0[c] != 1.0)
     assert moved > 0  # the search changed the initial step size of at least some chains
+
+
+@pytest.mark.parametrize("which", ["covtype", "eight_schools", "funnel_reparam", "sv", "bnn"])
+def test_frontend_models_run_like_fused_models(device, which):
+    """NUTS(model) with a model written against numpyro's API (tests/model_zoo.py) runs on the
+    fused kernel its structure maps to: draws, tree sizes and deterministic sites are bitwise
+    those of the registered fused model."""
+    import model_zoo as Z
+
+    if which == "covtype":
+        X, y = datasets.covtype_synthetic(n_rows=2000, seed=0)
+        args, m, fm = (X, y), Z.covtype_model, P.logistic_regression
+    elif which == "eight_schools":
+        args, m, fm = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y), Z.eight_schools, P.eight_schools
+    elif which == "funnel_reparam":
+        args, m, fm = (10,), Z.funnel_reparam, P.funnel_reparam
+    elif which == "sv":
+        args, m, fm = (datasets.sp500_synthetic(T=300),), Z.stochastic_volatility, P.stochastic_volatility
+    else:
+        X, Y = datasets.bnn_data(N=40, D_X=3)
+        args, m, fm = (X, Y, 5), Z.bnn, P.bnn
+    out = []
+    for model in (m, fm):
+        mcmc = MCMC(NUTS(model), num_warmup=40, num_samples=20, num_chains=48)
+        mcmc.run(3, *args, extra_fields=("num_steps",))
+        out.append((mcmc.get_samples(True), mcmc.get_extra_fields(True)["num_steps"]))
+    (sa, na), (sb, nb) = out
+    assert set(sa) == set(sb)
+    for k in sa:
+        np.testing.assert_array_equal(sa[k].cpu().numpy(), sb[k].cpu().numpy(), err_msg=k)
+    np.testing.assert_array_equal(na.cpu().numpy(), nb.cpu().numpy())
