@@ -44,6 +44,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    p.add_argument("--configs", default="c2,c3,c4",
+                   help="BASELINE.json secondary configs measured after the headline (comma list of c2 funnel-10k "
+                        "dense, c3 BNN dense, c4 stochastic volatility; 'none' skips); c2/c3 are one-GPU configs "
+                        "and run at --gpus 1 only, c4 shards its 8192 chains over the ranks")
     return p.parse_args()
 
 
@@ -97,7 +101,109 @@ def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds):
             "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
 
 
+# BASELINE.json configs[2..4]: (model, args, chains (total), warmup, timed transitions, dense mass,
+# roofline basis).  Short protocols (the adaptation windows of W = 20/50: one or two middle
+# windows), so the default bench run stays within minutes; the headline covtype line keeps the
+# SURVEY §8d protocol.
+def _config_specs():
+    from numpyro_amd import datasets
+    from numpyro_amd import potentials as P
+
+    X, Y = datasets.bnn_data(N=100, D_X=3)
+    H = 69
+    D_bnn = 1 + 3 * H + H * H + H
+    return {
+        "c2": dict(name="funnel D=10000, dense mass (pooled), examples/funnel.py", model=P.funnel, args=(10000,),
+                   chains=4096, warmup=20, steps=5, dense="pooled", one_gpu=True,
+                   flop=2.0 * 10000 * 10000, basis="2 D^2 FLOP per chain-leapfrog (z = mu + T w, g_w = T^T g_z)"),
+        "c3": dict(name="BNN D_X=3 N=100 H=69 (D=5038), dense mass (pooled), examples/bnn.py", model=P.bnn,
+                   args=(X, Y, H), chains=2048, warmup=20, steps=5, dense="pooled", one_gpu=True,
+                   flop=2.0 * D_bnn * D_bnn + 6.0 * 100 * H * H + 6.0 * 100 * 3 * H,
+                   basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog"),
+        "c4": dict(name="stochastic volatility T=2517 (D=2519), diag mass, examples/stochastic_volatility.py",
+                   model=P.stochastic_volatility, args=(datasets.sp500_synthetic(),), chains=8192, warmup=50,
+                   steps=10, dense=False, one_gpu=False, bytes=7 * 4 * 2519,
+                   basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)"),
+    }
+
+
+def secondary_configs(which, rank, world, device):
+    """Leapfrogs/s of the BASELINE.json secondary configs on synthetic data of their shape:
+    untimed adaptation, then `steps` transitions timed between barrier + synchronize (max over
+    ranks); value = sum(num_steps) over all ranks / wall."""
+    import torch
+    import torch.distributed as dist
+
+    from numpyro_amd import shard
+    from numpyro_amd.infer import MCMC, NUTS, shard_chains
+
+    out = {}
+    specs = _config_specs()
+    for key in [k.strip() for k in which.split(",") if k.strip() and k.strip() != "none"]:
+        sp = specs[key]
+        if sp["one_gpu"] and world > 1:
+            continue
+        lo, hi = shard_chains(sp["chains"], rank, world)
+        mcmc = MCMC(NUTS(sp["model"], dense_mass=sp["dense"]), num_warmup=sp["warmup"], num_samples=sp["steps"],
+                    num_chains=hi - lo, chain_offset=lo, progress_bar=False)
+        t0 = time.perf_counter()
+        mcmc.warmup(7, *sp["args"])
+        torch.cuda.synchronize()
+        setup_s = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mcmc.run(8, *sp["args"], extra_fields=("num_steps", "diverging"))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ef = mcmc.get_extra_fields()
+        st = torch.tensor([ef["num_steps"].to(torch.float64).sum().item(), wall,
+                           float(ef["diverging"].sum().item())], dtype=torch.float64, device=device)
+        if world > 1:
+            tot, mx = st.clone(), st.clone()
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            leap, wall, div = tot[0].item(), mx[1].item(), tot[2].item()
+        else:
+            leap, div = st[0].item(), st[2].item()
+        r = {"workload": sp["name"], "num_chains": sp["chains"], "warmup": sp["warmup"], "steps": sp["steps"],
+             "value": leap / wall, "unit": "leapfrog/s", "ms_per_step": wall * 1e3 / sp["steps"],
+             "mean_tree_size": leap / (sp["chains"] * sp["steps"]), "divergent_frac": div / (sp["chains"] * sp["steps"]),
+             "adapt_wall_s": setup_s, "dense_mass": sp["dense"] or False}
+        if "flop" in sp:
+            tf = sp["flop"] * leap / wall / 1e12
+            peak = MI355X_BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
+            r["roofline"] = {"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
+                             "basis": sp["basis"] + " over the sampling wall time (split-bf16 whitening GEMMs)"}
+        else:
+            gbs = sp["bytes"] * leap / wall / 1e9
+            r["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": gbs / MI355X_HBM_PEAK_GBS, "basis": sp["basis"] + " over the sampling wall time"}
+        if not sp["one_gpu"]:
+            # end-of-run exchange (SURVEY.md §8e): cross-chain R-hat / ESS over ranks + sample gather
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            s_site = mcmc.get_samples(group_by_chain=True)["s"]
+            rhat = shard.split_gelman_rubin(s_site) if s_site.shape[1] >= 4 else None
+            gathered = shard.gather_chains(s_site[:, :, :8])
+            torch.cuda.synchronize()
+            r["end_of_run"] = {"ms": (time.perf_counter() - te) * 1e3, "gathered_chains": int(gathered.shape[0]),
+                               "max_split_rhat": float(rhat.max()) if rhat is not None else None,
+                               "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"}
+            r["parallelism"] = f"chains sharded {world}-way (no data-path collective)"
+            r["scaling"] = "strong"
+        out[key] = r
+        del mcmc
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
+    t_start = time.perf_counter()
     args = parse()
     import numpy as np
     import torch
@@ -245,6 +351,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2),
                                                args.adapt + args.warmup, args.adapt, args.cpu_chains,
                                                args.cpu_seconds)
+    if args.configs != "none":
+        del mcmc, eng, pot, start_state
+        torch.cuda.empty_cache()
+        cfgs = secondary_configs(args.configs, rank, world, device)
+        if rank == 0:
+            out["configs"] = cfgs
+    if rank == 0:
+        out["bench_wall_s"] = time.perf_counter() - t_start
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

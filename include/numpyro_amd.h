@@ -184,6 +184,28 @@ int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, v
 int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
                   const int8_t* transform, void* stream);
 
+/* The step of the wide schedule (dim >= 257) fused with the potential of a D-split model:
+ * ONE call replaces `potential(z_eval) -> nmx_nuts_step` of the launched loop (the model's
+ * value_and_grad, hmc_util.py:242-252, then the leapfrog end / tree / transition logic of
+ * nmx_nuts_step) with three kernels instead of six: the model's row gradients fused with the
+ * leapfrog end of the same rows (per D-slice), a fixed-order slice reduction whose last block
+ * per chain group finishes U, the scalar-site gradients and the scalar logic, and the apply
+ * kernel.  Loop: nmx_nuts_resume, nmx_nuts_step once (starts the transitions), then this call
+ * until counters[0] == num_chains.  Same semantics as the launched loop; sums in a fixed
+ * order that depends on dim only (rounding differs from the separate kernels).
+ *   NMX_WIDE_STOCHASTIC_VOLATILITY: data = returns[n], dim == n + 2 (stochastic_volatility.py:57-65)
+ *   NMX_WIDE_FUNNEL:                data unused, n == dim (funnel.py:44-46)
+ *   NMX_WIDE_FUNNEL_NONCENTERED:    data unused, n == dim (funnel.py:49, LocScaleReparam(0))
+ * workspace: nmx_nuts_wide_model_workspace_bytes(dim, num_chains) bytes, zero-filled before
+ * the first call (the library leaves its arrival counters zero). */
+#define NMX_WIDE_STOCHASTIC_VOLATILITY 1
+#define NMX_WIDE_FUNNEL 2
+#define NMX_WIDE_FUNNEL_NONCENTERED 3
+size_t nmx_nuts_wide_model_workspace_bytes(int dim, int num_chains);
+int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                             const int8_t* transform, int model, const float* data, int n, void* workspace,
+                             void* stream);
+
 /* Persistent schedule for one-wave models (dim < 16): ONE launch runs
  * every remaining transition of [iter_begin, iter_end) of every chain -- each thread owns a
  * chain and alternates the model's potential (inline) with the fused step until the chain is

@@ -1,0 +1,148 @@
+// Per-coordinate potential terms of the D-split (wide) models, shared by their standalone
+// potential kernels (potential_wide.hip) and the fused leaf kernel of the wide NUTS step
+// (nuts.hip, k_wide_leaf / k_wide_rs), so both compute every coordinate gradient with the same
+// device code.  A model splits z into
+//   * per-coordinate rows [lo, hi): gradient from the row, its stencil neighbours and the
+//     model's global values; each row adds NSUM partial sums;
+//   * NSCALAR global (scalar-site) rows, whose gradients and U need the full sums (fin).
+// Gradients are hand-derived.
+#pragma once
+#include <math.h>
+
+#include "nmx_common.h"
+
+// digamma for x > 0: recurrence up to x >= 6, then the asymptotic series.
+__device__ __forceinline__ float nmx_digammaf(float x) {
+  float acc = 0.0f;
+  while (x < 6.0f) {
+    acc -= 1.0f / x;
+    x += 1.0f;
+  }
+  const float inv = 1.0f / x;
+  const float inv2 = inv * inv;
+  const float series =
+      inv2 * (1.0f / 12.0f - inv2 * (1.0f / 120.0f - inv2 * (1.0f / 252.0f - inv2 * (1.0f / 240.0f - inv2 / 132.0f))));
+  return acc + logf(x) - 0.5f * inv - series;
+}
+
+// Stochastic volatility (examples/stochastic_volatility.py:57-65), z = (a = log nu, s[T],
+// b = log sigma): rows 1..T are s_t (t = row - 1), scalar rows 0 (a) and T + 1 (b).
+// Sums: sum d_t^2, sum log1p(q_t), sum q_t / (1 + q_t), sum s_t.
+struct NmxWideSV {
+  const float* ret;
+  int T;
+  static constexpr int NSUM = 4;
+  static constexpr int NSCALAR = 2;
+  struct Glob {
+    float a, b, nu, inv_sig2, inv_nu;
+  };
+  NMX_HD int lo() const { return 1; }
+  NMX_HD int hi() const { return T + 1; }
+  NMX_HD int scalar_row(int i) const { return i == 0 ? 0 : T + 1; }
+  __device__ __forceinline__ Glob globals(const float* z, int ldc, int c) const {
+    Glob g;
+    g.a = z[c];
+    g.b = z[(size_t)(T + 1) * ldc + c];
+    g.nu = expf(g.a);
+    g.inv_sig2 = expf(-2.0f * g.b);
+    g.inv_nu = 1.0f / g.nu;
+    return g;
+  }
+  // dU/ds_t of row d = 1 + t (GaussianRandomWalk stencil + StudentT(nu, 0, e^s) term)
+  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob& g, float* sums) const {
+    const int t = d - 1;
+    const float s = z[(size_t)d * ldc + c];
+    const float sp = t > 0 ? z[(size_t)(d - 1) * ldc + c] : 0.0f;
+    const float sn = t + 1 < T ? z[(size_t)(d + 1) * ldc + c] : 0.0f;
+    const float dd = s - sp;
+    const float dn = t + 1 < T ? sn - s : 0.0f;
+    const float r = ret[t];
+    const float q = r * r * expf(-2.0f * s) * g.inv_nu;
+    const float qq = q / (1.0f + q);
+    sums[0] += dd * dd;
+    sums[1] += log1pf(q);
+    sums[2] += qq;
+    sums[3] += s;
+    // dU/ds_t = -( -(d_t - d_{t+1})/sigma^2 + (nu+1) q/(1+q) - 1 )
+    return (dd - dn) * g.inv_sig2 - (g.nu + 1.0f) * qq + 1.0f;
+  }
+  // U and the gradients of the scalar rows (gs[0] = dU/da, gs[1] = dU/db)
+  __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
+    const float a = g.a, b = g.b, nu = g.nu, inv_sig2 = g.inv_sig2, inv_nu = g.inv_nu;
+    const float Tf = (float)T;
+    const float sig = expf(b);
+    const float lg = lgammaf(0.5f * nu) - lgammaf(0.5f * (nu + 1.0f));
+    // log p
+    float lp = 3.912023005428146f - 50.0f * sig + b;                        // Exponential(50) + log|J|
+    lp += -0.5f * sums[0] * inv_sig2 - Tf * b - Tf * 0.9189385332046727f;  // GaussianRandomWalk
+    lp += -2.302585092994046f - 0.1f * nu + a;                              // Exponential(0.1) + log|J|
+    lp += -0.5f * (nu + 1.0f) * sums[1] - sums[3] -
+          Tf * (0.5f * logf(nu) + 0.5723649429247001f + lg);               // StudentT(nu, 0, e^s)
+    const float dig = nmx_digammaf(0.5f * nu) - nmx_digammaf(0.5f * (nu + 1.0f));
+    const float ga = nu * (-0.1f - 0.5f * sums[1] + 0.5f * (nu + 1.0f) * inv_nu * sums[2] - 0.5f * Tf * inv_nu -
+                           0.5f * Tf * dig) + 1.0f;
+    const float gb = -50.0f * sig + 1.0f + sums[0] * inv_sig2 - Tf;
+    gs[0] = -ga;
+    gs[1] = -gb;
+    return -lp;
+  }
+};
+
+// Centred funnel (examples/funnel.py:44-46), z = (x[K], y), K = dim - 1:
+// U = y^2/18 + log(3 sqrt(2 pi)) + sum_i [x_i^2 e^-y / 2 + y/2 + log(2 pi)/2].
+struct NmxWideFunnel {
+  int dim;
+  static constexpr int NSUM = 1;
+  static constexpr int NSCALAR = 1;
+  struct Glob {
+    float y, e;
+  };
+  NMX_HD int lo() const { return 0; }
+  NMX_HD int hi() const { return dim - 1; }
+  NMX_HD int scalar_row(int) const { return dim - 1; }
+  __device__ __forceinline__ Glob globals(const float* z, int ldc, int c) const {
+    Glob g;
+    g.y = z[(size_t)(dim - 1) * ldc + c];
+    g.e = expf(-g.y);
+    return g;
+  }
+  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob& g, float* sums) const {
+    const float x = z[(size_t)d * ldc + c];
+    sums[0] += x * x;
+    return x * g.e;
+  }
+  __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
+    const float K = (float)(dim - 1);
+    gs[0] = g.y / 9.0f + 0.5f * K - 0.5f * g.e * sums[0];
+    return g.y * g.y / 18.0f + 2.0175508218727822f + 0.5f * g.e * sums[0] + K * (0.5f * g.y + 0.9189385332046727f);
+  }
+};
+
+// Non-centred funnel (examples/funnel.py:49, LocScaleReparam(0), numpyro/infer/reparam.py:
+// 104-145), z = (x_decentered[K], y): U = y^2/18 + log(3 sqrt(2 pi)) + sum_i [x_i^2/2 +
+// log(2 pi)/2]; dU/dx_i = x_i, dU/dy = y/9.
+struct NmxWideFunnelNC {
+  int dim;
+  static constexpr int NSUM = 1;
+  static constexpr int NSCALAR = 1;
+  struct Glob {
+    float y;
+  };
+  NMX_HD int lo() const { return 0; }
+  NMX_HD int hi() const { return dim - 1; }
+  NMX_HD int scalar_row(int) const { return dim - 1; }
+  __device__ __forceinline__ Glob globals(const float* z, int ldc, int c) const {
+    Glob g;
+    g.y = z[(size_t)(dim - 1) * ldc + c];
+    return g;
+  }
+  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob&, float* sums) const {
+    const float x = z[(size_t)d * ldc + c];
+    sums[0] += x * x;
+    return x;
+  }
+  __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
+    gs[0] = g.y / 9.0f;
+    return g.y * g.y / 18.0f + 2.0175508218727822f + 0.5f * sums[0] + (float)(dim - 1) * 0.9189385332046727f;
+  }
+};

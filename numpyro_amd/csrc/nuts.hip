@@ -21,6 +21,7 @@
 
 #include "nmx_common.h"
 #include "nmx_small_models.h"
+#include "nmx_wide_models.h"
 
 namespace {
 
@@ -560,10 +561,10 @@ struct LeafIn {
   float ckr[MAXD], ckrs[MAXD];
 };
 
-template <bool NUTS, bool PRE>
+template <bool NUTS, bool PRE, bool LOADG = true>
 __device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t idx, LeafIn& x) {
   const Arena& a = *v.a;
-  x.g = AV(NMX_F_G_EVAL)[idx];
+  if constexpr (LOADG) x.g = AV(NMX_F_G_EVAL)[idx];
   x.rf = (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
   x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
   if constexpr (NUTS) {
@@ -949,6 +950,7 @@ __global__ __launch_bounds__(64) void k_nuts_persistent(StepArgs P, Pot pot, int
 constexpr int WIDE_WAVES = 4;   // waves per V1/V2 block (64 chains x one D-slice)
 constexpr int WIDE_SWAVES = 4;  // waves per S block (slices split across waves)
 
+
 struct WideArgs {
   StepArgs p;
   int ns;  // slices
@@ -1148,6 +1150,237 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   }
   block_sum<WIDE_WAVES, 1>(ke0, lds);
   if (wv == 0 && A.start_iter) a.part0[(size_t)s * ldc + c] = ke0[0];
+}
+
+// ---- fused leaf of the wide schedule for the D-split models (nmx_wide_models.h) -----------
+// The launched wide path runs six kernels per leaf: the model's part + fin, then V1, R, S, V2.
+// For a model whose potential is per-row terms plus global sums, three suffice:
+//   B  k_wide_leaf  (chain groups x D-slices): the model's row gradients and partial sums, with
+//                   the leapfrog end (V1) of the same rows on the gradient in registers;
+//   C  k_wide_rs    (chain groups x entries):  the fixed-order slice reduction of each partial
+//                   entry (R); the last block of a chain group to finish then completes the
+//                   potential (U and the scalar-site gradients), the leapfrog end of the
+//                   scalar-site rows, and runs the scalar logic (S);
+//   A  k_wide_v2    as before.
+// Sums are in a fixed order that depends on D only (slices in order, scalar-site rows last),
+// so draws stay independent of the launch composition and the number of GPUs; they differ
+// from the six-kernel path in rounding only (the potential's slices are the step's here).
+// Workspace: model partials [NS][WIDE_NSUM][ldc] f32, model totals [WIDE_NSUM][ldc] f32, one
+// arrival counter per chain group (zero on entry; the last block leaves it zero).
+constexpr int WIDE_NSUM = 4;  // largest M::NSUM
+
+inline size_t wide_ws_part_bytes(int D, int ldc) { return align_up((size_t)num_slices(D) * WIDE_NSUM * ldc * 4); }
+inline size_t wide_ws_tot_bytes(int ldc) { return align_up((size_t)WIDE_NSUM * ldc * 4); }
+
+// NUTS leapfrog end of rows d0, d0 + step, ... < d1 with the model's gradient, two rows per
+// round: both rows' leaf-state loads, then the model's loads (z and stencil neighbours), then
+// the stores (the one-pass form of leaf_rows; same sums in the same order).
+template <bool NUTS, class M>
+__device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, const M& m, const typename M::Glob& gl,
+                                                float seff, int d0, int d1, int step, int c, float* red,
+                                                float* sums) {
+  const Arena& a = *v.a;
+  const float* ZE = AV(NMX_F_Z_EVAL);
+  float* GE = AV(NMX_F_G_EVAL);
+  int d = d0;
+  for (; d + step < d1; d += 2 * step) {
+    const size_t i0 = (size_t)d * v.ldc + c, i1 = (size_t)(d + step) * v.ldc + c;
+    LeafIn x0, x1;
+    leaf_load<NUTS, true, false>(v, A, i0, x0);
+    leaf_load<NUTS, true, false>(v, A, i1, x1);
+    x0.g = m.row(ZE, v.ldc, c, d, gl, sums);
+    x1.g = m.row(ZE, v.ldc, c, d + step, gl, sums);
+    GE[i0] = x0.g;
+    GE[i1] = x1.g;
+    leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
+    leaf_store<NUTS, true>(v, A, seff, i1, x1, red);
+  }
+  for (; d < d1; d += step) {
+    const size_t i0 = (size_t)d * v.ldc + c;
+    LeafIn x0;
+    leaf_load<NUTS, true, false>(v, A, i0, x0);
+    x0.g = m.row(ZE, v.ldc, c, d, gl, sums);
+    GE[i0] = x0.g;
+    leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_leaf(WideArgs W, M m, float* ppart) {
+  constexpr int NR = NPART + M::NSUM;
+  constexpr int WV = WIDE_WAVES;
+  __shared__ float lds[NR * WV * 64];
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int s = blockIdx.y;
+  const int ldc = cfg.ldc, D = cfg.dim;
+  const bool valid = c < cfg.num_chains;
+  int ph = NMX_PH_DONE, dir = 0, subn = 0, depth = 0;
+  float seff0 = 0.0f;
+  if (valid) {
+    ph = AI(NMX_F_PHASE)[c];
+    dir = AI(NMX_F_DIR)[c];
+    subn = AI(NMX_F_SUB_N)[c];
+    depth = AI(NMX_F_DEPTH)[c];
+    seff0 = AF(NMX_F_STEP_EFF)[c];
+  }
+  if (!__syncthreads_or(ph == NMX_PH_LEAF)) return;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  Act A{};
+  A.leaf = ph == NMX_PH_LEAF;
+  A.dirR = A.leaf ? dir : 0;
+  A.k = (A.leaf && is_nuts) ? subn : 0;
+  A.j = (A.leaf && is_nuts) ? depth : 0;
+  A.imin = 1;
+  A.imax = 0;
+  if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);
+  A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
+  const float seff = A.leaf ? seff0 : 0.0f;
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
+  float red[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) red[i] = 0.0f;
+  const int r0 = max(s * W.sw, m.lo()), r1 = min(min(D, (s + 1) * W.sw), m.hi());
+  if (A.leaf) {
+    const typename M::Glob gl = m.globals(AV(NMX_F_Z_EVAL), ldc, c);
+    if (is_nuts) leaf_rows_model<true>(v, A, m, gl, seff, r0 + wv, r1, WV, c, red, red + NPART);
+    else leaf_rows_model<false>(v, A, m, gl, seff, r0 + wv, r1, WV, c, red, red + NPART);
+  }
+  block_sum<WV, NR>(red, lds);
+  if (wv == 0 && A.leaf) {
+    *(part_ptr(a, ldc, s, 0) + c) = red[0];
+    if (is_nuts) {
+#pragma unroll
+      for (int i = 0; i < MAXD; ++i)
+        if (i >= A.imin && i <= A.imax) {
+          *(part_ptr(a, ldc, s, 1 + 2 * i) + c) = red[1 + 2 * i];
+          *(part_ptr(a, ldc, s, 2 + 2 * i) + c) = red[2 + 2 * i];
+        }
+      if (A.tree_chk) {
+        *(part_ptr(a, ldc, s, 1 + 2 * MAXD) + c) = red[1 + 2 * MAXD];
+        *(part_ptr(a, ldc, s, 2 + 2 * MAXD) + c) = red[2 + 2 * MAXD];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < M::NSUM; ++k) ppart[((size_t)s * WIDE_NSUM + k) * ldc + c] = red[NPART + k];
+  }
+}
+
+// Reduction + (last block per chain group) potential finish, scalar-site leapfrog ends and
+// scalar logic.  Entries 0..NPART-1 = V1 partials, NPART = momentum KE, NPART + 1 + k = the
+// model's sum k.  The hand-off to the last block is the in-launch split reduction of
+// cdna_hip_programming.md §6 G16: write-through (sc1) stores of the totals, every storing
+// wave drained, a workgroup barrier, one relaxed agent-scope arrival add per block; the block
+// drawing the last ticket acquires (agent) before reading them.
+template <class M>
+__global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_rs(WideArgs W, M m, const float* ppart, float* ptot,
+                                                            int* cnt) {
+  constexpr int NE = NPART + 1 + M::NSUM;
+  __shared__ float lds[WIDE_SWAVES * 64];
+  __shared__ int last_block;
+  const nmx_nuts_config& cfg = W.p.cfg;
+  const Arena& a = W.p.a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int e = blockIdx.y;
+  const int ldc = cfg.ldc;
+  const bool valid = c < cfg.num_chains;
+  const int ph = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
+  // every block of a chain group sees the same phases: a group with no live chain is skipped
+  // by all of them (no arrival, no scalar logic: a DONE chain's step is a no-op)
+  if (!__syncthreads_or(ph != NMX_PH_DONE)) return;
+  bool need = false;
+  if (valid) need = e <= NPART ? entry_needed(cfg, a, c, e) : ph == NMX_PH_LEAF;
+  float sum = 0.0f;
+  if (need) {
+    if (e < NPART) {
+      for (int sl = wv; sl < W.ns; sl += WIDE_SWAVES) sum += *(part_ptr(a, ldc, sl, e) + c);
+    } else if (e == NPART) {
+      for (int sl = wv; sl < W.ns; sl += WIDE_SWAVES) sum += a.part0[(size_t)sl * ldc + c];
+    } else {
+      const int k = e - NPART - 1;
+      for (int sl = wv; sl < W.ns; sl += WIDE_SWAVES) sum += ppart[((size_t)sl * WIDE_NSUM + k) * ldc + c];
+    }
+  }
+  lds[wv * 64 + lane] = sum;
+  __syncthreads();
+  if (wv == 0 && need) {
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < WIDE_SWAVES; ++w) t += lds[w * 64 + lane];
+    float* dst = e <= NPART ? a.tot + (size_t)e * ldc + c : ptot + (size_t)(e - NPART - 1) * ldc + c;
+    __hip_atomic_store(dst, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last_block = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NE - 1;
+  __syncthreads();
+  if (!last_block) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (wv != 0) return;
+
+  // ---- last block, wave 0: one lane per chain ----
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+  ChainScalars S;
+  Act A;
+  const int ph_in = ph;
+  begin_step(cfg, a, c, valid, S, A);
+  const bool ke0_pending = valid && (AI(NMX_F_ACTION)[c] & ACT_KE0_PENDING);
+  const float* T = a.tot + c;
+  if (ke0_pending) {
+    S.E0 = S.pe + 0.5f * T[(size_t)NPART * ldc];  // build_tree :1130 (momentum KE from the last V2)
+    S.energy = S.E0;
+  }
+  float red[NPART];
+#pragma unroll
+  for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+  if (A.leaf) {
+    // potential: U and the scalar-site gradients from the reduced sums
+    float sums[M::NSUM];
+#pragma unroll
+    for (int k = 0; k < M::NSUM; ++k) sums[k] = ptot[(size_t)k * ldc + c];
+    const typename M::Glob gl = m.globals(AV(NMX_F_Z_EVAL), ldc, c);
+    float gs[M::NSCALAR];
+    A.pe_eval = m.fin(sums, gl, gs);
+    AF(NMX_F_PE_EVAL)[c] = A.pe_eval;
+    // leapfrog end of the scalar-site rows (their partial dots join the totals last)
+    const VecCtx v{&a, ldc, cfg.dim, (size_t)cfg.dim * ldc, cfg.unit_mass != 0};
+    const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+#pragma unroll
+    for (int i = 0; i < M::NSCALAR; ++i) {
+      const size_t idx = (size_t)m.scalar_row(i) * ldc + c;
+      AV(NMX_F_G_EVAL)[idx] = gs[i];
+      LeafIn x;
+      x.g = gs[i];
+      if (is_nuts) {
+        leaf_load<true, true, false>(v, A, idx, x);
+        leaf_store<true, true>(v, A, S.step_eff, idx, x, red);
+      } else {
+        leaf_load<false, true, false>(v, A, idx, x);
+        leaf_store<false, true>(v, A, S.step_eff, idx, x, red);
+      }
+    }
+  }
+  leaf_phase(cfg, S, A, A.leaf ? 0.5f * (T[0] + red[0]) : 0.0f, seed, gch);
+  tree_phase(
+      cfg, S, A, [&](int i, int side) { return T[(size_t)(1 + 2 * i + side) * ldc] + red[1 + 2 * i + side]; },
+      [&](int side) { return T[(size_t)(1 + 2 * MAXD + side) * ldc] + red[1 + 2 * MAXD + side]; }, seed, gch,
+      W.p.fields, c, true);
+  if (valid) {
+    AI(NMX_F_ACTION)[c] = pack_act(A);
+    AI(NMX_F_SLOT)[c] = A.slot;
+    AI(NMX_F_ACT_WFN)[c] = A.wfn;
+  }
+  end_step(cfg, a, c, valid, ph_in, S, A, false);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1537,4 +1770,61 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   else
     hipLaunchKernelGGL((k_nuts_step<8, STEP_CPW>), dim3(cfg->ldc / STEP_CPW), dim3(512), 0, s, args);
   return nmx_check_launch("k_nuts_step");
+}
+
+extern "C" size_t nmx_nuts_wide_model_workspace_bytes(int dim, int num_chains) {
+  const int ldc = ldc_of(num_chains);
+  if (num_slices(dim) == 0) return 0;
+  return wide_ws_part_bytes(dim, ldc) + wide_ws_tot_bytes(ldc) + align_up((size_t)(ldc / 64) * 4);
+}
+
+namespace {
+template <class M>
+int launch_wide_model(const WideArgs& w, const M& m, char* ws, int ldc, hipStream_t s) {
+  float* ppart = (float*)ws;
+  float* ptot = (float*)(ws + wide_ws_part_bytes(w.p.cfg.dim, ldc));
+  int* cnt = (int*)(ws + wide_ws_part_bytes(w.p.cfg.dim, ldc) + wide_ws_tot_bytes(ldc));
+  const int grid = ldc / 64;
+  hipLaunchKernelGGL(k_wide_leaf<M>, dim3(grid, w.ns), dim3(64 * WIDE_WAVES), 0, s, w, m, ppart);
+  hipLaunchKernelGGL(k_wide_rs<M>, dim3(grid, NPART + 1 + M::NSUM), dim3(64 * WIDE_SWAVES), 0, s, w, m,
+                     (const float*)ppart, ptot, cnt);
+  hipLaunchKernelGGL(k_wide_v2, dim3(grid, w.ns), dim3(64 * WIDE_WAVES), 0, s, w);
+  return nmx_check_launch("nmx_nuts_step_wide_model");
+}
+}  // namespace
+
+extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                                        const int8_t* transform, int model, const float* data, int n,
+                                        void* workspace, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!arena || !workspace) return nmx_fail(NMX_ERR_INVALID, "arena / workspace is NULL");
+  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+    return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
+  const int ns = num_slices(cfg->dim);
+  if (ns == 0) return nmx_fail(NMX_ERR_INVALID, "step_wide_model: dim %d uses the fused step (dim < %d)", cfg->dim,
+                               WIDE_MIN_D);
+  StepArgs args;
+  args.a = arena_of(cfg, arena);
+  args.cfg = *cfg;
+  args.samples = samples;
+  args.fields = fields;
+  args.transform = transform;
+  const WideArgs w{args, ns, slice_width(cfg->dim)};
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  switch (model) {
+    case NMX_WIDE_STOCHASTIC_VOLATILITY:
+      if (!data || n <= 1 || n + 2 != cfg->dim)
+        return nmx_fail(NMX_ERR_INVALID, "step_wide_model: stochastic volatility needs returns[T], dim == T + 2");
+      return launch_wide_model(w, NmxWideSV{data, n}, ws, cfg->ldc, s);
+    case NMX_WIDE_FUNNEL:
+      if (n != cfg->dim) return nmx_fail(NMX_ERR_INVALID, "step_wide_model: funnel needs n == dim");
+      return launch_wide_model(w, NmxWideFunnel{n}, ws, cfg->ldc, s);
+    case NMX_WIDE_FUNNEL_NONCENTERED:
+      if (n != cfg->dim) return nmx_fail(NMX_ERR_INVALID, "step_wide_model: funnel_noncentered needs n == dim");
+      return launch_wide_model(w, NmxWideFunnelNC{n}, ws, cfg->ldc, s);
+    default:
+      return nmx_fail(NMX_ERR_INVALID, "step_wide_model: unknown model %d", model);
+  }
 }

@@ -78,6 +78,9 @@ class Engine:
     # one-launch persistent schedule for one-wave models (False: the launched loop; tests
     # compare the two)
     persistent = True
+    # D-split models: the step fused with the potential (nmx_nuts_step_wide_model; False: the
+    # launched potential + step loop, which tests compare it with)
+    fused_wide = True
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
@@ -119,6 +122,7 @@ class Engine:
         # be resumed without copying the arena back (MCMC.run after warmup, kernel.sample)
         self.generation = 0
         self._pool = None  # dense pooled adaptation: (window, PooledCovariance) across run() calls
+        self._wide_ws = None  # nmx_nuts_step_wide_model workspace (zero-filled once)
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
 
@@ -441,6 +445,14 @@ class Engine:
         fn = getattr(self.potential, "small_model", None)
         return fn() if fn is not None else None
 
+    def _wide_model(self):
+        """(model id, data, n) when the step can run fused with a D-split model's potential
+        (nmx_nuts_step_wide_model: three launches per leaf instead of six)."""
+        if self.dense or not self.fused_wide or lib().nmx_nuts_num_slices(self.D) == 0:
+            return None
+        fn = getattr(self.potential, "wide_model", None)
+        return fn() if fn is not None else None
+
     def _run_segment(self, a, b, seed, cstart, thinning, S, samples, fields, poll_every, s, max_launches):
         """Transitions [a, b) of every chain; collection slots per (cstart, thinning, S)."""
         self._fill_cfg(a, b, self.num_warmup, seed, cstart, thinning, S)
@@ -479,8 +491,18 @@ class Engine:
         lists = self.eval_lists
         for b in lists:
             b.num_chains = self.C
+        wide = self._wide_model()
+        if wide is not None:
+            model, data, n = wide
+            if self._wide_ws is None:
+                nb = lib().nmx_nuts_wide_model_workspace_bytes(self.D, self.C)
+                self._wide_ws = torch.zeros(nb, dtype=torch.uint8, device=self.device)
+            wstep, dp, wsp = lib().nmx_nuts_step_wide_model, ptr(data), ptr(self._wide_ws)
         while True:
             for _ in range(poll_every):
+                if wide is not None:
+                    check(wstep(cfgp, arena, sp, fp, tp, model, dp, n, wsp, s), "nmx_nuts_step_wide_model")
+                    continue
                 evaluate(lists[parity], s)
                 parity ^= 1
                 cfg.parity = parity

@@ -77,6 +77,7 @@ class NutsConfig(ctypes.Structure):
 
 
 SMALL_DIAG_NORMAL, SMALL_EIGHT_SCHOOLS = 1, 2  # nmx_nuts_run_small models
+WIDE_SV, WIDE_FUNNEL, WIDE_FUNNEL_NC = 1, 2, 3  # nmx_nuts_step_wide_model models
 
 
 class EvalBatch(ctypes.Structure):
@@ -114,6 +115,8 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_predict_normal": (c_int, [c_vp, c_vp, c_int, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_predict_bnn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_nuts_step": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nmx_nuts_wide_model_workspace_bytes": (c_size, [c_int, c_int]),
+    "nmx_nuts_step_wide_model": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "nmx_pe_diag_normal": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_eight_schools": (c_int, [c_vp, c_vp, c_int, _evp, c_vp]),
     "nmx_pe_stochastic_volatility": (c_int, [c_vp, c_int, _evp, c_vp, c_vp]),

@@ -179,6 +179,10 @@ class StochasticVolatility(Potential):
         """Algorithmic HBM bytes per chain evaluation: read z, write grad (f32)."""
         return 2 * 4 * self.dim
 
+    def wide_model(self):
+        """Model of the wide step fused with this potential (nmx_nuts_step_wide_model)."""
+        return native.WIDE_SV, self.r, self.T
+
 
 class Funnel(Potential):
     """examples/funnel.py:44-46, centred: y ~ N(0, 3), x ~ N(0, exp(y/2))^(dim-1)."""
@@ -193,6 +197,9 @@ class Funnel(Potential):
 
     def evaluate(self, ev, stream):
         check(lib().nmx_pe_funnel(self.dim, ctypes.byref(ev), ptr(self.workspace), stream), "nmx_pe_funnel")
+
+    def wide_model(self):
+        return native.WIDE_FUNNEL, None, self.dim
 
     def bytes_per_eval(self):
         return 2 * 4 * self.dim
@@ -214,6 +221,9 @@ class FunnelNonCentered(Potential):
     def evaluate(self, ev, stream):
         check(lib().nmx_pe_funnel_noncentered(self.dim, ctypes.byref(ev), ptr(self.workspace), stream),
               "nmx_pe_funnel_noncentered")
+
+    def wide_model(self):
+        return native.WIDE_FUNNEL_NC, None, self.dim
 
     def deterministic(self, sites):
         # reparam.py:140-142: value = loc + scale ** (1 - centered) * (decentered - centered * loc)

@@ -127,8 +127,14 @@ def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None,
         out["roofline"] = {"bound": "mfma", "achieved_tflops": round(tf, 2), "peak": round(peak, 1),
                            "frac": round(tf / peak, 3)}
     if bytes_per_leapfrog:
-        gbs = bytes_per_leapfrog * ns / (pot_ms * 1e-3) / 1e9
-        out["roofline"] = {"bound": "hbm", "achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 3)}
+        # SURVEY.md §8d (C2 diag / C4): algorithmic bytes per chain-leapfrog 7 D x 4 B (z, r, g
+        # read + write, inverse mass read) over the sampling wall time (the whole step loop)
+        gbs = 7 * 4 * eng.D * ns / wall / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 3),
+                           "basis": "7*D*4 B per chain-leapfrog / sampling wall time"}
+        if pot_ms > 0:  # launched loop: the potential kernels alone (read z, write grad)
+            out["roofline"]["potential_GBs"] = round(bytes_per_leapfrog * ns / (pot_ms * 1e-3) / 1e9, 1)
+        out["fused_wide"] = launches == 0
     print(json.dumps(out), flush=True)
     return mcmc
 
@@ -143,7 +149,14 @@ def main():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--max-tree-depth", type=int, default=10)
     p.add_argument("--dense", type=int, default=1)
+    p.add_argument("--launched", action="store_true", help="wide models: potential + step loop (A/B)")
+    p.add_argument("--lib", default=None, help="A/B: load this build of libnumpyro_amd.so")
     a = p.parse_args()
+    if a.lib:
+        native.LIB_PATH = os.path.abspath(a.lib)
+    if a.launched:
+        from numpyro_amd.engine import Engine
+        Engine.fused_wide = False
     if a.what == "gemm":
         D = int(a.rest[0]) if a.rest else 10000
         C = int(a.rest[1]) if len(a.rest) > 1 else 4096

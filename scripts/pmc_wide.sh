@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/w" -o p 
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES --output-format csv -d "$O/s" -o p -- \
   python3 scripts/bench_configs.py $args > "$O/s.log" 2>&1 || exit $?
-for k in k_wide_v1 k_wide_v2 k_funnel_part k_sv_part; do
+for k in k_wide_v1 k_wide_v2 k_wide_part k_wide_leaf k_wide_rs; do
   echo "== $k"; python3 scripts/pmc_summary.py "$O" "$k"
 done > "$O/summary.txt"
 rm -rf "$O/f" "$O/w" "$O/s"  # per-dispatch CSVs exceed what gpurun copies back
