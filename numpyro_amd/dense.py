@@ -17,10 +17,12 @@ z = mu + T w before, g_w = T^T g_z after.  Results equal the reference's in exac
 arithmetic; in f32 they differ by rounding (the parity test follows the oracle's dense
 path at fixed step size).
 
-Adaptation is pooled across all chains of the job (an opt-in deviation, SURVEY.md §8a
-a18): at the end of every middle adaptation window the covariance of every chain's
-samples in that window (all ranks, reduced over RCCL) replaces M^-1 for every chain,
-regularised as in the reference with n = the pooled sample count.
+Adaptation is per chain, as the reference's vmapped init_kernel does (hmc.py:790-798), when
+the per-chain matrices fit (dim <= CHAIN_DENSE_MAX_D): ChainWhitenedPotential / ChainWelford.
+Otherwise dense_mass="pooled" is the explicit, warned opt-in: at the end of
+every middle adaptation window the covariance of every chain's samples in that window (all
+ranks, reduced over RCCL) replaces M^-1 for every chain, regularised as in the reference with
+n = the pooled sample count (PooledCovariance).
 """
 from __future__ import annotations
 

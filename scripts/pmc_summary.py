@@ -27,8 +27,8 @@ if w:
               "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_MISC"):
         if k in avg:
             print(f"{k} / WAVE_CYCLES = {avg[k] / w:.3f}")
-if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg and "SQ_BUSY_CU_CYCLES" in avg:
-    pass
-if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "SQ_BUSY_CYCLES" in avg:
-    print(f"MFMA_BUSY / (BUSY_CYCLES x 256 CU x 4 SIMD / 8 XCD?) raw ratio = "
-          f"{avg['SQ_VALU_MFMA_BUSY_CYCLES'] / avg['SQ_BUSY_CYCLES']:.3f}")
+if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
+    # SQ_VALU_MFMA_BUSY_CYCLES counts cycles (32 per 32x32x16 bf16 MFMA, MI355X_MICROARCH.md)
+    # summed over SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = GRBM / 8
+    busy = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 256 * 4)
+    print(f"MFMA pipe busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCD x 1024 SIMD) = {busy:.3f}")
