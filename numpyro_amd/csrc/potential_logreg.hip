@@ -305,8 +305,7 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 }
 
 // Software-pipelined: GEMM1 of tile k+1 is issued beside the epilogue of tile k (they are
-// independent), then GEMM2 of tile k.  SCHED 6 hand-interleaves the two (same arithmetic in
-// the same order: bitwise equal results).
+// independent), then GEMM2 of tile k.  SCHED 0 adds the igrouplp placement hints below.
 //
 template <int KB, int DT, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
@@ -408,49 +407,8 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         // the epilogue of tile k
         const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) & 1) * NA * 1024) + lane;
         float res[16];
-        if constexpr (SCHED == 6 && KB == 4) {
-          // Hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with
-          // row pairs of tile k's epilogue, which fill the MFMAs' dependency stalls.
-          // sched_barrier(0) pins the order; the operations and their per-value order equal
-          // x3_gemm1 / x3_epilogue (bitwise equal results).
-#pragma unroll
-          for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
-          float lin = 0.0f;
-          f32x2 prod = {1.0f, 1.0f};
-          bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
-#pragma unroll
-          for (int kb = 0; kb < KB; ++kb) {
-            bf16x8 n1, n2, n3;
-            if (kb + 1 < KB) {
-              n1 = fa[(kb + 1) * 64];
-              n2 = fa[(KB + kb + 1) * 64];
-              n3 = fa[(2 * KB + kb + 1) * 64];
-            }
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
-            x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
-            __builtin_amdgcn_sched_barrier(0);
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
-            x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
-            __builtin_amdgcn_sched_barrier(0);
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (kb + 1 < KB) {
-              a1 = n1;
-              a2 = n2;
-              a3 = n3;
-            }
-          }
-          x3_epi_finish(lin, prod, pe);
-        } else {
-          nxt = x3_gemm1<KB>(fa, z1, z2, z3);
-          x3_epilogue(acc, y4, res, pe);
-        }
+        nxt = x3_gemm1<KB>(fa, z1, z2, z3);
+        x3_epilogue(acc, y4, res, pe);
         x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
         if constexpr (SCHED == 0) {
           // scheduling hints (LLVM igrouplp): each GEMM1(k+1) MFMA followed by 5 VALU (tile k's
@@ -502,6 +460,243 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
   if (ct * 128 >= npos) return;
   x3_item<KB, DT, SCHED>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
+}
+
+// ---------------------------------------------------------------------------------------
+// Tail form with split roles (launches over <= X3_TAIL_TILES chain groups).  In a NUTS run's
+// tail one wave per chain tile and split ran the dependent GEMM1 -> epilogue -> split ->
+// GEMM2 chain of each of its tiles alone on its SIMD (~2.9k cycles a tile for 1.5k of MFMA
+// work).  Here a workgroup of 8 waves pairs every chain tile t with two waves on different
+// SIMDs: wave t (role A) runs GEMM1 of tile k+1 beside the epilogue of tile k (the
+// hand-interleaved order below) and hands the residual R(k) to its role-B wave (on another
+// SIMD) through LDS; B splits it and runs GEMM2(k) one tile behind.  Every product, its operands and
+// its accumulation order are those of x3_item (bitwise equal results; the residual crosses
+// LDS as an exact f32 copy).  LDS: the A ring (2 slots) as before, a 3-slot B ring (B still
+// reads tile k-1 while tile k+1 lands), two residual slots per chain tile.  One workgroup per
+// CU in these launches.
+__device__ __forceinline__ void x3_res_store(char* base, const float (&res)[16]) {
+  const unsigned a = (unsigned)(size_t)((__attribute__((address_space(3))) char*)base);
+  const f32x4 v0 = {res[0], res[1], res[2], res[3]}, v1 = {res[4], res[5], res[6], res[7]};
+  const f32x4 v2 = {res[8], res[9], res[10], res[11]}, v3 = {res[12], res[13], res[14], res[15]};
+  asm volatile(
+      "ds_write_b128 %0, %1\n\t"
+      "ds_write_b128 %0, %2 offset:1024\n\t"
+      "ds_write_b128 %0, %3 offset:2048\n\t"
+      "ds_write_b128 %0, %4 offset:3072" ::"v"(a), "v"(v0), "v"(v1), "v"(v2), "v"(v3)
+      : "memory");
+}
+__device__ __forceinline__ void x3_res_load(const char* base, float (&res)[16]) {
+  const unsigned a = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)base);
+  f32x4 v[4];
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(a)
+      : "memory");
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) res[4 * q + j] = v[q][j];
+}
+
+// workgroup barrier after this wave's LDS-DMA loads and LDS writes have completed
+__device__ __forceinline__ void x3_roles_barrier() {
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8) | (0 << 14));  // vmcnt(0) lgkmcnt(0)
+  asm volatile("s_barrier" ::: "memory");
+}
+
+constexpr int X3_ROLE_WAVES = 8;
+// A-ring slots: X tiles are prefetched PA - 1 tiles ahead (the B ring has PA + 1 slots); 2, 3
+// and 4 measured equal (the tail launch streams the 465 MB of split tiles at ~7 TB/s)
+constexpr int X3_ROLE_PA = 2;
+
+template <int KB, int DT, int PA>
+inline size_t x3_roles_lds_bytes() {
+  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB, NBP = NP - NA;
+  return (size_t)(PA * NA + (PA + 1) * NBP) * 1024 + (size_t)2 * 4 * 4096;
+}
+
+template <int KB, int DT, int PA>
+__global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const char* __restrict__ Xq,
+                                                                         int64_t ntiles, int D, int S, int Gt,
+                                                                         nmx_eval_batch ev, float* __restrict__ gpart,
+                                                                         double* __restrict__ pepart) {
+  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB, NBP = NP - NA;
+  static_assert(KB == 4, "role-split tail form: D in (48, 64]");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = blockIdx.x;
+  const int qb = b >> 3;
+  const int ct = qb % Gt;
+  const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
+  if (ct * 128 >= npos) return;
+  const int split = (qb / Gt) * 8 + (b & 7);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool roleA = w < 4;
+  // chain tile of the group: A waves 0-3 own tiles 0-3; B waves 4-7 own tiles 2, 3, 0, 1, so
+  // with waves dealt to SIMDs w mod 4 the two waves of tile 0 / 1 (the tail's usual 1-2 active
+  // tiles) sit on different SIMDs and their MFMA streams run in parallel
+  const int t = roleA ? w : ((w + 2) & 3);
+  const int h = lane >> 5;
+  const int l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int pos = (ct * 4 + t) * 32 + l31;
+  const int c = pos < ldc ? nmx_eval_chain(ev, pos) : -1;
+  const bool active = __any(c >= 0);  // wave-uniform, equal for the A and B waves of a tile
+  if (!__syncthreads_or(active)) return;
+
+  const int64_t per = (ntiles + S - 1) / S;
+  const int64_t t0 = min((int64_t)split * per, ntiles);
+  const int64_t t1 = min(t0 + per, ntiles);
+  const int nt = (int)(t1 - t0);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
+  constexpr int PB = PA + 1;
+  char* aring = lds;
+  char* bring = lds + PA * NA * 1024;
+  char* rring = bring + PB * NBP * 1024;  // [slot][tile][4 KB]
+  auto issue_a = [&](int k) {
+    char* dst = aring + (k % PA) * NA * 1024;
+#pragma unroll
+    for (int j = 0; j < (NA + X3_ROLE_WAVES - 1) / X3_ROLE_WAVES; ++j) {
+      const int i = w + X3_ROLE_WAVES * j;
+      if (i < NA)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                                 lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
+    }
+  };
+  auto issue_b = [&](int k) {
+    char* dst = bring + (k % PB) * NBP * 1024;
+#pragma unroll
+    for (int j = 0; j < (NBP + X3_ROLE_WAVES - 1) / X3_ROLE_WAVES; ++j) {
+      const int i = w + X3_ROLE_WAVES * j;
+      if (i < NBP)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                                 lane * 16, (unsigned)((k * NP + NA + i) * 1024), 0, 0);
+    }
+  };
+  char* const rmine = rring + t * 4096 + lane * 16;  // + slot * 4 * 4096
+
+  if (roleA) {
+    // ---- role A: GEMM1 + epilogue, hands R(k) to its B wave --------------------------------
+    const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc((void*)ev.z, 0, D * ldc * 4, 0x00020000);
+    const unsigned zoff = c >= 0 ? (unsigned)((8 * h * ldc + c) * 4) : 0xFFFFFFF0u;
+    bf16x8 z1[KB], z2[KB], z3[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zoff, (16 * kb + j) * ldc * 4, 0));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= -LOG2E;
+      split3(v, z1[kb], z2[kb], z3[kb]);
+    }
+    double pe = 0.0;
+    if (nt > 0) {
+      issue_a(0);
+      x3_roles_barrier();  // A(0) is in
+      for (int j = 1; j < PA && j < nt; ++j) issue_a(j);
+      for (int j = 0; j < PA - 1 && j < nt; ++j) issue_b(j);
+      f32x16 accA, accB;
+      if (active) accA = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      auto stepA = [&](int k, const f32x16& acc, f32x16& nxt) {
+        x3_roles_barrier();  // A(k+1), B(k) landed; R slot k&1 was read by B in iteration k-1
+        if (k + PA < nt) issue_a(k + PA);
+        if (k + PA - 1 < nt) issue_b(k + PA - 1);
+        if (!active) return;
+        f32x4 y4[4];
+        x3_labels(bring + (k % PB) * NBP * 1024 + (NBP - 1) * 1024, h, y4);
+        x3_labels_wait(y4);
+        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % PA) * NA * 1024) + lane;
+        float res[16];
+        // hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with row
+        // pairs of tile k's epilogue; sched_barrier(0) pins the order; the operations and their
+        // per-value order equal x3_gemm1 / x3_epilogue (bitwise equal results)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
+        float lin = 0.0f;
+        f32x2 prod = {1.0f, 1.0f};
+        bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          bf16x8 n1, n2, n3;
+          if (kb + 1 < KB) {
+            n1 = fa[(kb + 1) * 64];
+            n2 = fa[(KB + kb + 1) * 64];
+            n3 = fa[(2 * KB + kb + 1) * 64];
+          }
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
+          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
+          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (kb + 1 < KB) {
+            a1 = n1;
+            a2 = n2;
+            a3 = n3;
+          }
+        }
+        x3_epi_finish(lin, prod, pe);
+        x3_res_store(rmine + (k & 1) * 4 * 4096, res);
+      };
+      for (int k = 0; k < nt; k += 2) {
+        stepA(k, accA, accB);
+        if (k + 1 < nt) stepA(k + 1, accB, accA);
+      }
+      x3_roles_barrier();  // R(nt-1) handed over
+    }
+    if (!active || pos >= ldc) return;
+    const double p = pe + __shfl_xor(pe, 32);
+    if (h == 0) pepart[(size_t)split * ldc + pos] = p;
+  } else {
+    // ---- role B: split R(k-1) + GEMM2(k-1) --------------------------------------------------
+    f32x16 g[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g[dt][r] = 0.0f;
+    auto gemm2 = [&](int k) {  // GEMM2 of tile k
+      float res[16];
+      x3_res_load(rmine + (k & 1) * 4 * 4096, res);
+      x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bring + (k % PB) * NBP * 1024) - NA * 64 + lane, res, g);
+    };
+    if (nt > 0) {
+      issue_a(0);
+      x3_roles_barrier();
+      for (int j = 1; j < PA && j < nt; ++j) issue_a(j);
+      for (int j = 0; j < PA - 1 && j < nt; ++j) issue_b(j);
+      for (int k = 0; k < nt; ++k) {
+        x3_roles_barrier();
+        if (k + PA < nt) issue_a(k + PA);
+        if (k + PA - 1 < nt) issue_b(k + PA - 1);
+        if (active && k > 0) gemm2(k - 1);
+      }
+      x3_roles_barrier();
+      if (active) gemm2(nt - 1);
+    }
+    if (!active || pos >= ldc) return;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = 32 * dt + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = g[dt][r];
+      }
+  }
 }
 
 // Sum of slots sp0 .. sp1-1 at stride st (in slot order; 32 loads issued ahead of their adds)
@@ -572,10 +767,9 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
   }
 }
 
-// Launches over at most this many 128-chain tiles (one or two workgroups per CU, one wave
-// per SIMD) run the hand-interleaved form: GEMM1(k+1)'s MFMAs alternate with tile k's
-// epilogue rows -- the same arithmetic in the same order (bitwise equal), with no other wave on
-// the SIMD to fill the gaps (5-8% faster at 16-256 chains).
+// Launches over at most this many 128-chain groups (a NUTS run's tail: one workgroup per split
+// and CU) run the role-split form k_logreg_x3_roles (bitwise equal): 0.083 vs 0.105 ms per
+// evaluation at 16-64 chains, incl. the finalize.
 constexpr int X3_TAIL_TILES = 2;
 
 int check_ev(const nmx_eval_batch* ev) {
@@ -639,7 +833,9 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const int Gt = (nb + 127) / 128;
   const dim3 grid(Gt * S), blk(256);
   if (KB == 4 && Gt <= X3_TAIL_TILES)
-    hipLaunchKernelGGL((k_logreg_x3<4, 2, 2, 6>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
+                       (x3_roles_lds_bytes<4, 2, X3_ROLE_PA>()), s, Xq,
+                       nt, dim, S, Gt, *ev, gpart, pepart);
   else if (KB == 4)
     hipLaunchKernelGGL((k_logreg_x3<4, 2, 3, 0>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
   else if (KB == 3)

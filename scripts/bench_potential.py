@@ -1,11 +1,13 @@
 """Time the fused logreg potential alone (all chains active).
-usage: python scripts/bench_potential.py [ignored] [chains,...]"""
+usage: python scripts/bench_potential.py [ignored] [chains,...] [libnumpyro_amd.so of an A/B build]"""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from numpyro_amd import datasets, native
 from numpyro_amd.potentials import LogisticRegression
 
+if len(sys.argv) > 3:
+    native.LIB_PATH = os.path.abspath(sys.argv[3])
 variants = ["d"]
 chains = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "4096,1024").split(",")]
 X, y = datasets.covtype_synthetic(seed=0)
