@@ -371,6 +371,10 @@ int nmx_predict_bnn(const float* X, int n, int dx, int dh, int dy, const float* 
 int nmx_selftest_philox(const uint32_t* ctr_key, uint32_t* out, int n, void* stream);
 /* C[32][32] = A[32][K] * B[K][32] through v_mfma_f32_32x32x2_f32 (fragment-layout probe). */
 int nmx_selftest_mfma(const float* A, const float* B, float* C, int K, void* stream);
+/* Probe of the debug build's device checks (NMX_DCHECK): value != 0 prints a failed check from
+ * the device in libnumpyro_amd_debug.so.  Returns 1 in the debug build, 0 in the release build,
+ * a negative status on a launch error. */
+int nmx_selftest_dcheck(int value, void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,11 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libnumpyro_amd.so")
+# debug build: the NMX_DCHECK bounds / invariant checks compiled in (nmx_common.h), -g;
+# loaded instead of the release library when NUMPYRO_AMD_DEBUG=1 (native.py)
+DEBUG_OBJ_DIR = os.path.join(ROOT, "build", "obj_debug")
+DEBUG_LIB_PATH = os.path.join(LIB_DIR, "libnumpyro_amd_debug.so")
+DEBUG_FLAGS = ["-DNMX_DEBUG", "-g"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -45,44 +50,48 @@ def _stale(obj: str, src: str, headers) -> bool:
     return any(os.path.getmtime(p) > t for p in [src, *headers])
 
 
-def _compile(src: str, obj: str) -> None:
+def _compile(src: str, obj: str, extra=()) -> None:
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC, *COMMON_FLAGS, *lang, "-c", src, "-o", obj]
+    cmd = [HIPCC, *COMMON_FLAGS, *extra, *lang, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> str:
-    os.makedirs(OBJ_DIR, exist_ok=True)
+def build(verbose: bool = False, jobs: int | None = None, debug: bool = False) -> str:
+    obj_dir, lib_path = (DEBUG_OBJ_DIR, DEBUG_LIB_PATH) if debug else (OBJ_DIR, LIB_PATH)
+    extra = DEBUG_FLAGS if debug else ()
+    os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     headers = _headers()
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        o = os.path.join(obj_dir, os.path.basename(s) + ".o")
         objs.append(o)
         if _stale(o, s, headers):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = [ex.submit(_compile, s, o) for s, o in todo]
+            futs = [ex.submit(_compile, s, o, extra) for s, o in todo]
             for f in futs:
                 f.result()
             if verbose:
                 for s, _ in todo:
                     print("compiled", os.path.relpath(s, ROOT))
-    if todo or not os.path.exists(LIB_PATH):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+    if todo or not os.path.exists(lib_path):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print("linked", os.path.relpath(LIB_PATH, ROOT))
-    return LIB_PATH
+            print("linked", os.path.relpath(lib_path, ROOT))
+    return lib_path
 
 
 if __name__ == "__main__":
     build(verbose=True)
+    if "--debug" in sys.argv:
+        build(verbose=True, debug=True)
     sys.exit(0)

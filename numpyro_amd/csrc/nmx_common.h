@@ -14,6 +14,23 @@
 
 #define NMX_HD __host__ __device__ __forceinline__
 
+// Bounds / invariant checks of the debug build (numpyro_amd.build(debug=True), -DNMX_DEBUG;
+// loaded with NUMPYRO_AMD_DEBUG=1): a failed check prints its location from the device (the
+// tests scan the output) and the kernel continues -- no trap, so a bad index shows up as a
+// message, not as a GPU fault.  Compiled out of the release library.
+#ifdef NMX_DEBUG
+#include <stdio.h>
+#define NMX_DCHECK(cond)                                                                           \
+  do {                                                                                             \
+    if (!(cond)) printf("NMX_DCHECK failed %s:%d: %s (block %d thread %d)\n", __FILE__, __LINE__, #cond, \
+                        (int)blockIdx.x, (int)threadIdx.x);                                        \
+  } while (0)
+#else
+#define NMX_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 // RNG event tags (high byte of counter word 2).
 enum nmx_rng_event : uint32_t {
   NMX_EV_MOMENTUM = 1u,   // momentum draw, word2 low bits = block of 4 coordinates
@@ -101,7 +118,12 @@ __device__ __forceinline__ float nmx_sigmoid(float x) {
 
 // Chain evaluated at batch position `pos` of a potential launch, or -1.
 __device__ __forceinline__ int nmx_eval_chain(const nmx_eval_batch& ev, int pos) {
-  if (ev.active_idx) return pos < *ev.active_count ? ev.active_idx[pos] : -1;
+  if (ev.active_idx) {
+    if (pos >= *ev.active_count) return -1;
+    const int c = ev.active_idx[pos];
+    NMX_DCHECK(c >= 0 && c < ev.ldc && pos < ev.ldc);
+    return c;
+  }
   if (pos >= ev.num_chains) return -1;
   if (ev.phase && ev.phase[pos] < NMX_PH_LEAF) return -1;
   return pos;

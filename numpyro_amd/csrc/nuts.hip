@@ -299,6 +299,8 @@ __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Aren
   A.j = (A.leaf && is_nuts) ? S.depth : 0;
   if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);  // :1036
   A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
+  // the checkpoint rows a leaf touches exist: imax <= depth < max_depth_alloc
+  NMX_DCHECK(!(A.leaf && is_nuts) || (A.imax < cfg.max_depth_alloc && A.j < cfg.max_depth_alloc));
   return ph;
 }
 
@@ -458,6 +460,7 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
         if (s < cfg.collection_size) A.slot = s;
       }
     }
+    NMX_DCHECK(A.slot < cfg.collection_size);
     if (A.slot >= 0 && writer) {
       float* F = fields + (size_t)A.slot * NMX_NUM_COLLECT * ldc;
       F[NMX_C_POTENTIAL_ENERGY * ldc + c] = S.pe;
@@ -538,6 +541,7 @@ __device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena
     base = __shfl(base, __builtin_ctzll(m));
     if (pend) {
       const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
+      NMX_DCHECK(pos < cfg.num_chains);
       a.active_idx[(size_t)cfg.parity * cfg.ldc + pos] = c;
     }
   }
@@ -1315,8 +1319,11 @@ __global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_rs(WideArgs W, M m, c
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    last_block = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NE - 1;
+  if (threadIdx.x == 0) {
+    const int ticket = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    NMX_DCHECK(ticket >= 0 && ticket < NE);  // the counters start at zero and are left at zero
+    last_block = ticket == NE - 1;
+  }
   __syncthreads();
   if (!last_block) return;
   if (threadIdx.x == 0) {

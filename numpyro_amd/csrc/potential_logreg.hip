@@ -327,6 +327,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
   const int64_t t0 = min((int64_t)split * per, ntiles);
   const int64_t t1 = min(t0 + per, ntiles);
   const int nt = (int)(t1 - t0);
+  NMX_DCHECK(split < S && t1 <= ntiles && nt >= 0);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
 

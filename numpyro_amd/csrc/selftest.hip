@@ -53,3 +53,17 @@ extern "C" int nmx_selftest_mfma(const float* A, const float* B, float* C, int K
   hipLaunchKernelGGL(k_mfma_probe, dim3(1), dim3(64), 0, stream, A, B, C, K);
   return nmx_check_launch("k_mfma_probe");
 }
+
+// NMX_DCHECK(value == 0) in one thread: prints a failed check in the debug build, nothing in
+// the release build (where the check is compiled out).  Returns 1 in the debug build.
+__global__ void k_dcheck_probe(int value) { NMX_DCHECK(value == 0); }
+
+extern "C" int nmx_selftest_dcheck(int value, void* stream) {
+  hipLaunchKernelGGL(k_dcheck_probe, dim3(1), dim3(1), 0, (hipStream_t)stream, value);
+  if (int st = nmx_check_launch("k_dcheck_probe")) return -st;
+#ifdef NMX_DEBUG
+  return 1;
+#else
+  return 0;
+#endif
+}

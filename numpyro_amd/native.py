@@ -15,7 +15,9 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libnumpyro_amd.so")
+# NUMPYRO_AMD_DEBUG=1: the debug build (bounds / invariant checks, numpyro_amd.build(debug=True))
+LIB_PATH = os.path.join(_HERE, "_lib", "libnumpyro_amd_debug.so" if os.environ.get("NUMPYRO_AMD_DEBUG") == "1"
+                        else "libnumpyro_amd.so")
 
 _lib = None
 
@@ -99,6 +101,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_struct_size": (c_size, [c_int]),
     "nmx_selftest_philox": (c_int, [c_vp, c_vp, c_int, c_vp]),
     "nmx_selftest_mfma": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
+    "nmx_selftest_dcheck": (c_int, [c_int, c_vp]),
     "nmx_nuts_arena_bytes": (c_size, [c_int, c_int, c_int, c_int]),
     "nmx_nuts_num_slices": (c_int, [c_int]),
     "nmx_nuts_field_info": (c_int, [c_int, c_int, c_int, c_int, c_int, _P(c_size), _P(c_size)]),
