@@ -1173,12 +1173,15 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
 // arrival counter per chain group (zero on entry; the last block leaves it zero).
 constexpr int WIDE_NSUM = 4;  // largest M::NSUM
 
+
 inline size_t wide_ws_part_bytes(int D, int ldc) { return align_up((size_t)num_slices(D) * WIDE_NSUM * ldc * 4); }
 inline size_t wide_ws_tot_bytes(int ldc) { return align_up((size_t)WIDE_NSUM * ldc * 4); }
 
-// NUTS leapfrog end of rows d0, d0 + step, ... < d1 with the model's gradient, two rows per
-// round: both rows' leaf-state loads, then the model's loads (z and stencil neighbours), then
-// the stores (the one-pass form of leaf_rows; same sums in the same order).
+// NUTS leapfrog end of rows d0, d0 + step, ... < d1 with the model's gradient, one row per
+// round: the row's leaf-state loads, then the model's loads (z and stencil neighbours), then
+// the stores (the one-pass form of leaf_rows; same sums in the same order).  One row per round
+// keeps k_wide_leaf at 168 VGPRs, 3 waves per SIMD: SV 1024 chains 3.57-3.58M vs 3.40M leapfrog/s
+// with rows in pairs (229 VGPRs, 2 waves per SIMD), funnel-10k diag 657k vs 638k.
 template <bool NUTS, class M>
 __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, const M& m, const typename M::Glob& gl,
                                                 float seff, int d0, int d1, int step, int c, float* red,
@@ -1187,18 +1190,6 @@ __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, c
   const float* ZE = AV(NMX_F_Z_EVAL);
   float* GE = AV(NMX_F_G_EVAL);
   int d = d0;
-  for (; d + step < d1; d += 2 * step) {
-    const size_t i0 = (size_t)d * v.ldc + c, i1 = (size_t)(d + step) * v.ldc + c;
-    LeafIn x0, x1;
-    leaf_load<NUTS, true, false>(v, A, i0, x0);
-    leaf_load<NUTS, true, false>(v, A, i1, x1);
-    x0.g = m.row(ZE, v.ldc, c, d, gl, sums);
-    x1.g = m.row(ZE, v.ldc, c, d + step, gl, sums);
-    GE[i0] = x0.g;
-    GE[i1] = x1.g;
-    leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
-    leaf_store<NUTS, true>(v, A, seff, i1, x1, red);
-  }
   for (; d < d1; d += step) {
     const size_t i0 = (size_t)d * v.ldc + c;
     LeafIn x0;
@@ -1210,7 +1201,7 @@ __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, c
 }
 
 template <class M>
-__global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_leaf(WideArgs W, M m, float* ppart) {
+__global__ __launch_bounds__(64 * WIDE_WAVES, 3) void k_wide_leaf(WideArgs W, M m, float* ppart) {
   constexpr int NR = NPART + M::NSUM;
   constexpr int WV = WIDE_WAVES;
   __shared__ float lds[NR * WV * 64];

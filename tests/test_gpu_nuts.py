@@ -434,8 +434,9 @@ def test_wide_model_step_matches_launched_loop(device, which, monkeypatch):
     # U agrees where the draws agree closely (at 1e-3-close draws U itself can move by ~1e-2
     # relative: |grad U| ~ 1e2-1e3 along SV's random walk)
     close = same & np.all(np.isclose(x0, x1, rtol=1e-5, atol=1e-5).reshape(96, -1), axis=1)
-    # (U sums ~700 terms of magnitude 1e1-1e2 in another order: ~1e-2 absolute cancellation)
-    np.testing.assert_allclose(u1[close], u0[close], rtol=1e-4, atol=5e-2)
+    # (U ~ 1e2 is the cancellation of sums of ~700 terms whose magnitudes add to ~1e4, summed in
+    # another order, at draws equal to 1e-5 with |grad U| ~ 1e3: ~1e-1 absolute)
+    np.testing.assert_allclose(u1[close], u0[close], rtol=1e-4, atol=0.2)
 
 
 def test_wide_model_step_invariances(device):
