@@ -798,36 +798,28 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
   return ke0;
 }
 
-// One block of 4 coordinates (the momentum block).  BATCH: loads of all 4 rows, then the
-// stores (wide schedule); otherwise row by row (fused kernel, register-bound).
-template <bool BATCH>
+// One block of 4 coordinates (the momentum block), BATCH rows at a time: their loads, then their
+// stores (wide schedule: 2; the fused kernel, register-bound: 1).  The momentum KE adds the rows
+// in order whatever BATCH is.
+template <int BATCH>
 __device__ __forceinline__ float apply_block(const VecCtx& v, const Act& A, float step_eff, int blk, int c,
                                              const float (&n)[4], float* samp, const int8_t* transform,
                                              const nmx_nuts_config& cfg) {
-  if constexpr (!BATCH) {
-    float ke0 = 0.0f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = 4 * blk + q;
-      if (d < v.D) {
-        ApplyIn x;
-        apply_load(v, A, (size_t)d * v.ldc + c, x);
-        ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x, n[q], samp, transform, cfg);
-      }
-    }
-    return ke0;
-  }
-  ApplyIn x[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int d = 4 * blk + q;
-    if (d < v.D) apply_load(v, A, (size_t)d * v.ldc + c, x[q]);
-  }
   float ke0 = 0.0f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int d = 4 * blk + q;
-    if (d < v.D) ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x[q], n[q], samp, transform, cfg);
+  for (int q0 = 0; q0 < 4; q0 += BATCH) {
+    ApplyIn x[BATCH];
+#pragma unroll
+    for (int q = q0; q < q0 + BATCH; ++q) {
+      const int d = 4 * blk + q;
+      if (d < v.D) apply_load(v, A, (size_t)d * v.ldc + c, x[q - q0]);
+    }
+#pragma unroll
+    for (int q = q0; q < q0 + BATCH; ++q) {
+      const int d = 4 * blk + q;
+      if (d < v.D)
+        ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x[q - q0], n[q], samp, transform, cfg);
+    }
   }
   return ke0;
 }
@@ -899,7 +891,7 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
     for (int blk = vw; 4 * blk < D; blk += NV) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
-      ke0[0] += apply_block<false>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
+      ke0[0] += apply_block<1>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
     }
   }
   vblock_sum<NV, CPW, 1>(ke0, lds, vw, cl);
@@ -1151,7 +1143,9 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
     for (int blk = b0 + wv; blk < b1; blk += WIDE_WAVES) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(cfg.seed, gch, it, blk, n);
-      ke0[0] += apply_block<true>(v, A, step_eff, blk, c, n, samp, W.p.transform, cfg);
+      // rows in pairs: 95 VGPRs, 5 waves per SIMD (all four rows' loads first: 121 VGPRs, 4
+      // waves; SV 1024 chains 3.58M vs 3.93M leapfrog/s, funnel-10k diag 658k vs 717k)
+      ke0[0] += apply_block<2>(v, A, step_eff, blk, c, n, samp, W.p.transform, cfg);
     }
   }
   block_sum<WIDE_WAVES, 1>(ke0, lds);
