@@ -48,6 +48,7 @@ def parse():
                    help="BASELINE.json secondary configs measured after the headline (comma list of c2 funnel-10k "
                         "dense, c3 BNN dense, c4 stochastic volatility; 'none' skips); c2/c3 are one-GPU configs "
                         "and run at --gpus 1 only, c4 shards its 8192 chains over the ranks")
+    p.add_argument("--lib", default=None, help="(experiments) load this build of the library instead")
     return p.parse_args()
 
 
@@ -227,6 +228,10 @@ def secondary_configs(which, rank, world, device):
 def main():
     t_start = time.perf_counter()
     args = parse()
+    if args.lib:
+        from numpyro_amd import native as _native
+
+        _native.LIB_PATH = os.path.abspath(args.lib)
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -831,6 +831,43 @@ __device__ __forceinline__ void momentum_block(uint64_t seed, uint32_t gch, int 
   nmx_box_muller(x.z, x.w, n[2], n[3]);
 }
 
+// Rows d0, d0 + step, ... of chain column c, BATCH rows per round: their loads, then the momentum
+// normals (the row's Philox block, recomputed per row: ALU that hides the loads' latency), then
+// their stores.  The fused kernel's form (TPC > 1): a chain's rows spread evenly over its lanes,
+// instead of momentum blocks of four (14 of 32 lanes busy at D = 55, four rounds each).
+template <int BATCH>
+__device__ __forceinline__ float apply_rows(const VecCtx& v, const Act& A, float step_eff, int d0, int step, int c,
+                                            uint64_t seed, uint32_t gch, int it, float* samp,
+                                            const int8_t* transform, const nmx_nuts_config& cfg) {
+  float ke0 = 0.0f;
+  for (int d = d0; d < v.D; d += BATCH * step) {
+    ApplyIn x[BATCH];
+#pragma unroll
+    for (int q = 0; q < BATCH; ++q) {
+      const int dq = d + q * step;
+      if (dq < v.D) apply_load(v, A, (size_t)dq * v.ldc + c, x[q]);
+    }
+    float n[BATCH];
+#pragma unroll
+    for (int q = 0; q < BATCH; ++q) {
+      const int dq = d + q * step;
+      n[q] = 0.0f;
+      if (A.start_iter && dq < v.D) {
+        float nb[4];
+        momentum_block(seed, gch, it, dq >> 2, nb);
+        const int j = dq & 3;
+        n[q] = j == 0 ? nb[0] : (j == 1 ? nb[1] : (j == 2 ? nb[2] : nb[3]));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BATCH; ++q) {
+      const int dq = d + q * step;
+      if (dq < v.D) ke0 += apply_store(v, A, step_eff, dq, (size_t)dq * v.ldc + c, x[q], n[q], samp, transform, cfg);
+    }
+  }
+  return ke0;
+}
+
 // ---- fused schedule ----------------------------------------------------------------------
 // One fused step for the chains of this block (LIST: append the chains whose next leaf is
 // pending to the compacted list; the persistent kernel evaluates inline instead).  A block
@@ -872,9 +909,17 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
   float red[NPART];
 #pragma unroll
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+#ifndef NMX_STEP_LROWS
+#define NMX_STEP_LROWS 1
+#endif
+#ifndef NMX_STEP_AROWS
+#define NMX_STEP_AROWS 1
+#endif
+  constexpr int LROWS = TPC > 1 ? (NMX_STEP_LROWS == 2 ? 2 : 1) : 1;
+  constexpr bool LPRE = TPC > 1 && NMX_STEP_LROWS >= 1;
   if (A.leaf) {
-    if (is_nuts) leaf_rows<true, 1>(v, A, seff, vw, D, NV, c, red);
-    else leaf_rows<false, 1>(v, A, seff, vw, D, NV, c, red);
+    if (is_nuts) leaf_rows<true, LROWS, LPRE>(v, A, seff, vw, D, NV, c, red);
+    else leaf_rows<false, LROWS, LPRE>(v, A, seff, vw, D, NV, c, red);
   }
   vblock_sum<NV, CPW, NPART>(red, lds, vw, cl);
   leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
@@ -888,10 +933,14 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
   if (vec2) {
     float* const samp = A.slot >= 0 ? P.samples + (size_t)A.slot * D * ldc : nullptr;
     const float step_eff = S.step_eff;
-    for (int blk = vw; 4 * blk < D; blk += NV) {
-      float n[4] = {0.f, 0.f, 0.f, 0.f};
-      if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
-      ke0[0] += apply_block<1>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
+    if constexpr (TPC > 1 && NMX_STEP_AROWS >= 1) {
+      ke0[0] = apply_rows<NMX_STEP_AROWS>(v, A, step_eff, vw, NV, c, seed, gch, S.it, samp, P.transform, cfg);
+    } else {
+      for (int blk = vw; 4 * blk < D; blk += NV) {
+        float n[4] = {0.f, 0.f, 0.f, 0.f};
+        if (A.start_iter) momentum_block(seed, gch, S.it, blk, n);
+        ke0[0] += apply_block<1>(v, A, step_eff, blk, c, n, samp, P.transform, cfg);
+      }
     }
   }
   vblock_sum<NV, CPW, 1>(ke0, lds, vw, cl);

@@ -1,10 +1,12 @@
 """Potential launch time with a compacted active list inside a wide batch (ldc = 4096), as in
 the tail of a NUTS run, vs a dense batch of the same chains.
-usage: python scripts/logreg_list_bench.py [counts]"""
+usage: python scripts/logreg_list_bench.py [counts] [lib]"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from numpyro_amd import datasets, native
+if len(sys.argv) > 2:
+    native.LIB_PATH = os.path.abspath(sys.argv[2])
 from numpyro_amd.potentials import LogisticRegression
 
 counts = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "1,32,69,128,256,512").split(",")]
