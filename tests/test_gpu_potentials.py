@@ -101,6 +101,30 @@ def test_logreg_split_invariance(device):
     np.testing.assert_array_equal(g_a[200:260], g_b)
 
 
+@pytest.mark.parametrize("n_rows", [4001, 70001, 581012])
+def test_logreg_tail_forms_are_bitwise_the_full_kernel(device, n_rows):
+    """Launches over <= 256 chains run the role-split tail form; the chains of a 300-chain
+    launch (the full split-bf16 kernel) get bitwise the same U / dU from it: one chain, one
+    chain tile, two chain groups; ragged row counts (a short last split, padded tile rows)
+    up to the covtype size."""
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(n_rows % 1000)
+    X = rs.randn(n_rows, 55).astype(np.float32)
+    y = (rs.rand(n_rows) < 0.4).astype(np.float32)
+    Z = rs.randn(300, 55).astype(np.float32) * 0.05
+    pot = LogisticRegression(X, y)
+    pe_a, g_a = _eval(pot, Z, device)
+    for lo, hi in ((7, 8), (200, 232), (0, 256)):
+        pe_b, g_b = _eval(pot, Z[lo:hi], device)
+        np.testing.assert_array_equal(pe_a[lo:hi], pe_b, err_msg=f"chains {lo}:{hi}")
+        np.testing.assert_array_equal(g_a[lo:hi], g_b, err_msg=f"chains {lo}:{hi}")
+    if n_rows <= 70001:
+        pe_r, g_r = OP.LogisticRegression(X, y).pe_grad_batch(Z[:8])
+        np.testing.assert_allclose(pe_a[:8], pe_r, rtol=2e-5)
+        np.testing.assert_allclose(g_a[:8], g_r, rtol=1e-3, atol=1e-2)
+
+
 def test_eight_schools_matches_oracle(device):
     from numpyro_amd.potentials import EightSchools
 
