@@ -32,7 +32,9 @@ constexpr int STEP_CPW = 16;        // chains per wave of the fused step (TPC = 
 constexpr int SMALL_CPW = 16;        // chains per wave of the one-wave step (D < 16) and persistent kernel
 
 // slice width of the wide schedule: 32 (D < 4096) and 64 measured best over 16-256
-inline int slice_width(int D) { return D >= 4096 ? 64 : 32; }
+// 64 from D = 2048: SV (D = 2519) at 8192 chains 4.49M vs 4.36M leapfrog/s at 32, at 1024 chains
+// 3.89M vs 3.93M (fused wide step); narrower models keep 32 (more blocks per chain group)
+inline int slice_width(int D) { return D >= 2048 ? 64 : 32; }
 inline int num_slices(int D) { return D >= WIDE_MIN_D ? (D + slice_width(D) - 1) / slice_width(D) : 0; }
 constexpr size_t ALIGN = 256;
 
