@@ -717,12 +717,15 @@ __device__ __forceinline__ T sum_slots(const T* __restrict__ p, size_t st, int s
 }
 
 // One workgroup per (64 batch positions, coordinate d or the U row d = D).  Wave w sums the
-// slots [w S / 4, (w + 1) S / 4) in order, then the four are added in wave order: a fixed
-// order that depends on S (a function of n_rows) only, and four independent load streams per
-// output, so the small launches of a NUTS tail are not one long dependent chain of loads.
+// slots [w S / W, (w + 1) S / W) in order, then the W wave sums are added in wave order: a
+// fixed order that depends on S (a function of n_rows) only, and W independent load streams
+// per output, so the small launches of a NUTS tail are not one long dependent chain of loads.
 // wcol: U gains the per-chain linear term w . b; pe_shift removes the log(2) terms of the zero
-// rows that pad the split-bf16 tiles
-constexpr int FIN_WAVES = 4;
+// rows that pad the split-bf16 tiles.  (NMX_FIN_WAVES: compile-time A/B, scripts/ab_build.py)
+#ifndef NMX_FIN_WAVES
+#define NMX_FIN_WAVES 4
+#endif
+constexpr int FIN_WAVES = NMX_FIN_WAVES;
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float* __restrict__ gpart,
                                                                     const double* __restrict__ pepart, int S, int D,
                                                                     nmx_eval_batch ev,
