@@ -721,11 +721,8 @@ __device__ __forceinline__ T sum_slots(const T* __restrict__ p, size_t st, int s
 // fixed order that depends on S (a function of n_rows) only, and W independent load streams
 // per output, so the small launches of a NUTS tail are not one long dependent chain of loads.
 // wcol: U gains the per-chain linear term w . b; pe_shift removes the log(2) terms of the zero
-// rows that pad the split-bf16 tiles.  (NMX_FIN_WAVES: compile-time A/B, scripts/ab_build.py)
-#ifndef NMX_FIN_WAVES
-#define NMX_FIN_WAVES 4
-#endif
-constexpr int FIN_WAVES = NMX_FIN_WAVES;
+// rows that pad the split-bf16 tiles.  W = 4 (8 and 16 measured slower)
+constexpr int FIN_WAVES = 4;
 __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float* __restrict__ gpart,
                                                                     const double* __restrict__ pepart, int S, int D,
                                                                     nmx_eval_batch ev,
