@@ -63,43 +63,58 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds):
+def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None):
     """Reduced-chain CPU comparator (SURVEY.md §8d CPU side 2): `chains` chains of the oracle's
     NUTS (oracle/hmc_ref.py, float32) started from the GPU's adapted state of the first chains
     (z, U, grad, step size, diagonal mass) and the same Philox stream, so they run the timed
     workload's trees; their potential calls are batched into the OpenMP C restatement of the
-    covtype potential (oracle/c/logreg_batch.c, one X pass per batch: GEMM form).  Runs whole
-    transitions until `seconds` have elapsed; returns leapfrogs/s."""
+    covtype potential (oracle/c/logreg_batch.c: register-blocked AVX-512 GEMMs over the full
+    data).  Chains run on continuously until `seconds` have elapsed (a fixed batch: no chain
+    waits for the others between transitions); returns leapfrogs/s.
+
+    Full-size parity (with dev_ns [chains, T] / dev_z [chains, T, D], the GPU's timed
+    transitions of those chains): the oracle chains' tree sizes and draws are compared with the
+    GPU's transitions from the same state on the same stream, and every chain that leaves the
+    GPU's path is reported with the oracle's decision closest to a tie at that transition."""
     import numpy as np
 
     from oracle import cpu_batched as CB
-    from oracle import hmc_ref as H
 
     f = CB.LogRegBatch(X, y)
     D = X.shape[1]
     cols = lambda t: t[:chains].detach().cpu().numpy()  # noqa: E731
-    z, g, pe = cols(state.z["coefs"]), cols(state.z_grad), cols(state.potential_energy)
-    ss, imm = cols(state.adapt_state.step_size), cols(state.adapt_state.inverse_mass_matrix)
-    oracles, states = [], []
-    for c in range(chains):
-        o = H.NUTSOracle(None, D, num_warmup, step_size=float(ss[c]), inverse_mass_matrix=imm[c])
-        wa = o.wa_init((z[c],), None, np.float32(ss[c]), inverse_mass_matrix=imm[c], mass_matrix_size=D)
-        oracles.append(o)
-        states.append(H.HMCState(it0, z[c].astype(np.float32), g[c].astype(np.float32), np.float32(pe[c]), None,
-                                 None, None, 0, np.float32(0), np.float32(0), False, wa, (seed, c)))
+    states, oracles = CB.chains_from_state(
+        cols(state.z["coefs"]), cols(state.z_grad), cols(state.potential_energy), cols(state.adapt_state.step_size),
+        cols(state.adapt_state.inverse_mass_matrix), cols(state.adapt_state.mass_matrix_sqrt), it0, seed, num_warmup)
+    f(np.zeros((chains, D), np.float32))  # untimed: OpenMP pool and first-touch of the partials
+    stats = {}
     t0 = time.perf_counter()
-    leap, trans = 0, 0
-    while time.perf_counter() - t0 < seconds:
-        states, _, evals, _ = CB.run_chains(f, states, oracles, 1)
-        leap += evals
-        trans += 1
+    _, hist, leap, calls = CB.run_chains(f, states, oracles, 1 << 30, deadline=t0 + seconds,
+                                         record=dev_ns is not None, stats=stats)
     dt = time.perf_counter() - t0
-    return {"value": leap / dt, "unit": "leapfrog/s", "cores": f.threads(), "kind": "port",
-            "sample": f"reduced C={chains}: {chains} chains of the timed workload (GPU-adapted state, same "
-                      f"stream), {trans} transitions = {leap} leapfrogs in {dt:.1f}s; NumPy oracle NUTS "
-                      f"(oracle/hmc_ref.py) with the potential batched over chains into the OpenMP C "
-                      f"restatement (oracle/c/logreg_batch.c, full {X.shape[0]}x{D} f32 data)",
-            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    trans = sum(len(h) for h in hist)
+    gflops = 4.0 * X.shape[0] * D * leap / stats["pot_s"] / 1e9
+    out = {"value": leap / dt, "unit": "leapfrog/s", "cores": f.threads(), "kind": "port",
+           "sample": f"reduced C={chains}: {chains} chains of the timed workload (GPU-adapted state, same "
+                     f"stream) run continuously for {dt:.1f}s: {trans} transitions = {leap} leapfrogs in {calls} "
+                     f"batched potential calls; NumPy oracle NUTS (oracle/hmc_ref.py) with the potential batched "
+                     f"over chains into the OpenMP C restatement (oracle/c/logreg_batch.c, register-blocked "
+                     f"AVX-512, full {X.shape[0]}x{D} f32 data)",
+           "potential_gflops": gflops, "potential_share": stats["pot_s"] / dt,
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    if dev_ns is not None:
+        par = CB.compare_paths(hist, dev_ns[:chains], dev_z[:chains], atol=1e-4)
+        ties = sum(1 for m in par["mismatches"] if m[4])
+        for c, t, kind, m, tie in par["mismatches"]:
+            print(f"[parity] chain {c}: first difference at timed transition {t}, closest oracle decision {kind} "
+                  f"margin {m:.3g} ({'rounding tie' if tie else 'NOT a tie'})", file=sys.stderr)
+        par["mismatches_at_tie"] = ties
+        par["mismatches"] = [list(m) for m in par["mismatches"]]
+        par["basis"] = ("oracle NUTS (C potential, full data) vs the GPU's timed transitions of the same chains "
+                        "from the same state on the same Philox stream: equal tree sizes and draws within 1e-4 "
+                        "per transition")
+        out["parity"] = par
+    return out
 
 
 # BASELINE.json configs[2..4]: (model, args, chains (total), warmup, timed transitions, dense mass,
@@ -375,9 +390,12 @@ def main():
                            "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2),
-                                               args.adapt + args.warmup, args.adapt, args.cpu_chains,
-                                               args.cpu_seconds)
+            k = min(args.cpu_chains, hi - lo)
+            cb = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2), args.adapt + args.warmup, args.adapt, k,
+                              args.cpu_seconds, dev_ns=ns[:k].cpu().numpy(),
+                              dev_z=site[:k].to(torch.float64).cpu().numpy())
+            out["parity"] = cb.pop("parity")
+            out["cpu_baseline"] = cb
     if args.configs != "none":
         del mcmc, eng, pot, start_state
         torch.cuda.empty_cache()

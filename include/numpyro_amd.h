@@ -178,7 +178,8 @@ int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, v
  * with build_tree hmc_util.py:1088-1180 unrolled into leaves): consumes the potential at
  * z_eval for LEAF chains, advances trees / transitions / adaptation / collection, and
  * writes the next z_eval.  samples: [collection_size][D][ldc] (constrained via transform,
- * int8 [D]: 0 identity, 1 exp); fields: [collection_size][NMX_NUM_COLLECT][ldc].
+ * int8 [D]: 0 identity, 1 exp; NULL: no draws are written, only the fields);
+ * fields: [collection_size][NMX_NUM_COLLECT][ldc].
  * dim <= 256: one fused kernel; dim >= 257: three D-split kernels (leapfrog end + partial
  * dots / fixed-order reduction + scalar logic / apply), same results semantics. */
 int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,

@@ -933,7 +933,7 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
   const bool vec2 = A.take_leaf || A.done_sub || A.take_biased || A.hmc_accept || A.iter_done || A.start_iter ||
                     A.prep_leaf;
   if (vec2) {
-    float* const samp = A.slot >= 0 ? P.samples + (size_t)A.slot * D * ldc : nullptr;
+    float* const samp = (A.slot >= 0 && P.samples) ? P.samples + (size_t)A.slot * D * ldc : nullptr;
     const float step_eff = S.step_eff;
     if constexpr (TPC > 1 && NMX_STEP_AROWS >= 1) {
       ke0[0] = apply_rows<NMX_STEP_AROWS>(v, A, step_eff, vw, NV, c, seed, gch, S.it, samp, P.transform, cfg);
@@ -1186,7 +1186,8 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   A.slot = slot;
   A.wfn = wfn;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
-  float* const samp = (A.iter_done && A.slot >= 0) ? W.p.samples + (size_t)A.slot * D * ldc : nullptr;
+  float* const samp = (A.iter_done && A.slot >= 0 && W.p.samples) ? W.p.samples + (size_t)A.slot * D * ldc
+                                                                   : nullptr;
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   float ke0[1] = {0.0f};
   if (act & VEC) {
@@ -1758,7 +1759,8 @@ extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float
   int st = validate(cfg);
   if (st) return st;
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
-  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+  // samples may be NULL: the per-transition fields alone are collected
+  if (cfg->collection_size > 0 && (!fields || !transform))
     return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
   if (tpc_for_dim(cfg->dim) != 1 || num_slices(cfg->dim) != 0)
     return nmx_fail(NMX_ERR_INVALID, "run_small: dim %d is not a one-wave model (dim < 16)", cfg->dim);
@@ -1790,7 +1792,8 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   int st = validate(cfg);
   if (st) return st;
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
-  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+  // samples may be NULL: the per-transition fields alone are collected
+  if (cfg->collection_size > 0 && (!fields || !transform))
     return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
   StepArgs args;
   args.a = arena_of(cfg, arena);
@@ -1844,7 +1847,8 @@ extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena,
   int st = validate(cfg);
   if (st) return st;
   if (!arena || !workspace) return nmx_fail(NMX_ERR_INVALID, "arena / workspace is NULL");
-  if (cfg->collection_size > 0 && (!samples || !fields || !transform))
+  // samples may be NULL: the per-transition fields alone are collected
+  if (cfg->collection_size > 0 && (!fields || !transform))
     return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
   const int ns = num_slices(cfg->dim);
   if (ns == 0) return nmx_fail(NMX_ERR_INVALID, "step_wide_model: dim %d uses the fused step (dim < %d)", cfg->dim,

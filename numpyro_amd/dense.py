@@ -51,6 +51,7 @@ class Whitening:
         self.mu = torch.zeros(self.D, dtype=torch.float32, device=self.device)
         self._ws = {}
         self._split = {}
+        self.version = 0  # bumped by set(): cached views of the matrices are keyed by it
         self.x3 = bool(x3)
         if self.x3:  # MFMA-fragment packs of T^T and T (nmx_gemm_x3_pack_a)
             nb = lib().nmx_gemm_x3_packed_a_bytes(self.lda)
@@ -95,7 +96,8 @@ class Whitening:
             raise ValueError(f"inverse_mass_matrix must be [{self.D}, {self.D}]")
         # tril_inv = swap(chol(cov[::-1, ::-1])[::-1, ::-1])  (hmc_util.py:228-231); T = tril_inv^T
         T = torch.linalg.cholesky(imm.flip(0, 1)).flip(0, 1)
-        self.inverse_mass_matrix = imm
+        self.inverse_mass_matrix = imm.clone()  # never the caller's tensor: snapshots share it
+        self.version += 1
         self.T = T
         self._tinv = None
         self.fwd_t[:self.D, :self.D] = T.t().to(torch.float32)
@@ -265,6 +267,7 @@ class ChainWhitening:
         self.device = torch.device(device)
         self.fwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T^T
         self.bwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T
+        self.version = 0
         eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
         self.set(eye.expand(self.C, self.D, self.D))
 
@@ -279,7 +282,8 @@ class ChainWhitening:
         if imm.shape != (self.C, self.D, self.D):
             raise ValueError(f"inverse_mass_matrix must be [{self.C}, {self.D}, {self.D}]")
         T = torch.linalg.cholesky(imm.flip(-2, -1)).flip(-2, -1)  # upper, T T^T = imm
-        self.inverse_mass_matrix = imm.contiguous()
+        self.inverse_mass_matrix = imm.contiguous().clone()
+        self.version += 1
         self.T = T
         self.fwd.copy_(T.transpose(-1, -2))
         self.bwd.copy_(T)

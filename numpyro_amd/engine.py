@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import uuid
 from dataclasses import dataclass
 
 import torch
@@ -22,7 +23,11 @@ from .native import NutsConfig, EvalBatch, check, lib, ptr, stream_ptr
 
 INIT_ATTEMPTS = 100  # find_valid_initial_params (numpyro/infer/util.py:386-388)
 
-_generations = iter(range(1, 1 << 62))  # ids of arena contents (Engine.generation)
+# ids of arena contents (Engine.generation): (process token, counter), so a state pickled in
+# another process never matches a generation of this one
+_PROCESS_TOKEN = uuid.uuid4().hex
+_counter = iter(range(1, 1 << 62))
+_generations = ((_PROCESS_TOKEN, n) for n in _counter)
 
 
 def build_adaptation_schedule(num_steps):
@@ -85,6 +90,11 @@ class Engine:
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
         self.dense = bool(opts.dense_mass)
+        if self.dense and opts.find_heuristic_step_size:
+            # the search would run in whitened coordinates and never again after a window-end
+            # re-expression: not the reference's find_reasonable_step_size (hmc.py:320-331)
+            raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
+                                      "coordinates, the dense engine in whitened ones")
         self.model_potential = potential
         # dense mass: per-chain matrices (the reference's semantics) when they are adapted and
         # fit, one pooled matrix when asked for ("pooled"), one shared whitening when the
@@ -120,9 +130,12 @@ class Engine:
         self.num_warmup = 0
         # id of the arena's current contents: a state snapshot taken at this generation can
         # be resumed without copying the arena back (MCMC.run after warmup, kernel.sample)
-        self.generation = 0
+        self.generation = None
         self._pool = None  # dense pooled adaptation: (window, PooledCovariance) across run() calls
         self._wide_ws = None  # nmx_nuts_step_wide_model workspace (zero-filled once)
+        self._mass_cache = None  # dense: (whitening version, HMCAdaptState mass fields)
+        # False: collected draws stay unconstrained (MCMC(postprocess_fn=...) maps them itself)
+        self.constrain_samples = True
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
 
@@ -201,6 +214,9 @@ class Engine:
         """Reset adaptation state and find a valid initial point for every chain
         (HMC.init -> initialize_model / find_valid_initial_params + init_kernel)."""
         s = stream_ptr(stream)
+        # the arena is about to change: no earlier snapshot may take the no-copy resume
+        # shortcut, even if the initial-point search below raises
+        self.generation = next(_generations)
         self.num_warmup = int(num_warmup)
         self._alloc(self.iter_capacity)
         self._fill_cfg(0, 0, num_warmup, seed, 0, 1, 0)
@@ -249,8 +265,11 @@ class Engine:
 
     # ------------------------------------------------------------------ dense mass
     def _heuristic(self):
+        # wa_init searches whenever adapt_step_size is set, num_warmup = 0 included
+        # (hmc.py:319-339 -> hmc_util.py:572-576); the window-end searches exist only with
+        # middle windows (_window_ends is empty without warmup)
         o = self.opts
-        return bool(o.find_heuristic_step_size) and bool(o.adapt_step_size) and self.num_warmup > 0
+        return bool(o.find_heuristic_step_size) and bool(o.adapt_step_size)
 
     def _find_step_size(self, at_init, s):
         """find_reasonable_step_size for every chain from its stored state (warmup_adapter at
@@ -291,13 +310,23 @@ class Engine:
         if bad:
             raise RuntimeError(f"{bad} chains have a non-finite potential after the mass-matrix update")
 
+    def _positive(self):
+        """Coordinates the collection maps through exp (ExpTransform sites), as a bool mask."""
+        pos = self.model_potential.transform_codes().to(torch.bool)
+        return pos if self.constrain_samples else torch.zeros_like(pos)
+
+    def _collect_codes(self):
+        """Transform codes the step kernels apply to collected draws (all zero: unconstrained)."""
+        tr = self.potential.transform_codes()
+        return tr if self.constrain_samples else torch.zeros_like(tr)
+
     def _convert_slots(self, samples, slots, s):
         """In place: whitened draws of collection slots -> model space -> constrained."""
-        if len(slots) == 0:
+        if len(slots) == 0 or samples.shape[0] == 0:
             return
         wt = self.potential.whitening
         tmp = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
-        pos = self.model_potential.transform_codes().to(torch.bool)
+        pos = self._positive()
         for k in slots:
             wt.to_model(samples[k], tmp, stream=s)
             samples[k].copy_(tmp)
@@ -329,10 +358,12 @@ class Engine:
         return segs
 
     def run(self, num_iters: int, seed: int, collect_begin: int = 0, collection_size: int | None = None,
-            thinning: int = 1, poll_every: int = 16, stream=None, max_launches: int | None = None):
+            thinning: int = 1, poll_every: int = 16, stream=None, max_launches: int | None = None,
+            collect_samples: bool = True):
         """Advance every chain by `num_iters` transitions.  Transitions with relative index
         i >= start_idx (fori_collect semantics) are collected into the returned buffers.
-        Returns (samples [S, D, ldc], fields [S, NC, ldc], launches)."""
+        Returns (samples [S, D, ldc], fields [S, NC, ldc], launches); with collect_samples
+        False only the fields are collected (samples is [0, D, ldc])."""
         s = stream_ptr(stream)
         num_iters = int(num_iters)
         lower = int(collect_begin)
@@ -344,7 +375,8 @@ class Engine:
             self._grow_finished(num_iters)
         S = max(int(collection_size), 0)
         if S > 0:
-            samples = torch.empty((S, self.D, self.ldc), dtype=torch.float32, device=self.device)
+            samples = torch.empty((S if collect_samples else 0, self.D, self.ldc), dtype=torch.float32,
+                                  device=self.device)
             fields = torch.zeros((S, len(native.COLLECT), self.ldc), dtype=torch.float32, device=self.device)
         else:  # nothing is collected: the device writes no slot (collection_size 0)
             samples = torch.empty((0, self.D, self.ldc), dtype=torch.float32, device=self.device)
@@ -395,7 +427,7 @@ class Engine:
         from .dense import ChainWelford, PooledCovariance
         chunk = max(1, int(self.opts.dense_adapt_bytes) // (4 * self.D * self.ldc))
         wt = self.potential.whitening
-        pos = self.model_potential.transform_codes().to(torch.bool)
+        pos = self._positive()
         launches = 0
         for a, b, win in self._dense_segments(it0, it1):
             if win is None:
@@ -422,9 +454,10 @@ class Engine:
                         pool.add(zbuf[:, :self.C])
                     slot = self._slot_of(ca + k, cstart, thinning, S)
                     if slot >= 0:
-                        samples[slot].copy_(zbuf)
-                        if bool(pos.any()):
-                            samples[slot][pos] = torch.exp(samples[slot][pos])
+                        if samples.shape[0] > 0:
+                            samples[slot].copy_(zbuf)
+                            if bool(pos.any()):
+                                samples[slot][pos] = torch.exp(samples[slot][pos])
                         fields[slot].copy_(afld[k])
                 del abuf, afld
             if b == win[1]:
@@ -458,7 +491,7 @@ class Engine:
         self._fill_cfg(a, b, self.num_warmup, seed, cstart, thinning, S)
         cfgp = ctypes.byref(self.cfg)
         arena = ptr(self.arena)
-        tr = self.potential.transform_codes()
+        tr = self._collect_codes()
         check(lib().nmx_nuts_resume(cfgp, arena, s), "nmx_nuts_resume")
         small = self._persistent_model()
         if small is not None:
@@ -469,7 +502,8 @@ class Engine:
             max_steps = (b - a) * ((1 << self.md) + 2) + 16
             launches = 0
             while True:
-                check(lib().nmx_nuts_run_small(cfgp, arena, ptr(samples), ptr(fields), ptr(tr), model, ptr(p0),
+                check(lib().nmx_nuts_run_small(cfgp, arena, ptr(samples) if samples.shape[0] else None, ptr(fields),
+                                               ptr(tr), model, ptr(p0),
                                                ptr(p1), n, max_steps, s), "nmx_nuts_run_small")
                 launches += 1
                 if int(self.view("counters")[0].item()) >= self.C:
@@ -482,7 +516,7 @@ class Engine:
         pending = False
         launches = 0
         step = lib().nmx_nuts_step
-        sp, fp, tp = ptr(samples), ptr(fields), ptr(tr)
+        sp, fp, tp = ptr(samples) if samples.shape[0] else None, ptr(fields), ptr(tr)
         cfg = self.cfg
         parity = 0
         cfg.parity = parity
@@ -550,9 +584,16 @@ class Engine:
         them: per-chain diagonals [C, D], per-chain dense matrices [C, D, D], or the pooled /
         shared dense matrices [D, D]."""
         if self.dense:
+            # the matrices change only when the whitening is set (window ends): computed once
+            # per version (mass_matrix_sqrt is a triangular solve) and shared by every snapshot
+            # until then; Whitening.set replaces them, never writes into them
             wt = self.potential.whitening
-            return (wt.inverse_mass_matrix.to(torch.float32).clone(), wt.mass_matrix_sqrt().to(torch.float32),
-                    wt.mass_matrix_sqrt_inv().to(torch.float32).clone())
+            key = (id(wt), wt.version)
+            if self._mass_cache is None or self._mass_cache[0] != key:
+                self._mass_cache = (key, (wt.inverse_mass_matrix.to(torch.float32),
+                                          wt.mass_matrix_sqrt().to(torch.float32),
+                                          wt.mass_matrix_sqrt_inv().to(torch.float32).clone()))
+            return self._mass_cache[1]
         ms = self.chain_state("mass_sqrt").clone()
         return self.chain_state("inv_mass").clone(), ms, 1.0 / ms
 
@@ -560,11 +601,18 @@ class Engine:
         if not self.dense:
             return None
         wt = self.potential.whitening
-        return (wt.inverse_mass_matrix.clone(), None if self.chain_dense else wt.mu.clone())
+        # inverse_mass_matrix is replaced by Whitening.set, not written: shared; mu is written
+        return (wt.inverse_mass_matrix, None if self.chain_dense else wt.mu.clone())
 
     def set_whitening_state(self, st):
         if st is not None:
             self.potential.whitening.set(st[0], st[1])
+
+    def layout(self):
+        """What a state's arena copy must match to be resumed by this engine (a pickled
+        state is resumed by the engine of an unpickled MCMC / kernel in another process)."""
+        return (type(self.model_potential).__name__, self.C, self.D, self.md, self.chain_offset, self.dense,
+                self.chain_dense, self.opts.algo)
 
     def chain_state(self, name):
         """Per-chain view without padding: scalars [C], vectors [C, D]."""

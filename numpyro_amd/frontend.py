@@ -304,11 +304,73 @@ def potential_from_model(model, args=(), kwargs=None):
     for m in MATCHERS:
         pot = m(trace)
         if pot is not None:
-            return pot
+            return _with_traced_deterministics(pot, trace)
     raise NotImplementedError(
         "no fused kernel for this model structure (sites: " + ", ".join(map(repr, trace.sites.values())) +
         "); supported: the reference's covtype logistic regression, eight schools, funnel (+ LocScaleReparam), "
         "stochastic volatility and BNN examples, and diagonal / multivariate normal targets")
+
+
+# ----------------------------------------------------------------------------- deterministic sites
+_SYM_UNARY = {"tanh": "tanh", "exp": "exp", "sqrt": "sqrt", "log": "log", "neg": "neg"}
+_SYM_BINARY = {"add": "add", "sub": "sub", "mul": "mul", "div": "div", "pow": "pow"}
+
+
+def eval_sym(x, values):
+    """Value of a traced expression over a batch of draws: `values` maps latent site names to
+    tensors [*batch, *site shape] (constrained values, as the model sees them).  Constants
+    broadcast against the trailing (event) dimensions; a product with a vector operand (event
+    rank 1, known from the trace) treats it as a column / row."""
+    import torch
+
+    if not isinstance(x, Sym):
+        ref = next(iter(values.values()))
+        return torch.as_tensor(_host(x), dtype=torch.float32, device=ref.device)
+    if x.op == "latent":
+        return values[x.args[0]]
+    if x.op in _SYM_UNARY:
+        return getattr(torch, _SYM_UNARY[x.op])(eval_sym(x.args[0], values))
+    if x.op in _SYM_BINARY:
+        a, b = (eval_sym(v, values) for v in x.args)
+        return getattr(torch, _SYM_BINARY[x.op])(a, b)
+    if x.op == "matmul":
+        a_s, b_s = x.args
+        a, b = eval_sym(a_s, values), eval_sym(b_s, values)
+        va, vb = len(shape_of(a_s)) == 1, len(shape_of(b_s)) == 1
+        if vb:
+            b = b.unsqueeze(-1)
+        if va:
+            a = a.unsqueeze(-2)
+        out = torch.matmul(a, b)
+        if vb:
+            out = out.squeeze(-1)
+        if va:
+            out = out.squeeze(-2)
+        return out
+    raise NotImplementedError(f"deterministic expression with operation {x.op!r}")
+
+
+def _with_traced_deterministics(pot, trace):
+    """The model's own numpyro.deterministic sites (primitives.py:293-314) come back with the
+    samples (MCMC.get_samples, postprocess_fn), evaluated from the traced expressions after
+    the fused potential's deterministic sites."""
+    dets = dict(trace.deterministics)
+    if not dets:
+        return pot
+    base = pot.deterministic
+
+    def deterministic(sites):
+        out = base(sites)
+        vals = dict(sites)
+        vals.update(out)
+        for name, expr in dets.items():
+            v = eval_sym(expr, vals)
+            out[name] = v
+            vals[name] = v
+        return out
+
+    pot.deterministic = deterministic
+    return pot
 
 
 # ----------------------------------------------------------------------------- reparam

@@ -23,7 +23,32 @@ _HMCStateBase = namedtuple(
 
 class HMCState(_HMCStateBase):
     """numpyro/infer/hmc.py:31-48 field names; values are per-chain torch tensors (chains
-    first).  Carries a device snapshot so it can be used as ``post_warmup_state``."""
+    first).  Carries a device snapshot so it can be used as ``post_warmup_state``.
+
+    Pickling (test/test_pickle.py:215-220; MCMC.__getstate__ / HMC.__getstate__ at
+    mcmc.py:797-800, hmc.py:818-822): the snapshot travels as host tensors without the engine
+    reference; an engine of the same layout (model, chains, dimension, depth, mass-matrix
+    mode) resumes it, in this or another process."""
+
+    def __reduce__(self):
+        extra = {k: v for k, v in self.__dict__.items() if k != "_engine"}
+        eng = self.__dict__.get("_engine")
+        if extra.get("_arena") is None and eng is not None and eng.generation == extra.get("_generation"):
+            # the current state of its engine (kernel.sample's in-place snapshot): its arena is it
+            extra["_arena"] = eng.arena
+        if extra.get("_arena") is not None:
+            extra["_arena"] = extra["_arena"].cpu()
+        w = extra.get("_whitening")
+        if w is not None:
+            extra["_whitening"] = tuple(None if t is None else t.cpu() for t in w)
+        return (_rebuild_state, (tuple(self), extra))
+
+
+def _rebuild_state(fields, extra):
+    st = HMCState(*fields)
+    st.__dict__.update(extra)
+    st._engine = None
+    return st
 
 
 HMCAdaptState = namedtuple(  # hmc_util.py:18-30
@@ -61,26 +86,37 @@ def snapshot_state(eng, seed, keep_arena=True):
     st._iteration = eng.iteration
     st._num_warmup = eng.num_warmup
     st._generation = eng.generation
+    st._iter_capacity = eng.iter_capacity
+    st._layout = eng.layout()
     st._engine = eng
     assert C == st.i.shape[0]
     return st
 
 
 def restore_state(eng, state):
-    """Make `state` the engine's current state (no copy when it already is)."""
-    if getattr(state, "_engine", None) is not eng:
-        raise ValueError("the state belongs to a different model/data binding")
-    if eng.generation == state._generation:
+    """Make `state` the engine's current state (no copy when it already is).  A state of
+    another engine -- e.g. unpickled from another process -- is copied in when its layout
+    matches (same model, chains, dimension, depth, mass-matrix mode), and is then bound to
+    this engine."""
+    own = getattr(state, "_engine", None) is eng
+    if not own:
+        if getattr(state, "_engine", None) is not None or getattr(state, "_layout", None) != eng.layout():
+            raise ValueError("the state belongs to a different model/data binding (layout "
+                             f"{getattr(state, '_layout', None)} vs {eng.layout()})")
+    elif eng.generation == state._generation:
         return
     if state._arena is None:
         raise ValueError("this state was advanced in place by a later sample() call and holds no device "
                          "copy; pass the state returned by the most recent sample()")
+    if eng.arena is None or eng.iter_capacity != state._iter_capacity:
+        eng._alloc(state._iter_capacity)
     eng.arena.copy_(state._arena)
     eng.set_whitening_state(state._whitening)
     eng.iteration = state._iteration
     eng.num_warmup = state._num_warmup
     eng._pool = None
     eng.generation = state._generation
+    state._engine = eng
 
 
 class MCMCKernel:
@@ -271,7 +307,14 @@ class HMC(MCMCKernel):
 
         eng = getattr(state, "_engine", None)
         if eng is None:
-            raise ValueError("state must come from init() or sample() of this kernel")
+            if getattr(state, "_layout", None) is None:
+                raise ValueError("state must come from init() or sample() of this kernel")
+            # an unpickled state: resumed by an engine of this kernel for these model args
+            eng = getattr(self, "_engine", None)
+            if eng is None or eng.layout() != state._layout:
+                C, chain_offset = state._layout[1], state._layout[4]
+                eng = self.make_engine(C, model_args, model_kwargs, chain_offset=chain_offset)
+                self._engine = eng
         with torch.cuda.device(eng.device):
             restore_state(eng, state)
             eng.run(1, state.adapt_state.rng_key, collection_size=0)
@@ -301,6 +344,8 @@ class HMC(MCMCKernel):
         state = self.__dict__.copy()
         state["_sample_fn"] = None
         state["_engine"] = None
+        if self._model is not None:  # rebuilt from the model and its args by potential()
+            state["_potential"] = None
         return state
 
 

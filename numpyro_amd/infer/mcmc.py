@@ -39,8 +39,11 @@ class MCMC:
         if not isinstance(thinning, int) or thinning < 1:
             raise ValueError("thinning must be a positive integer")
         self.thinning = thinning
-        if postprocess_fn is not None:
-            raise NotImplementedError("postprocess_fn: samples are constrained on the device")
+        # postprocess_fn (mcmc.py:331,345,422-442): maps a dict of unconstrained site values to
+        # the collected values; None = the sampler's (constrain + deterministic sites, done on
+        # the device and by the potential).  Applied to the batch of draws [chains, draws, ...]
+        # (the reference vmaps it over chains, mcmc.py:425-433)
+        self.postprocess_fn = postprocess_fn
         if not callable(chain_method) and chain_method not in ("parallel", "vectorized", "sequential"):
             raise ValueError('Only supporting the following methods to draw chains: "sequential", '
                              '"parallel", or "vectorized"')
@@ -66,6 +69,8 @@ class MCMC:
         self._samples = None
         self._fields = None
         self._collected = ()
+        self._args, self._kwargs = (), {}
+        self._host_potential = None  # (args key, potential) for results of an unpickled MCMC
         self.last_run_stats = {}
 
     # ------------------------------------------------------------------ engine
@@ -127,6 +132,8 @@ class MCMC:
         self._collected = tuple(collect)
         seed = key_to_seed(rng_key)
         eng = self._get_engine(args, kwargs)
+        self._args, self._kwargs = tuple(args), dict(kwargs)
+        eng.constrain_samples = self.postprocess_fn is None
         dev = eng.device
         with torch.cuda.device(dev):
             if resume is not None:
@@ -149,7 +156,8 @@ class MCMC:
             end = torch.cuda.Event(enable_timing=True)
             start.record()
             samples, fields, launches = eng.run(n_iter, seed, collect_begin=lower, thinning=self.thinning,
-                                                poll_every=self.poll_every)
+                                                poll_every=self.poll_every,
+                                                collect_samples=not getattr(self, "_fields_only", False))
             end.record()
             end.synchronize()
             self.last_run_stats = {"launches": launches, "device_ms": start.elapsed_time(end),
@@ -158,27 +166,42 @@ class MCMC:
         self._last_state = self._snapshot(eng, seed)
 
     # ------------------------------------------------------------------ results
+    def _model_potential(self):
+        """The model's potential (site layout, deterministic sites): the engine's, or -- for an
+        unpickled MCMC, which has no engine -- rebuilt from the sampler and the run's args."""
+        if self._engine is not None:
+            return self._engine.model_potential
+        if self._host_potential is None:
+            self._host_potential = self.sampler.potential(self._args, self._kwargs)
+        return self._host_potential
+
     def _site_arrays(self, group_by_chain, include_deterministic=True):
-        eng = self._engine
+        pot = self._model_potential()
+        C = self.local_chains
         S = self._samples.shape[0]
-        flat = self._samples[:, :, :eng.C].permute(2, 0, 1)  # [C, S, D]
-        out = eng.potential.unflatten(flat)
-        if include_deterministic:
-            out.update(eng.potential.deterministic(out))
+        flat = self._samples[:, :, :C].permute(2, 0, 1)  # [C, S, D]
+        out = pot.unflatten(flat)
+        if self.postprocess_fn is not None:
+            # draws are unconstrained here (Engine.constrain_samples = False)
+            names = set(out)
+            out = dict(self.postprocess_fn(out))
+            if not include_deterministic:  # print_summary keeps the sample sites (mcmc.py:748-758)
+                out = {k: v for k, v in out.items() if k in names}
+        elif include_deterministic:
+            out.update(pot.deterministic(out))
         if not group_by_chain:
-            out = {k: v.reshape(eng.C * S, *v.shape[2:]) for k, v in out.items()}
+            out = {k: v.reshape(C * S, *v.shape[2:]) for k, v in out.items()}
         return out
 
     def get_samples(self, group_by_chain=False):
         return self._site_arrays(group_by_chain)
 
     def get_extra_fields(self, group_by_chain=False):
-        eng = self._engine
         out = {}
         for f in self._collected:
             if f == self._sample_field:
                 continue
-            v = self._fields[:, native.COLLECT.index(f), :eng.C].t()  # [C, S]
+            v = self._fields[:, native.COLLECT.index(f), :self.local_chains].t()  # [C, S]
             if f == "num_steps" or f == "i":
                 v = v.round().to(torch.int32)
             elif f == "diverging":
@@ -221,6 +244,10 @@ class MCMC:
         self._fields = self._fields.cpu()
 
     def __getstate__(self):
+        # mcmc.py:797-800: the engine (device arena, bound kernels) is rebuilt on the next run;
+        # post_warmup_state / last_state keep host copies of the chain state (HMCState)
         state = self.__dict__.copy()
         state["_engine"] = None
+        state["_engine_key"] = None
+        state["_host_potential"] = None
         return state

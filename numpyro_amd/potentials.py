@@ -32,9 +32,17 @@ class Potential:
     dim: int = 0
 
     def bind(self, num_chains: int, ldc: int, device) -> None:
+        before = set(self.__dict__)
         self.num_chains, self.ldc, self.device = num_chains, ldc, torch.device(device)
         self._codes = None
         self._bind(num_chains, ldc, self.device)
+        # attributes made by binding (device copies of the data, workspaces) are not pickled:
+        # an unpickled potential is unbound and binds again on its engine
+        self._bound_keys = getattr(self, "_bound_keys", set()) | (set(self.__dict__) - before)
+
+    def __getstate__(self):
+        drop = getattr(self, "_bound_keys", set()) | {"_bound_keys"}
+        return {k: v for k, v in self.__dict__.items() if k not in drop}
 
     def _bind(self, num_chains, ldc, device):
         pass
@@ -314,6 +322,14 @@ class FusedModel:
 
     def __repr__(self):
         return f"FusedModel({self.__name__})"
+
+    def __reduce__(self):
+        # pickled by reference, like a model function (module-level name in this module)
+        return (_fused_model, (self.__name__,))
+
+
+def _fused_model(name):
+    return globals()[name]
 
 
 logistic_regression = FusedModel(

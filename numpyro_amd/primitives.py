@@ -20,6 +20,16 @@ def _tracer():
 
 
 def sample(name, fn, obs=None, rng_key=None, sample_shape=(), infer=None, obs_mask=None):
+    """numpyro.sample (primitives.py:154-239).  `obs_mask` (a masked likelihood with imputed
+    latent entries, :177-191) and `infer` options (enumeration, auxiliary sites) change the
+    potential; the fused kernels implement the full-data likelihood only, so both are refused
+    here instead of being dropped."""
+    if obs_mask is not None:
+        raise NotImplementedError(f"sample site {name!r}: obs_mask (masked likelihood) is not supported by the "
+                                  "fused potentials")
+    if infer:
+        raise NotImplementedError(f"sample site {name!r}: infer={dict(infer)!r} is not supported by the fused "
+                                  "potentials")
     return _tracer().sample(name, fn, obs, tuple(sample_shape))
 
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import time
 
 import numpy as np
 
@@ -62,6 +63,7 @@ class _Batcher:
         self.res = {}
         self.evals = 0
         self.calls = 0
+        self.pot_s = 0.0  # seconds inside the batched potential
         self.error = None
 
     def pe_grad(self, k, z):
@@ -89,7 +91,9 @@ class _Batcher:
                 keys = sorted(self.req)
                 Z = np.stack([self.req.pop(k) for k in keys])
             try:
+                t0 = time.perf_counter()
                 pe, g = self.f(Z)
+                self.pot_s += time.perf_counter() - t0
             except Exception as e:  # noqa: BLE001  (propagated to every waiting chain)
                 with self.cv:
                     self.error = e
@@ -103,10 +107,15 @@ class _Batcher:
                 self.cv.notify_all()
 
 
-def run_chains(pe_grad_batch, states, oracles, num_transitions):
+def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, record=False, stats=None):
     """Advance every (oracle, state) pair by `num_transitions` transitions with batched
     potential evaluations.  `oracles[k]` must have been built with pe_grad = None; it is bound
-    here.  Returns (final states, per-chain list of states, potential evaluations, batched calls)."""
+    here.  With `deadline` (a time.perf_counter() value) a chain starts no further transition
+    once it has passed (chains run on continuously until then, so the batch stays full: the
+    CPU comparator's fixed-batch mode).  With `record`, every history entry is (state,
+    decisions of that transition: (kind, margin) list, see hmc_ref.record_decisions).  `stats`
+    (a dict) receives the seconds spent inside the batched potential ("pot_s").
+    Returns (final states, per-chain list of states, potential evaluations, batched calls)."""
     n = len(states)
     b = _Batcher(pe_grad_batch, n)
     out = [None] * n
@@ -121,8 +130,13 @@ def run_chains(pe_grad_batch, states, oracles, num_transitions):
             o.vv_init, o.vv_update = H.velocity_verlet(fn)
             st = states[k]
             for _ in range(num_transitions):
+                if deadline is not None and time.perf_counter() >= deadline:
+                    break
+                log = [] if record else None
+                H.record_decisions(log)
                 st = o.sample(st)
-                hist[k].append(st)
+                hist[k].append((st, log) if record else st)
+            H.record_decisions(None)
             out[k] = st
         except Exception as e:  # noqa: BLE001
             errs.append(e)
@@ -137,4 +151,53 @@ def run_chains(pe_grad_batch, states, oracles, num_transitions):
         t.join()
     if errs:
         raise errs[0]
+    if stats is not None:
+        stats["pot_s"] = b.pot_s
     return out, hist, b.evals, b.calls
+
+
+def chains_from_state(z, grad, pe, step_size, inverse_mass, mass_sqrt, it0, seed, num_warmup, chain_offset=0):
+    """Oracle chains resuming a device state (arrays [C, ...] of the first C chains: position,
+    gradient, potential energy, adapted step size, diagonal inverse mass and its square root,
+    transition index it0 >= num_warmup, i.e. sampling), on the device's Philox stream `seed`.
+    Returns (states, oracles) for run_chains; the oracles' next transitions are the ones the
+    device ran from that state (bench.py's cpu_baseline leg, tests/test_gpu_nuts.py)."""
+    oracles, states = [], []
+    D = z.shape[1]
+    for c in range(z.shape[0]):
+        o = H.NUTSOracle(None, D, num_warmup, step_size=float(step_size[c]), inverse_mass_matrix=inverse_mass[c])
+        wa = o.wa_init((z[c],), None, np.float32(step_size[c]), inverse_mass_matrix=inverse_mass[c],
+                       mass_matrix_size=D)
+        # the device's own square root (the same formula; taken as is so nothing is recomputed)
+        wa = wa._replace(mass_matrix_sqrt=np.asarray(mass_sqrt[c], np.float32))
+        oracles.append(o)
+        states.append(H.HMCState(int(it0), np.asarray(z[c], np.float32), np.asarray(grad[c], np.float32),
+                                 np.float32(pe[c]), None, None, None, 0, np.float32(0), np.float32(0), False, wa,
+                                 (seed, chain_offset + c)))
+    return states, oracles
+
+
+def compare_paths(hist, dev_num_steps, dev_z, atol):
+    """Per-chain parity of oracle histories (run_chains(record=True)) with the device's
+    transitions from the same state: a chain matches while its tree sizes are equal and its
+    draws agree to `atol`; at the first difference the oracle's closest decision to a tie is
+    reported.  Returns {chains, transitions, matched, max_abs_dz, mismatches: [(chain,
+    transition, kind, margin, is_tie)]}."""
+    matched, transitions, max_dz, mism = 0, 0, 0.0, []
+    for c, h in enumerate(hist):
+        T = min(len(h), dev_num_steps.shape[1])
+        transitions += T
+        bad = None
+        for t in range(T):
+            st, log = h[t]
+            dz = float(np.max(np.abs(np.asarray(st.z, np.float64) - dev_z[c, t])))
+            if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
+                bad = t
+                d = H.closest_decision(log)
+                mism.append((c, t, d[0], d[1], H.is_tie(d)))
+                break
+            max_dz = max(max_dz, dz)
+        if bad is None:
+            matched += 1
+    return {"chains": len(hist), "transitions": transitions, "matched": matched, "max_abs_dz": max_dz,
+            "mismatches": mism}

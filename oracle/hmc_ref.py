@@ -21,6 +21,7 @@ left the oracle's did so at a rounding-level tie (tests/test_gpu_nuts.py).
 from __future__ import annotations
 
 import math
+import threading
 from collections import namedtuple
 
 import numpy as np
@@ -28,11 +29,42 @@ import numpy as np
 from . import philox
 
 DECISIONS = None  # list -> record (kind, margin) of every discrete decision
+_TLS = threading.local()  # per-thread log (oracle.cpu_batched runs one chain per thread)
 
 
 def _log(kind, margin):
-    if DECISIONS is not None:
-        DECISIONS.append((kind, float(margin)))
+    d = getattr(_TLS, "decisions", None)
+    if d is None:
+        d = DECISIONS
+    if d is not None:
+        d.append((kind, float(margin)))
+
+
+def record_decisions(log):
+    """Log this thread's decisions into `log` (a list), or stop logging them (None)."""
+    _TLS.decisions = log
+
+
+# A decision is a rounding-level tie when device and oracle can order it differently: the
+# two compute in f32 with different summation orders (potential, kinetic energy, U-turn
+# dots), so energies differ by ~1e-6 relative (dE by ~1e-4 absolute for |E| ~ 1e2-1e3) and
+# dot products by ~1e-6 of the magnitude of their terms.  Margins are scale-free (see _log).
+TIE = {"transition": 2e-3, "accept": 2e-3, "turn": 1e-3, "diverge": 1e-4}
+
+
+def tie_score(d):
+    kind, m = d
+    return m / TIE[kind]
+
+
+def closest_decision(decisions):
+    """The decision of a transition closest to a tie, ("none", inf) without decisions."""
+    return min(decisions, key=tie_score) if decisions else ("none", math.inf)
+
+
+def is_tie(d):
+    kind, m = d
+    return kind in TIE and m <= TIE[kind]
 
 
 AdaptWindow = namedtuple("AdaptWindow", ["start", "end"])  # hmc_util.py:16

@@ -99,26 +99,39 @@ def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None,
     kernel = NUTS(model, **kernel_kw)
     mcmc = MCMC(kernel, num_warmup=warmup, num_samples=steps, num_chains=chains, progress_bar=False)
     t0 = time.time()
-    mcmc.warmup(0, *args, extra_fields=("num_steps",))
+    mcmc._fields_only = True  # warmup transitions' fields (tree sizes, divergences), no draws
+    mcmc.warmup(0, *args, collect_warmup=True, extra_fields=("num_steps", "diverging"))
+    mcmc._fields_only = False
     torch.cuda.synchronize()
     t_warm = time.time() - t0
+    wf = mcmc.get_extra_fields(group_by_chain=True)
+    w_ns = wf["num_steps"].to(torch.float64)
+    warm = {"warmup_leapfrogs": int(w_ns.sum().item()), "warmup_leapfrog_per_s": round(float(w_ns.sum()) / t_warm, 1),
+            "warmup_mean_tree_per_window_third": [round(float(x.mean()), 1) for x in w_ns.chunk(3, dim=1)],
+            "warmup_divergent_frac": round(float(wf["diverging"].float().mean()), 4)}
     eng = mcmc._engine
     timer = Timed(eng.potential)
     timer.on = True
     torch.cuda.synchronize()
     t0 = time.time()
-    mcmc.run(1, *args, extra_fields=("num_steps",))
+    mcmc.run(1, *args, extra_fields=("num_steps", "diverging"))
     torch.cuda.synchronize()
     wall = time.time() - t0
     timer.on = False
     ns = int(mcmc.get_extra_fields()["num_steps"].sum().item())
+    from numpyro_amd import shard
+    sm = mcmc.get_samples(group_by_chain=True)
+    rh = max(float(shard.split_gelman_rubin(v.reshape(v.shape[0], v.shape[1], -1)).max()) for v in sm.values()) \
+        if steps >= 4 else None
+    warm.update({"divergent_frac": round(float(mcmc.get_extra_fields()["diverging"].float().mean()), 4),
+                 "max_split_rhat": rh, "mean_tree": round(ns / (chains * steps), 1)})
     pot_ms = timer.total_ms()
     launches = len(timer.events)
     out = {"config": name, "chains": chains, "dim": eng.D, "warmup": warmup, "steps": steps,
            "leapfrogs": ns, "wall_s": round(wall, 3), "leapfrog_per_s": round(ns / wall, 1),
            "launches": launches, "potential_ms_avg": round(pot_ms / max(launches, 1), 4),
            "potential_share": round(pot_ms / 1e3 / wall, 3), "warmup_wall_s": round(t_warm, 2),
-           "dense": bool(eng.dense)}
+           "dense": bool(eng.dense), **warm}
     if flops_per_leapfrog:
         tf = flops_per_leapfrog * ns / (pot_ms * 1e-3) / 1e12
         peak = PEAK_F32_TFLOPS

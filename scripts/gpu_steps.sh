@@ -1,7 +1,12 @@
 #!/bin/bash
 # Run GPU steps in order; stop at the first fault/abort/timeout (exit 124,134,137,139 or
 # signal), continue past ordinary test failures.  Usage: scripts/gpu_steps.sh name:secs:cmd ...
+# A heartbeat file under gpurun_out/ is appended every 50 s while the steps run (long
+# benchmark steps print only at their end); it stops with the script.
 mkdir -p gpurun_out
+( while true; do date +%s >> gpurun_out/heartbeat.log; sleep 50; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 for spec in "$@"; do
   name="${spec%%:*}"; rest="${spec#*:}"; secs="${rest%%:*}"; cmd="${rest#*:}"
   echo "=== $name ($secs s): $cmd" >> gpurun_out/steps.log

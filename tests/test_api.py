@@ -137,3 +137,40 @@ def test_host_diagnostics_known_values():
     lo, hi = diagnostics.hpdi(rs.randn(100000), prob=0.9)
     np.testing.assert_allclose([lo, hi], [-1.645, 1.645], atol=0.05)
     assert math.isclose(float(diagnostics.autocorrelation(np.arange(10.0))[0]), 1.0)
+
+
+def test_pickling_kernels_models_and_states():
+    """test/test_pickle.py: samplers, models and states pickle (by reference for model
+    functions and fused models, mcmc.py:797-800, hmc.py:818-822); bound device data and the
+    engine are left out and rebuilt."""
+    import pickle
+
+    import torch
+
+    import model_zoo as Z
+    from numpyro_amd.infer.hmc import HMCAdaptState, HMCState
+
+    for model in (P.eight_schools, P.logistic_regression, Z.covtype_model):
+        k = pickle.loads(pickle.dumps(NUTS(model, target_accept_prob=0.9)))
+        assert k.model is model and k._target_accept_prob == 0.9
+    m = MCMC(NUTS(P.funnel), num_warmup=3, num_samples=4, num_chains=6, postprocess_fn=dict)
+    m2 = pickle.loads(pickle.dumps(m))
+    assert m2.sampler.model is P.funnel and m2.postprocess_fn is dict and m2.num_samples == 4
+    # a bound potential pickles without its device data and binds again
+    pot = P.DiagNormal([0.0, 1.0], [1.0, 2.0])
+    pot.bind(4, 64, "cpu")
+    assert hasattr(pot, "prec")
+    p2 = pickle.loads(pickle.dumps(pot))
+    assert not hasattr(p2, "prec") and not hasattr(p2, "_bound_keys")
+    p2.bind(4, 64, "cpu")
+    torch.testing.assert_close(p2.prec, pot.prec)
+    # a state snapshot: host copies of the arena / whitening, no engine reference
+    t = torch.arange(3.0)
+    st = HMCState(t, {"x": t}, t, t, t, None, 1.0, t, t, t, t > 1,
+                  HMCAdaptState(t, t, t, t, (t,), (t,), t, 7), 7)
+    st._arena, st._whitening, st._engine = torch.ones(16, dtype=torch.uint8), (t, None), object()
+    st._layout, st._generation = ("DiagNormal", 3, 1, 10, 0, False, False, 1), ("tok", 5)
+    st2 = pickle.loads(pickle.dumps(st))
+    assert type(st2) is HMCState and st2._engine is None and st2._layout == st._layout
+    torch.testing.assert_close(st2._arena, st._arena)
+    assert st2.adapt_state.rng_key == 7 and st2._whitening[1] is None

@@ -70,3 +70,66 @@ def test_unsupported_structures_are_refused(change):
 def test_model_cannot_run_eagerly():
     with pytest.raises(RuntimeError, match="traces them"):
         Z.funnel(10)
+
+
+def test_masked_likelihood_and_infer_options_are_refused():
+    """A masked likelihood (obs_mask, primitives.py:177-191) or infer options change the
+    potential: refused, not silently mapped onto the full-data kernel."""
+    X, y = datasets.covtype_synthetic(n_rows=200, seed=2)
+
+    def masked(features, labels):
+        beta = numpyro.sample("beta", dist.Normal(np.zeros(55), np.ones(55)))
+        numpyro.sample("y", dist.Bernoulli(logits=features @ beta), obs=labels, obs_mask=labels > 0)
+
+    def enum(features, labels):
+        beta = numpyro.sample("beta", dist.Normal(np.zeros(55), np.ones(55)), infer={"enumerate": "parallel"})
+        numpyro.sample("y", dist.Bernoulli(logits=features @ beta), obs=labels)
+
+    for m in (masked, enum):
+        with pytest.raises(NotImplementedError, match="not supported"):
+            potential_from_model(m, (X, y))
+
+
+def test_model_deterministic_sites_are_evaluated():
+    """numpyro.deterministic sites of the model (primitives.py:293-314) come back with the
+    draws: the traced expressions evaluated over a batch of constrained site values."""
+    import torch
+
+    X, Y = datasets.bnn_data(N=20, D_X=3)
+
+    def bnn_det(X, Y, D_H):
+        w1 = numpyro.sample("w1", dist.Normal(np.zeros((3, D_H)), np.ones((3, D_H))))
+        z1 = numpyro.deterministic("z1", Z.jnp.tanh(Z.jnp.matmul(X, w1)))
+        w2 = numpyro.sample("w2", dist.Normal(np.zeros((D_H, D_H)), np.ones((D_H, D_H))))
+        z2 = Z.jnp.tanh(Z.jnp.matmul(z1, w2))
+        w3 = numpyro.sample("w3", dist.Normal(np.zeros((D_H, 1)), np.ones((D_H, 1))))
+        z3 = numpyro.deterministic("z3", Z.jnp.matmul(z2, w3))
+        prec = numpyro.sample("prec_obs", dist.Gamma(3.0, 1.0))
+        numpyro.deterministic("sigma_obs", 1.0 / Z.jnp.sqrt(prec))
+        with numpyro.plate("data", X.shape[0]):
+            numpyro.sample("Y", dist.Normal(z3, 1.0 / Z.jnp.sqrt(prec)).to_event(1), obs=Y)
+
+    pot = potential_from_model(bnn_det, (X, Y, 4))
+    assert isinstance(pot, P.BNN)
+    rs = np.random.RandomState(0)
+    B = (5, 2)  # [chains, draws]
+    vals = {"w1": rs.randn(*B, 3, 4), "w2": rs.randn(*B, 4, 4), "w3": rs.randn(*B, 4, 1),
+            "prec_obs": rs.rand(*B) + 0.5}
+    out = pot.deterministic({k: torch.tensor(v, dtype=torch.float32) for k, v in vals.items()})
+    z1 = np.tanh(np.einsum("nd,cidh->cinh", X, vals["w1"]))
+    z3 = np.einsum("cinh,cihk->cink", np.tanh(np.einsum("cinh,cihk->cink", z1, vals["w2"])), vals["w3"])
+    np.testing.assert_allclose(out["z1"].numpy(), z1, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["z3"].numpy(), z3, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(out["sigma_obs"].numpy(), 1 / np.sqrt(vals["prec_obs"]), rtol=1e-6)
+    # vector operands: covtype logits as a deterministic site
+    Xc, yc = datasets.covtype_synthetic(n_rows=50, seed=3)
+
+    def cov_det(data, labels):
+        coefs = numpyro.sample("coefs", dist.Normal(np.zeros(55), np.ones(55)))
+        logits = numpyro.deterministic("logits", Z.jnp.dot(data, coefs))
+        numpyro.sample("obs", dist.Bernoulli(logits=logits), obs=labels)
+
+    pot = potential_from_model(cov_det, (Xc, yc))
+    c = rs.randn(7, 55).astype(np.float32)
+    out = pot.deterministic({"coefs": torch.from_numpy(c)})
+    np.testing.assert_allclose(out["logits"].numpy(), c @ Xc.T, rtol=1e-4, atol=1e-4)

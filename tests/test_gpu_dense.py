@@ -477,7 +477,7 @@ def test_per_chain_dense_adaptation_matches_oracle(device, model):
     oracle's dense-mass NUTS (mass_matrix_sqrt @ eps momentum, M^-1 r in the leapfrog and the
     U-turn dots, hmc_util.py:1183-1220) takes the device's next three trees and draws (>= 95%
     of chains, every mismatch at a rounding-level decision tie)."""
-    from test_gpu_nuts import _explain_mismatches, _first_split, _tie_score
+    from test_gpu_nuts import _explain_mismatches, _first_split
 
     seed, C, W, D = 17, 64, 150, 6
     rs = np.random.RandomState(3)
@@ -530,7 +530,7 @@ def test_per_chain_dense_adaptation_matches_oracle(device, model):
                 s = o.sample(s)
             finally:
                 d, H.DECISIONS = H.DECISIONS, None
-            margins.append(min(d, key=_tie_score) if d else ("none", np.inf))
+            margins.append(H.closest_decision(d))
             ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
         t = _first_split(ok)
         if t < 0:

@@ -38,21 +38,12 @@ def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS",
         finally:
             if margins is not None:
                 d, H.DECISIONS = H.DECISIONS, None
-                margins.append(min(d, key=_tie_score) if d else ("none", np.inf))
+                margins.append(H.closest_decision(d))
         out.append(s)
     return out
 
 
-# A decision is a rounding-level tie when device and oracle can order it differently: the
-# two compute in f32 with different summation orders (potential, kinetic energy, U-turn
-# dots), so energies differ by ~1e-6 relative (ΔE by ~1e-4 absolute for |E| ~ 1e2-1e3) and
-# dot products by ~1e-6 of the magnitude of their terms.
-TIE = {"transition": 2e-3, "accept": 2e-3, "turn": 1e-3, "diverge": 1e-4}
-
-
-def _tie_score(d):
-    kind, m = d
-    return m / TIE[kind]
+TIE = H.TIE  # rounding-level tie bounds of each decision kind (oracle/hmc_ref.py)
 
 
 def _first_split(ok_per_transition):
@@ -66,7 +57,7 @@ def _explain_mismatches(mism, label):
     for c, t, (kind, m) in mism:
         print(f"[{label}] chain {c}: first difference at transition {t}, closest decision {kind} "
               f"margin {m:.3g} (tie bound {TIE.get(kind, 0):.0e})")
-    unexplained = [(c, t, k, m) for c, t, (k, m) in mism if not (k in TIE and m <= TIE[k])]
+    unexplained = [(c, t, k, m) for c, t, (k, m) in mism if not H.is_tie((k, m))]
     assert not unexplained, f"[{label}] mismatches not at a rounding tie: {unexplained}"
 
 
@@ -143,12 +134,15 @@ def _fixed_step_case(model, dim, rs):
         return (r,), P.stochastic_volatility, OP.StochasticVolatility(r, dtype=np.float32), "s", \
             (lambda z: z[..., 1:-1]), 0.005, 0.9, None
     if model == "bnn":
-        H = {46: 5, 321: 16}[dim]
-        X, Y = datasets.bnn_data(N=30, D_X=3)
+        # D = 5038 is BASELINE config 3 (examples/bnn.py: D_X = 3, N = 100, H = 69)
+        H = {46: 5, 321: 16, 5038: 69}[dim]
+        X, Y = datasets.bnn_data(N=100 if H == 69 else 30, D_X=3)
         o = 1 + 3 * H
         # shared well-conditioned start (small weights, prec ~ e): from U(-2, 2) the tanh
-        # layers saturate and |U| ~ 1e3, where fp32 energy rounding flips leaf choices
+        # layers saturate and |U| ~ 1e3, where fp32 energy rounding flips leaf choices; the
+        # hidden-to-hidden weights scale with 1/sqrt(H) so the second layer stays unsaturated
         z0 = (0.3 * rs.randn(64, dim)).astype(np.float32)
+        z0[:, o:] *= np.float32(min(1.0, np.sqrt(5.0 / H)))
         z0[:, 0] = 1.0
         return (X, Y, H), P.bnn, OP.BNN(X, Y, H, dtype=np.float32), "w2", \
             (lambda z: z[..., o:o + H * H]), 0.01, 0.9, z0
@@ -158,7 +152,7 @@ def _fixed_step_case(model, dim, rs):
 @pytest.mark.parametrize("algo", ["NUTS", "HMC"])
 @pytest.mark.parametrize("model,dim", [("logreg", 4), ("logreg", 40), ("diag_normal", 300),
                                        ("diag_normal", 1500), ("funnel", 600), ("sv", 302),
-                                       ("bnn", 46), ("bnn", 321)])
+                                       ("bnn", 46), ("bnn", 321), ("bnn", 5038)])
 def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     """No adaptation, fixed step size: every transition is a deterministic function of
     the Philox stream; device and oracle must take the same discrete path.  D < 257 runs the
@@ -200,6 +194,39 @@ def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     print(f"[fixed-step {algo} {model} D={dim}] {match}/{C} chains reproduce the oracle path and draws")
     _explain_mismatches(mism, f"{algo} {model} D={dim}")
     assert match >= int(frac * C), f"only {match}/{C} chains reproduced the oracle path and draws"
+
+
+def test_covtype_full_size_nuts_matches_oracle(device):
+    """BASELINE config 1 at its full data size (581012 x 55, synthetic covtype): after a device
+    warmup, 8 chains run 2 sampling transitions on the GPU; the oracle's NUTS resumes the same
+    chains from the device's post-warmup state on the same Philox stream, with its potential
+    evaluated by the C restatement over the full data (oracle/c/logreg_batch.c).  Tree sizes
+    must agree and draws to 1e-4 (posterior sd ~3e-3 at this N) for >= 7 of 8 chains, and a
+    chain that leaves the device's path must do so at a rounding-level tie
+    (hmc_util.py:1088-1180 build_tree, examples/covtype.py:66-71)."""
+    from numpyro_amd.random import key_to_seed
+    from oracle import cpu_batched as CB
+
+    X, y = datasets.covtype_synthetic(seed=0)
+    assert X.shape == (581012, 55)
+    C, W, T, seed = 8, 100, 2, 5
+    Xd, yd = torch.from_numpy(X).to(device), torch.from_numpy(y).to(device)
+    mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=W, num_samples=T, num_chains=C)
+    mcmc.warmup(seed, Xd, yd)
+    st = mcmc.post_warmup_state
+    mcmc.run(seed + 1, Xd, yd, extra_fields=("num_steps",))
+    ns = mcmc.get_extra_fields(group_by_chain=True)["num_steps"].cpu().numpy()
+    z = mcmc.get_samples(group_by_chain=True)["coefs"].to(torch.float64).cpu().numpy()
+    cols = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    states, oracles = CB.chains_from_state(
+        cols(st.z["coefs"]), cols(st.z_grad), cols(st.potential_energy), cols(st.adapt_state.step_size),
+        cols(st.adapt_state.inverse_mass_matrix), cols(st.adapt_state.mass_matrix_sqrt), W, key_to_seed(seed + 1), W)
+    _, hist, evals, _ = CB.run_chains(CB.LogRegBatch(X, y), states, oracles, T, record=True)
+    par = CB.compare_paths(hist, ns, z, atol=1e-4)
+    print(f"[covtype 581012x55] {par['matched']}/{C} chains reproduce the device's {T} transitions "
+          f"({evals} oracle leapfrogs; max |dz| on matched paths {par['max_abs_dz']:.2e})")
+    _explain_mismatches([(c, t, (k, m)) for c, t, k, m, _ in par["mismatches"]], "covtype full size")
+    assert par["matched"] >= C - 1
 
 
 def _device_adapt_run(model, dim, C, seed, W):
@@ -292,7 +319,7 @@ def test_adaptation_matches_oracle(device, model, dim, C):
                     st = o.sample(st)
                 finally:
                     d, H.DECISIONS = H.DECISIONS, None
-                margins.append(min(d, key=_tie_score) if d else ("none", np.inf))
+                margins.append(H.closest_decision(d))
                 t = e + k
                 ok.append(st.num_steps == dev["num_steps"][c, t]
                           and np.isclose(dev["step_size"][c, t], st.adapt_state.step_size, rtol=1e-3, atol=0)
@@ -657,6 +684,30 @@ def test_find_heuristic_step_size_matches_oracle(device, model, dim):
             np.testing.assert_allclose(ss[c, t], wa.step_size, rtol=1e-5, err_msg=f"chain {c} after transition {t}")
         moved += int(ss0[c] != 1.0)
     assert moved > 0  # the search changed the initial step size of at least some chains
+
+
+@pytest.mark.parametrize("model,dim", [("diag_normal", 40), ("logreg", 55)])
+def test_find_heuristic_step_size_without_warmup(device, model, dim):
+    """num_warmup = 0: wa_init still runs find_reasonable_step_size whenever adapt_step_size is
+    set (hmc.py:319-339 -> hmc_util.py:572-576), and with no warmup the chains sample at the
+    searched step size.  Oracle: the same search on the same Philox stream from each chain's
+    initial point."""
+    seed, C, S = 31, 64, 3
+    rs = np.random.RandomState(dim)
+    args, fm, ref, *_ = _fixed_step_case(model, dim, rs)
+    eng = NUTS(fm, find_heuristic_step_size=True).make_engine(C, args)
+    eng.initialize(seed, 0)
+    ss0 = eng.chain_state("step_size").cpu().numpy().copy()
+    z0 = eng.chain_state("z").cpu().numpy().copy()
+    _, fields, _ = eng.run(S, seed)
+    ss = fields[:, native.COLLECT.index("step_size"), :C].cpu().numpy().T
+    np.testing.assert_array_equal(ss, np.repeat(ss0[:, None], S, axis=1))
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    for c in range(C):
+        st = H.NUTSOracle(pe_grad, dim, 0, find_heuristic_step_size=True).init(z0[c], seed, c)
+        np.testing.assert_allclose(ss0[c], st.adapt_state.step_size, rtol=1e-6, err_msg=f"chain {c}")
+    assert np.any(ss0 != 1.0)
 
 
 @pytest.mark.parametrize("which", ["covtype", "eight_schools", "funnel_reparam", "sv", "bnn"])
