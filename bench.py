@@ -39,7 +39,11 @@ def parse():
     p.add_argument("--chains", type=int, default=4096, help="total chains over all GPUs")
     p.add_argument("--rows", type=int, default=581012)
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget")
+    p.add_argument("--design", default="iid", choices=["iid", "structured"],
+                   help="synthetic covtype design: iid N(0,1) columns (default) or the real data's structure "
+                        "(one-hot groups collinear with the intercept: depth-saturated trees, datasets.covtype_structured)")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (headline)")
+    p.add_argument("--config-cpu-seconds", type=float, default=10.0, help="CPU baseline budget per config")
     p.add_argument("--cpu-chains", type=int, default=64, help="chains of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
@@ -117,41 +121,102 @@ def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=Non
     return out
 
 
-# BASELINE.json configs[2..4]: (model, args, chains (total), warmup, timed transitions, dense mass,
-# roofline basis).  Short protocols (the adaptation windows of W = 20/50: one or two middle
-# windows), so the default bench run stays within minutes; the headline covtype line keeps the
-# SURVEY §8d protocol.
+# BASELINE.json configs[2..4]: (model, args, chains (total), adaptation transitions, timed
+# transitions, dense mass, roofline basis, CPU-comparator potential).  Each runs in an adapted
+# regime (mcmc.warmup with the reference's window schedule), the timed transitions after it.
 def _config_specs():
     from numpyro_amd import datasets
     from numpyro_amd import potentials as P
+    from oracle import batched as OB
 
     X, Y = datasets.bnn_data(N=100, D_X=3)
     H = 69
     D_bnn = 1 + 3 * H + H * H + H
+    r = datasets.sp500_synthetic()
     return {
         "c2": dict(name="funnel D=10000, dense mass (pooled), examples/funnel.py", model=P.funnel, args=(10000,),
-                   chains=4096, warmup=20, steps=5, dense="pooled", one_gpu=True,
-                   flop=2.0 * 10000 * 10000, basis="2 D^2 FLOP per chain-leapfrog (z = mu + T w, g_w = T^T g_z)"),
+                   chains=4096, warmup=CONFIG_WARMUP["c2"], steps=5, dense="pooled", one_gpu=True,
+                   flop=2.0 * 10000 * 10000, basis="2 D^2 FLOP per chain-leapfrog (z = mu + T w, g_w = T^T g_z)",
+                   cpu=lambda: OB.FunnelBatch(10000), cpu_chains=16),
         "c3": dict(name="BNN D_X=3 N=100 H=69 (D=5038), dense mass (pooled), examples/bnn.py", model=P.bnn,
-                   args=(X, Y, H), chains=2048, warmup=20, steps=5, dense="pooled", one_gpu=True,
+                   args=(X, Y, H), chains=2048, warmup=CONFIG_WARMUP["c3"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * D_bnn * D_bnn + 6.0 * 100 * H * H + 6.0 * 100 * 3 * H,
-                   basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog"),
+                   basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog",
+                   cpu=lambda: OB.BNNBatch(X, Y, H), cpu_chains=16),
         "c4": dict(name="stochastic volatility T=2517 (D=2519), diag mass, examples/stochastic_volatility.py",
-                   model=P.stochastic_volatility, args=(datasets.sp500_synthetic(),), chains=8192, warmup=50,
+                   model=P.stochastic_volatility, args=(r,), chains=8192, warmup=CONFIG_WARMUP["c4"],
                    steps=10, dense=False, one_gpu=False, bytes=7 * 4 * 2519,
-                   basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)"),
+                   basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)",
+                   cpu=lambda: OB.SVBatch(r), cpu_chains=32),
     }
 
 
-def secondary_configs(which, rank, world, device):
+# adaptation transitions per config (the reference examples use 1000; bounded so that the
+# default bench run stays within a few minutes)
+CONFIG_WARMUP = {"c2": 100, "c3": 100, "c4": 200}
+
+
+def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds):
+    """CPU side of a secondary config (SURVEY.md §8d CPU side 2): `cpu_chains` of the oracle's
+    NUTS resumed from the GPU's adapted state of the first chains (whitened coordinates and the
+    pooled whitening T, mu for dense mass; step size, diagonal mass otherwise) on the same
+    Philox stream, their potential calls batched over chains (oracle/batched.py: NumPy float32,
+    products on multithreaded BLAS), run continuously for `seconds`.  Returns the baseline and a
+    parity record of the oracle's transitions against the GPU's timed ones (tree sizes, draws
+    in model space to 1e-3 relative)."""
+    import numpy as np
+    import threadpoolctl
+
+    from oracle import batched as OB
+    from oracle import cpu_batched as CB
+
+    k = min(sp["cpu_chains"], eng.C)
+    st = {n: eng.chain_state(n)[:k].detach().cpu().numpy().copy()
+          for n in ("z", "zgrad", "pe", "step_size", "inv_mass", "mass_sqrt")}
+    f = sp["cpu"]()
+    to_model = None
+    if eng.dense:
+        wt = eng.potential.whitening
+        f = OB.Whitened(f, wt.T.cpu().numpy(), wt.mu.cpu().numpy())
+        st["inv_mass"] = np.ones_like(st["z"])  # identity mass on w (unit_mass on the device)
+        st["mass_sqrt"] = np.ones_like(st["z"])
+        to_model = lambda w: f.to_model(np.asarray(w)[None])[0]  # noqa: E731
+    states, oracles = CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"],
+                                           st["mass_sqrt"], eng.iteration, seed, eng.num_warmup,
+                                           chain_offset=eng.chain_offset)
+    f(np.zeros((k, eng.D), np.float32))  # untimed: BLAS pool, page faults
+    stats = {}
+    t0 = time.perf_counter()
+    _, hist, leap, calls = CB.run_chains(f, states, oracles, 1 << 30, deadline=t0 + seconds, record=True,
+                                         stats=stats)
+    dt = time.perf_counter() - t0
+    trans = sum(len(h) for h in hist)
+    blas = max([p.get("num_threads", 1) for p in threadpoolctl.threadpool_info()] or [1])
+    out = {"value": leap / dt, "unit": "leapfrog/s", "cores": blas, "kind": "port",
+           "sample": f"reduced C={k}: {k} chains of the timed workload (GPU-adapted state, same stream) run "
+                     f"continuously for {dt:.1f}s: {trans} transitions = {leap} leapfrogs in {calls} batched "
+                     f"potential calls; NumPy oracle NUTS (oracle/hmc_ref.py) with the potential batched over "
+                     f"chains (oracle/batched.py, float32, BLAS products)" +
+                     ("; dense mass as the whitened identity-mass chain with the GPU's pooled T, mu"
+                      if eng.dense else ""),
+           "potential_share": stats["pot_s"] / dt, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    par = CB.compare_paths(hist, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model)
+    par["mismatches_at_tie"] = sum(1 for m in par["mismatches"] if m[4])
+    par["mismatches"] = [list(m) for m in par["mismatches"]]
+    return out, par
+
+
+def secondary_configs(which, rank, world, device, cpu_seconds):
     """Leapfrogs/s of the BASELINE.json secondary configs on synthetic data of their shape:
-    untimed adaptation, then `steps` transitions timed between barrier + synchronize (max over
-    ranks); value = sum(num_steps) over all ranks / wall."""
+    adaptation (untimed; its tree sizes and divergences reported), then `steps` transitions
+    timed between barrier + synchronize (max over ranks); value = sum(num_steps) over all
+    ranks / wall.  At one rank each config also gets its CPU comparator and parity record."""
     import torch
     import torch.distributed as dist
 
     from numpyro_amd import shard
     from numpyro_amd.infer import MCMC, NUTS, shard_chains
+    from numpyro_amd.random import key_to_seed
 
     out = {}
     specs = _config_specs()
@@ -160,15 +225,24 @@ def secondary_configs(which, rank, world, device):
         if sp["one_gpu"] and world > 1:
             continue
         lo, hi = shard_chains(sp["chains"], rank, world)
+        # postprocess_fn: the draws stay unconstrained (model coordinates), as the CPU
+        # comparator's chains hold them
         mcmc = MCMC(NUTS(sp["model"], dense_mass=sp["dense"]), num_warmup=sp["warmup"], num_samples=sp["steps"],
-                    num_chains=hi - lo, chain_offset=lo, progress_bar=False)
+                    num_chains=hi - lo, chain_offset=lo, progress_bar=False, postprocess_fn=_identity)
         t0 = time.perf_counter()
-        mcmc.warmup(7, *sp["args"])
+        mcmc._fields_only = True  # the adaptation's tree sizes and divergences, not its draws
+        mcmc.warmup(7, *sp["args"], collect_warmup=True, extra_fields=("num_steps", "diverging"))
+        mcmc._fields_only = False
         torch.cuda.synchronize()
         setup_s = time.perf_counter() - t0
+        wf = mcmc.get_extra_fields(group_by_chain=True)
+        w_ns = wf["num_steps"].to(torch.float64)
+        wst = torch.tensor([w_ns.sum().item(), float(wf["diverging"].sum().item())], dtype=torch.float64,
+                           device=device)
         # the potential launches (dense: whitening products + model kernel + column packing)
         # timed with HIP events on their stream inside the timed region, as for the headline
-        pot = mcmc._engine.potential
+        eng = mcmc._engine
+        pot = eng.potential
         orig_eval, evs = pot.evaluate, []
         stream = torch.cuda.current_stream()
 
@@ -192,20 +266,24 @@ def secondary_configs(which, rank, world, device):
         wall = time.perf_counter() - t0
         pot.evaluate = orig_eval
         pot_ms = sum(a.elapsed_time(b) for a, b in evs)
-        ef = mcmc.get_extra_fields()
+        ef = mcmc.get_extra_fields(group_by_chain=True)
         st = torch.tensor([ef["num_steps"].to(torch.float64).sum().item(), wall,
                            float(ef["diverging"].sum().item())], dtype=torch.float64, device=device)
         if world > 1:
             tot, mx = st.clone(), st.clone()
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(wst)
             leap, wall, div = tot[0].item(), mx[1].item(), tot[2].item()
         else:
             leap, div = st[0].item(), st[2].item()
-        r = {"workload": sp["name"], "num_chains": sp["chains"], "warmup": sp["warmup"], "steps": sp["steps"],
+        n_ch, W = sp["chains"], sp["warmup"]
+        r = {"workload": sp["name"], "num_chains": n_ch, "warmup": W, "steps": sp["steps"],
              "value": leap / wall, "unit": "leapfrog/s", "ms_per_step": wall * 1e3 / sp["steps"],
-             "mean_tree_size": leap / (sp["chains"] * sp["steps"]), "divergent_frac": div / (sp["chains"] * sp["steps"]),
-             "adapt_wall_s": setup_s, "dense_mass": sp["dense"] or False}
+             "mean_tree_size": leap / (n_ch * sp["steps"]), "divergent_frac": div / (n_ch * sp["steps"]),
+             "adapt_wall_s": setup_s, "adapt_leapfrogs": wst[0].item(),
+             "adapt_leapfrog_per_s": wst[0].item() / setup_s, "adapt_mean_tree_size": wst[0].item() / (n_ch * W),
+             "adapt_divergent_frac": wst[1].item() / (n_ch * W), "dense_mass": sp["dense"] or False}
         if "flop" in sp:
             tf = sp["flop"] * leap / wall / 1e12
             peak = MI355X_BF16_MFMA_PEAK_TFLOPS / SPLIT_PRODUCTS
@@ -221,23 +299,37 @@ def secondary_configs(which, rank, world, device):
             gbs = sp["bytes"] * leap / wall / 1e9
             r["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": gbs / MI355X_HBM_PEAK_GBS, "basis": sp["basis"] + " over the sampling wall time"}
+        # end-of-run exchange: cross-chain split R-hat over ranks (+ sample
+        # gather for the sharded config); R-hat of the timed draws is the regime check
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        sm = mcmc.get_samples(group_by_chain=True)
+        rh = max(float(shard.split_gelman_rubin(v.reshape(v.shape[0], v.shape[1], -1)).max()) for v in sm.values())
+        r["max_split_rhat"] = rh
         if not sp["one_gpu"]:
-            # end-of-run exchange: cross-chain R-hat / ESS over ranks + sample gather
-            torch.cuda.synchronize()
-            te = time.perf_counter()
-            s_site = mcmc.get_samples(group_by_chain=True)["s"]
-            rhat = shard.split_gelman_rubin(s_site) if s_site.shape[1] >= 4 else None
-            gathered = shard.gather_chains(s_site[:, :, :8])
+            gathered = shard.gather_chains(sm["s"][:, :, :8])
             torch.cuda.synchronize()
             r["end_of_run"] = {"ms": (time.perf_counter() - te) * 1e3, "gathered_chains": int(gathered.shape[0]),
-                               "max_split_rhat": float(rhat.max()) if rhat is not None else None,
                                "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"}
             r["parallelism"] = f"chains sharded {world}-way (no data-path collective)"
             r["scaling"] = "strong"
+        if world == 1 and rank == 0 and cpu_seconds > 0:
+            k = min(sp["cpu_chains"], eng.C)
+            dev_ns = ef["num_steps"][:k].cpu().numpy()
+            dev_z = mcmc._samples[:, :, :k].permute(2, 0, 1).to(torch.float64).cpu().numpy()  # model space
+            # resume the CPU chains from the post-warmup state (the timed run moved the engine on)
+            from numpyro_amd.infer.hmc import restore_state
+            restore_state(eng, mcmc.post_warmup_state)
+            cb, par = cpu_baseline_config(sp, eng, key_to_seed(8), dev_ns, dev_z, cpu_seconds)
+            r["cpu_baseline"], r["parity"] = cb, par
         out[key] = r
-        del mcmc
+        del mcmc, eng, pot
         torch.cuda.empty_cache()
     return out
+
+
+def _identity(z):
+    return z
 
 
 def main():
@@ -264,7 +356,13 @@ def main():
     from numpyro_amd.infer import MCMC, NUTS, shard_chains
     from numpyro_amd.random import key_to_seed
 
-    X, y = datasets.covtype_synthetic(n_rows=args.rows, seed=0)
+    if args.design == "structured":
+        X, y = datasets.covtype_structured(n_rows=args.rows, seed=0)
+        data_desc = ("synthetic covtype, real-data column structure (10 correlated quantitative + one-hot 4 wilderness "
+                     "+ 40 soil types, standardized + intercept; y~Bernoulli(sigmoid(X@ref_coefs)))")
+    else:
+        X, y = datasets.covtype_synthetic(n_rows=args.rows, seed=0)
+        data_desc = "synthetic covtype (581012x54 N(0,1) standardized + intercept, y~Bernoulli(sigmoid(X@ref_coefs)))"
     lo, hi = shard_chains(args.chains, rank, world)
     kernel = NUTS(P.logistic_regression)
     mcmc = MCMC(kernel, num_warmup=args.adapt, num_samples=args.warmup, num_chains=hi - lo,
@@ -363,10 +461,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic covtype (581012x54 N(0,1) standardized + intercept, y~Bernoulli(sigmoid(X@ref_coefs)))",
+            "data": data_desc,
             "config": {"workload": "covtype logistic regression NUTS, diag mass, max_tree_depth 10",
                        "num_chains": args.chains, "rows": args.rows, "dim": int(X.shape[1]),
-                       "adapt_transitions": args.adapt,
+                       "adapt_transitions": args.adapt, "design": args.design,
                        "parallelism": f"chains sharded {world}-way (no data-path collective)",
                        "schedule": "lockstep" if args.sync_chains else "per-chain async"},
             "useful_leapfrogs": useful,
@@ -399,7 +497,8 @@ def main():
     if args.configs != "none":
         del mcmc, eng, pot, start_state
         torch.cuda.empty_cache()
-        cfgs = secondary_configs(args.configs, rank, world, device)
+        cfgs = secondary_configs(args.configs, rank, world, device,
+                                 0.0 if args.no_cpu_baseline else args.config_cpu_seconds)
         if rank == 0:
             out["configs"] = cfgs
     if rank == 0:

@@ -39,6 +39,12 @@ COMMON_FLAGS = [
 ]
 
 
+# per-file flags: the covtype kernel's epilogue and residual split stay scalar VALU (the SLP
+# vectorizer would pair them into v_pk_*_f32, which issue slower beside MFMAs on gfx950;
+# potential_logreg.hip x3_epi_one)
+FILE_FLAGS = {"potential_logreg.hip": ["-fno-slp-vectorize"]}
+
+
 def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
 
@@ -74,7 +80,8 @@ def build(verbose: bool = False, jobs: int | None = None, debug: bool = False) -
     jobs = jobs or min(8, os.cpu_count() or 4, max(1, len(todo)))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = [ex.submit(_compile, s, o, extra) for s, o in todo]
+            futs = [ex.submit(_compile, s, o, (*extra, *FILE_FLAGS.get(os.path.basename(s), ())))
+                    for s, o in todo]
             for f in futs:
                 f.result()
             if verbose:

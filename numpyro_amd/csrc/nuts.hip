@@ -1149,8 +1149,16 @@ __global__ __launch_bounds__(64) void k_wide_s(WideArgs W) {
   end_step(cfg, a, c, valid, ph_in, S, A);
 }
 
-__global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
-  __shared__ float lds[WIDE_WAVES * 64];
+#ifndef NMX_V2_WAVES
+#define NMX_V2_WAVES 4
+#endif
+#ifndef NMX_V2_BATCH
+#define NMX_V2_BATCH 2
+#endif
+constexpr int V2_WAVES = NMX_V2_WAVES;  // waves per V2 block: each takes momentum blocks wv, wv + V2_WAVES, ...
+
+__global__ __launch_bounds__(64 * V2_WAVES) void k_wide_v2(WideArgs W) {
+  __shared__ float lds[V2_WAVES * 64];
   const nmx_nuts_config& cfg = W.p.cfg;
   const Arena& a = W.p.a;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1192,15 +1200,15 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v2(WideArgs W) {
   float ke0[1] = {0.0f};
   if (act & VEC) {
     const int b0 = (s * W.sw) / 4, b1 = (min(D, (s + 1) * W.sw) + 3) / 4;
-    for (int blk = b0 + wv; blk < b1; blk += WIDE_WAVES) {
+    for (int blk = b0 + wv; blk < b1; blk += V2_WAVES) {
       float n[4] = {0.f, 0.f, 0.f, 0.f};
       if (A.start_iter) momentum_block(cfg.seed, gch, it, blk, n);
       // rows in pairs: 95 VGPRs, 5 waves per SIMD (all four rows' loads first: 121 VGPRs, 4
       // waves; SV 1024 chains 3.58M vs 3.93M leapfrog/s, funnel-10k diag 658k vs 717k)
-      ke0[0] += apply_block<2>(v, A, step_eff, blk, c, n, samp, W.p.transform, cfg);
+      ke0[0] += apply_block<NMX_V2_BATCH>(v, A, step_eff, blk, c, n, samp, W.p.transform, cfg);
     }
   }
-  block_sum<WIDE_WAVES, 1>(ke0, lds);
+  block_sum<V2_WAVES, 1>(ke0, lds);
   if (wv == 0 && A.start_iter) a.part0[(size_t)s * ldc + c] = ke0[0];
 }
 
@@ -1810,7 +1818,7 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
     hipLaunchKernelGGL(k_wide_v1, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
     hipLaunchKernelGGL(k_wide_r, dim3(grid, NPART + 1), dim3(64 * WIDE_SWAVES), 0, s, w);
     hipLaunchKernelGGL(k_wide_s, dim3(grid), dim3(64), 0, s, w);
-    hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
+    hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * V2_WAVES), 0, s, w);
     return nmx_check_launch("k_nuts_step (wide)");
   }
   if (tpc_for_dim(cfg->dim) == 1)
@@ -1836,7 +1844,7 @@ int launch_wide_model(const WideArgs& w, const M& m, char* ws, int ldc, hipStrea
   hipLaunchKernelGGL(k_wide_leaf<M>, dim3(grid, w.ns), dim3(64 * WIDE_WAVES), 0, s, w, m, ppart);
   hipLaunchKernelGGL(k_wide_rs<M>, dim3(grid, NPART + 1 + M::NSUM), dim3(64 * WIDE_SWAVES), 0, s, w, m,
                      (const float*)ppart, ptot, cnt);
-  hipLaunchKernelGGL(k_wide_v2, dim3(grid, w.ns), dim3(64 * WIDE_WAVES), 0, s, w);
+  hipLaunchKernelGGL(k_wide_v2, dim3(grid, w.ns), dim3(64 * V2_WAVES), 0, s, w);
   return nmx_check_launch("nmx_nuts_step_wide_model");
 }
 }  // namespace

@@ -95,6 +95,14 @@ constexpr float LN2 = 0.6931471805599453f;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// VALU instructions the scheduling hints place after each GEMM1(k+1) / GEMM2(k) MFMA (x3_item)
+#ifndef NMX_X3_VALU1
+#define NMX_X3_VALU1 5
+#endif
+#ifndef NMX_X3_VALU2
+#define NMX_X3_VALU2 3
+#endif
+
 constexpr int X3_ROWS = 32;
 constexpr int X3_MAX_S = 256;
 
@@ -235,44 +243,36 @@ __device__ __forceinline__ void x3_labels_wait(f32x4 (&y4)[4]) {
 //   residual:  R' = y - sigmoid(l) = (y - 1/2) + copysign(1/(1+e) - 1/2, m)
 //              (sigmoid(l) - 1/2 = copysign(1/(1+e) - 1/2, l), sign(l) = -sign(m)); GEMM2
 //              accumulates X^T R' = -X^T (sigmoid(l) - y) and the finalize subtracts it.
-// Labels come as y - 1/2.  Per value: exp and rcp, 1/2 of a packed add (1 + e), 1/2 packed
-// mul (product), 1/2 packed add (- 1/2), one bitfield insert (copysign), 1/2 packed add
-// (+ label), one add (|m|): the even and odd rows keep separate products (each <= 2^8).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void x3_epi_pair(const f32x16& acc, const f32x4 (&yh4)[4], int p, float (&res)[16],
-                                            float& lin, f32x2& prod) {
-  const int r0 = 2 * p, r1 = 2 * p + 1;
-  const float m0 = acc[r0], m1 = acc[r1];
-  f32x2 e;
-  e.x = __builtin_amdgcn_exp2f(-fabsf(m0));
-  e.y = __builtin_amdgcn_exp2f(-fabsf(m1));
-  const f32x2 ope = e + 1.0f;
+// Labels come as y - 1/2.  Per value: exp and rcp, one add (1 + e), one mul (product), one
+// add (- 1/2), one bitfield insert (copysign), one add (+ label), one add (|m|); the even and
+// odd rows keep separate products (each <= 2^8).  All scalar VALU: packed f32 (v_pk_*_f32)
+// beside MFMAs costs extra issue cycles per pair on gfx950 (MI355X_MICROARCH.md, VALU/MFMA
+// co-issue), so this file is also compiled without the SLP vectorizer (build.py FILE_FLAGS).
+__device__ __forceinline__ void x3_epi_one(float m, float yh, float& res, float& lin, float& prod) {
+  const float e = __builtin_amdgcn_exp2f(-fabsf(m));
+  const float ope = e + 1.0f;
   prod = prod * ope;
-  f32x2 inv;
-  inv.x = __builtin_amdgcn_rcpf(ope.x);
-  inv.y = __builtin_amdgcn_rcpf(ope.y);
-  const f32x2 hh = inv - 0.5f;
+  const float hh = __builtin_amdgcn_rcpf(ope) - 0.5f;
   constexpr unsigned SB = 0x80000000u;
-  f32x2 sg;
-  sg.x = __uint_as_float((__float_as_uint(m0) & SB) | (__float_as_uint(hh.x) & ~SB));
-  sg.y = __uint_as_float((__float_as_uint(m1) & SB) | (__float_as_uint(hh.y) & ~SB));
-  f32x2 yh;
-  yh.x = yh4[r0 >> 2][r0 & 3];
-  yh.y = yh4[r1 >> 2][r1 & 3];
-  const f32x2 rr = sg + yh;
-  res[r0] = rr.x;
-  res[r1] = rr.y;
-  lin += fabsf(m0);
-  lin += fabsf(m1);
+  const float sg = __uint_as_float((__float_as_uint(m) & SB) | (__float_as_uint(hh) & ~SB));
+  res = sg + yh;
+  lin += fabsf(m);
 }
 
-__device__ __forceinline__ void x3_epi_finish(float lin, f32x2 prod, double& pe) {
-  pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod.x * prod.y) * (double)LN2;
+__device__ __forceinline__ void x3_epi_pair(const f32x16& acc, const f32x4 (&yh4)[4], int p, float (&res)[16],
+                                            float& lin, float (&prod)[2]) {
+  const int r0 = 2 * p, r1 = 2 * p + 1;
+  x3_epi_one(acc[r0], yh4[r0 >> 2][r0 & 3], res[r0], lin, prod[0]);
+  x3_epi_one(acc[r1], yh4[r1 >> 2][r1 & 3], res[r1], lin, prod[1]);
+}
+
+__device__ __forceinline__ void x3_epi_finish(float lin, const float (&prod)[2], double& pe) {
+  pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod[0] * prod[1]) * (double)LN2;
 }
 
 __device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&yh4)[4], float (&res)[16], double& pe) {
   float lin = 0.0f;
-  f32x2 prod = {1.0f, 1.0f};
+  float prod[2] = {1.0f, 1.0f};
 #pragma unroll
   for (int p = 0; p < 8; ++p) x3_epi_pair(acc, yh4, p, res, lin, prod);
   x3_epi_finish(lin, prod, pe);
@@ -419,13 +419,13 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
           // and 1-3 VALU per group all within 1.5%.
 #pragma unroll
           for (int i = 0; i < 6 * KB; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);            // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, NMX_X3_VALU1, 0);  // VALU
           }
 #pragma unroll
           for (int i = 0; i < 12 * DT; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, NMX_X3_VALU2, 0);
           }
         }
       };
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
 #pragma unroll
         for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
         float lin = 0.0f;
-        f32x2 prod = {1.0f, 1.0f};
+        float prod[2] = {1.0f, 1.0f};
         bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {

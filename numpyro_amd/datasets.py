@@ -45,6 +45,43 @@ def covtype_synthetic(n_rows: int = COVTYPE_N, seed: int = 0):
     return X, y
 
 
+def covtype_structured(n_rows: int = COVTYPE_N, seed: int = 0):
+    """Synthetic covtype with the real data's column structure (numpyro/examples/datasets.py
+    COVTYPE: 10 quantitative columns, then one-hot wilderness area (4) and soil type (40)), all
+    54 columns standardized as examples/covtype.py:48 does, + intercept.  Each one-hot group
+    sums to one, so after standardization both groups are collinear with the intercept: the
+    likelihood leaves two directions to the N(0, 1) prior while the others have posterior sd
+    ~1/sqrt(N), which is why NUTS on the real covtype saturates its trees (~948 leapfrogs per
+    transition, notebooks/source/logistic_regression.ipynb:237).  Soil types follow a skewed
+    (Zipf-like) frequency as in the real data; quantitative columns are correlated Gaussians.
+    y ~ Bernoulli(sigmoid(X @ ref_coefs)).  Returns (X float32 [n, 55], y float32 [n])."""
+    rs = np.random.Generator(np.random.PCG64(seed))
+    q = 10
+    A = rs.standard_normal((q, q)) * 0.4 + np.eye(q)
+    quant = (rs.standard_normal((n_rows, q)) @ A.T).astype(np.float32)
+    wild_p = np.array([0.45, 0.05, 0.44, 0.06])
+    soil_p = 1.0 / np.arange(1, 41) ** 1.3
+    soil_p = soil_p[rs.permutation(40)]
+    soil_p /= soil_p.sum()
+    wild = rs.choice(4, size=n_rows, p=wild_p)
+    soil = rs.choice(40, size=n_rows, p=soil_p)
+    feats = np.zeros((n_rows, COVTYPE_FEATURES), np.float32)
+    feats[:, :q] = quant
+    feats[np.arange(n_rows), q + wild] = 1.0
+    feats[np.arange(n_rows), q + 4 + soil] = 1.0
+    mu = feats.mean(0, dtype=np.float64)
+    sd = feats.std(0, dtype=np.float64)
+    sd[sd == 0] = 1.0
+    feats = ((feats - mu) / sd).astype(np.float32)
+    X = np.empty((n_rows, COVTYPE_FEATURES + 1), np.float32)
+    X[:, :COVTYPE_FEATURES] = feats
+    X[:, COVTYPE_FEATURES] = 1.0
+    logits = X.astype(np.float64) @ COVTYPE_REF_COEFS
+    p = 1.0 / (1.0 + np.exp(-logits))
+    y = (rs.random(n_rows) < p).astype(np.float32)
+    return X, y
+
+
 def sp500_synthetic(T: int = SP500_T, seed: int = 0):
     """Synthetic daily returns: log-vol random walk (sigma 0.02) + StudentT(10) noise."""
     rs = np.random.Generator(np.random.PCG64(seed))

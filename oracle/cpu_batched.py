@@ -177,12 +177,13 @@ def chains_from_state(z, grad, pe, step_size, inverse_mass, mass_sqrt, it0, seed
     return states, oracles
 
 
-def compare_paths(hist, dev_num_steps, dev_z, atol):
+def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None):
     """Per-chain parity of oracle histories (run_chains(record=True)) with the device's
     transitions from the same state: a chain matches while its tree sizes are equal and its
-    draws agree to `atol`; at the first difference the oracle's closest decision to a tie is
-    reported.  Returns {chains, transitions, matched, max_abs_dz, mismatches: [(chain,
-    transition, kind, margin, is_tie)]}."""
+    draws agree to atol + rtol |z| (`to_model` maps the oracle's coordinates to the device
+    draws' first, e.g. whitened -> model space); at the first difference the oracle's closest
+    decision to a tie is reported.  Returns {chains, transitions, matched, max_abs_dz,
+    mismatches: [(chain, transition, kind, margin, is_tie)]}."""
     matched, transitions, max_dz, mism = 0, 0, 0.0, []
     for c, h in enumerate(hist):
         T = min(len(h), dev_num_steps.shape[1])
@@ -190,7 +191,9 @@ def compare_paths(hist, dev_num_steps, dev_z, atol):
         bad = None
         for t in range(T):
             st, log = h[t]
-            dz = float(np.max(np.abs(np.asarray(st.z, np.float64) - dev_z[c, t])))
+            z = np.asarray(st.z, np.float64) if to_model is None else np.asarray(to_model(st.z), np.float64)
+            ref = np.asarray(dev_z[c, t], np.float64)
+            dz = float(np.max(np.abs(z - ref) - rtol * np.abs(ref)))
             if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
                 bad = t
                 d = H.closest_decision(log)

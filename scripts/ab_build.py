@@ -16,10 +16,15 @@ src = os.path.join(ROOT, "numpyro_amd", "csrc", sys.argv[1])
 objs = [o for o in glob.glob(os.path.join(B.OBJ_DIR, "*.o")) if os.path.basename(o) != os.path.basename(src) + ".o"]
 for spec in sys.argv[2:]:
     name, _, flags = spec.partition("=")
+    if flags.startswith("@"):  # name=@path/to/variant.hip [flags]: another version of the source
+        path, _, flags = flags[1:].partition(" ")
+        src_v = os.path.abspath(path)
+    else:
+        src_v = src
     out = os.path.join(ROOT, "build", "ab", name)
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, os.path.basename(src) + ".o")
-    cmd = [B.HIPCC, *B.COMMON_FLAGS, *shlex.split(flags), "-x", "hip", "-c", src, "-o", obj]
+    cmd = [B.HIPCC, *B.COMMON_FLAGS, *shlex.split(flags), "-x", "hip", "-c", src_v, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         sys.exit(f"{name}: compile failed\n{r.stderr[-3000:]}")

@@ -57,3 +57,37 @@ def test_batched_chains_are_the_oracle_chains():
             assert a.num_steps == b.num_steps
             np.testing.assert_array_equal(a.z, b.z)
             assert a.adapt_state.step_size == b.adapt_state.step_size
+
+
+def test_fixed_batch_mode_and_path_comparison():
+    """run_chains(deadline=...) keeps every chain running until the deadline (the CPU
+    comparator's fixed batch); record=True returns each transition's decisions, and
+    compare_paths reports a chain whose tree sizes or draws leave the reference's with the
+    closest decision to a tie."""
+    import time
+
+    X, y = _data(N=200, D=5, seed=3)
+    ref = OP.LogisticRegression(X, y, dtype=np.float32)
+
+    def rowwise(Z):
+        out = [ref.pe_grad(z) for z in Z]
+        return np.array([o[0] for o in out], np.float32), np.stack([o[1] for o in out])
+
+    seed, n, W = 9, 4, 10
+    mk = lambda: ([H.NUTSOracle(ref.pe_grad, 5, W).init(philox.init_uniform(seed, c, 0, 5), seed, c)  # noqa: E731
+                   for c in range(n)], [H.NUTSOracle(None, 5, W) for _ in range(n)])
+    states, oracles = mk()
+    t0 = time.perf_counter()
+    _, hist, evals, _ = CB.run_chains(rowwise, states, oracles, 1 << 30, deadline=t0 + 0.5, record=True)
+    assert all(len(h) >= 2 for h in hist) and evals > 0
+    st, log = hist[0][0]
+    assert isinstance(log, list) and all(k in H.TIE for k, _ in log)
+    T = min(len(h) for h in hist)
+    ns = np.array([[h[t][0].num_steps for t in range(T)] for h in hist])
+    zs = np.array([[h[t][0].z for t in range(T)] for h in hist], np.float64)
+    par = CB.compare_paths(hist, ns, zs, atol=0.0)
+    assert par["matched"] == n and par["transitions"] == n * T and not par["mismatches"]
+    ns_bad = ns.copy()
+    ns_bad[1, 1] += 1
+    par = CB.compare_paths(hist, ns_bad, zs, atol=0.0)
+    assert par["matched"] == n - 1 and par["mismatches"][0][:2] == (1, 1)
