@@ -117,6 +117,22 @@ __device__ __forceinline__ float nmx_sigmoid(float x) {
 }
 
 // Chain evaluated at batch position `pos` of a potential launch, or -1.
+// Element (d, c) of a chain-minor [D][ldc] field as a 32-bit byte offset.  Every field (and
+// every checkpoint level) of the arena is < 4 GiB, so an access takes the SGPR-base + 32-bit
+// VGPR-offset form of the global load / store and one offset register serves every field of a
+// row (64-bit per-field addresses cost two VGPRs each and a 64-bit add per access).
+__device__ __forceinline__ uint32_t nmx_row_off(int d, int ldc, int c) {
+  return ((uint32_t)d * (uint32_t)ldc + (uint32_t)c) << 2;
+}
+template <class T>
+__device__ __forceinline__ T& nmx_at(T* base, uint32_t off) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+}
+template <class T>
+__device__ __forceinline__ const T& nmx_at(const T* base, uint32_t off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+}
+
 __device__ __forceinline__ int nmx_eval_chain(const nmx_eval_batch& ev, int pos) {
   if (ev.active_idx) {
     if (pos >= *ev.active_count) return -1;

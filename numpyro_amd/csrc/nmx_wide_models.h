@@ -49,11 +49,13 @@ struct NmxWideSV {
     return g;
   }
   // dU/ds_t of row d = 1 + t (GaussianRandomWalk stencil + StudentT(nu, 0, e^s) term)
-  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob& g, float* sums) const {
+  // (off: nmx_row_off(d, ldc, c); ldc4 = 4 ldc, the byte stride between rows)
+  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
+                                       float* sums) const {
     const int t = d - 1;
-    const float s = z[(size_t)d * ldc + c];
-    const float sp = t > 0 ? z[(size_t)(d - 1) * ldc + c] : 0.0f;
-    const float sn = t + 1 < T ? z[(size_t)(d + 1) * ldc + c] : 0.0f;
+    const float s = nmx_at(z, off);
+    const float sp = t > 0 ? nmx_at(z, off - ldc4) : 0.0f;
+    const float sn = t + 1 < T ? nmx_at(z, off + ldc4) : 0.0f;
     const float dd = s - sp;
     const float dn = t + 1 < T ? sn - s : 0.0f;
     const float r = ret[t];
@@ -106,8 +108,8 @@ struct NmxWideFunnel {
     g.e = expf(-g.y);
     return g;
   }
-  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob& g, float* sums) const {
-    const float x = z[(size_t)d * ldc + c];
+  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t, int, const Glob& g, float* sums) const {
+    const float x = nmx_at(z, off);
     sums[0] += x * x;
     return x * g.e;
   }
@@ -136,8 +138,8 @@ struct NmxWideFunnelNC {
     g.y = z[(size_t)(dim - 1) * ldc + c];
     return g;
   }
-  __device__ __forceinline__ float row(const float* z, int ldc, int c, int d, const Glob&, float* sums) const {
-    const float x = z[(size_t)d * ldc + c];
+  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t, int, const Glob&, float* sums) const {
+    const float x = nmx_at(z, off);
     sums[0] += x * x;
     return x;
   }

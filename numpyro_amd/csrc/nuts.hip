@@ -568,55 +568,55 @@ struct LeafIn {
 };
 
 template <bool NUTS, bool PRE, bool LOADG = true>
-__device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, size_t idx, LeafIn& x) {
+__device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, uint32_t off, LeafIn& x) {
   const Arena& a = *v.a;
-  if constexpr (LOADG) x.g = AV(NMX_F_G_EVAL)[idx];
-  x.rf = (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
-  x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
+  if constexpr (LOADG) x.g = nmx_at(AV(NMX_F_G_EVAL), off);
+  x.rf = nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+  x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
   if constexpr (NUTS) {
-    x.rs_old = A.k == 0 ? 0.0f : AV(NMX_F_RSUM_SUB)[idx];
+    x.rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
     if (A.tree_chk) {
-      x.rst = AV(NMX_F_RSUM)[idx];
-      x.ro = (A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx];  // the other end's momentum
+      x.rst = nmx_at(AV(NMX_F_RSUM), off);
+      x.ro = nmx_at((A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR)), off);  // the other end's momentum
     }
     // checkpoints read by the U-turn check; the range is empty for even leaves, whose
     // checkpoint write below therefore never feeds this step's check (:1036-1047)
 #pragma unroll
     for (int i = 0; i < MAXD; ++i) {
       if (PRE && i >= A.imin && i <= A.imax) {
-        x.ckr[i] = a.ckr[i * v.ck_stride + idx];
-        x.ckrs[i] = a.ckrs[i * v.ck_stride + idx];
+        x.ckr[i] = nmx_at(a.ckr + i * v.ck_stride, off);
+        x.ckrs[i] = nmx_at(a.ckrs + i * v.ck_stride, off);
       }
     }
   }
 }
 
 template <bool NUTS, bool PRE>
-__device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float seff, size_t idx, const LeafIn& x,
+__device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float seff, uint32_t off, const LeafIn& x,
                                            float* red) {
   const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
   const float r = x.rf - half * x.g;
-  (A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = r;
+  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
   // the moving end's z / grad stay in Z_EVAL / G_EVAL (the frontier); apply_store saves
   // them into the side arrays only when the next doubling turns around
   const float im = x.im;
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
     const float rs = (A.k == 0) ? r : x.rs_old + r;
-    AV(NMX_F_RSUM_SUB)[idx] = rs;
+    nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
     if ((A.k & 1) == 0) {  // checkpoint update (:1040-1047)
-      a.ckr[A.imax * v.ck_stride + idx] = r;
-      a.ckrs[A.imax * v.ck_stride + idx] = rs;
+      nmx_at(a.ckr + A.imax * v.ck_stride, off) = r;
+      nmx_at(a.ckrs + A.imax * v.ck_stride, off) = rs;
     }
     // _is_iterative_turning (:961-981): all checkpoints in [imin, imax]; the reference
     // stops at the first turning one, the OR over them is the same predicate.
 #pragma unroll
     for (int i = 0; i < MAXD; ++i) {
       if (i >= A.imin && i <= A.imax) {
-        const float rl = PRE ? x.ckr[i] : a.ckr[i * v.ck_stride + idx];
-        const float rsub = (rs - (PRE ? x.ckrs[i] : a.ckrs[i * v.ck_stride + idx])) + rl;
+        const float rl = PRE ? x.ckr[i] : nmx_at(a.ckr + i * v.ck_stride, off);
+        const float rsub = (rs - (PRE ? x.ckrs[i] : nmx_at(a.ckrs + i * v.ck_stride, off))) + rl;
         const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
         red[1 + 2 * i] += (im * rl) * rss;
         red[2 + 2 * i] += (im * r) * rss;
@@ -642,7 +642,7 @@ __device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float s
   if constexpr (ROWS == 2) {
     for (; d + step < d1; d += 2 * step) {
       LeafIn x0, x1;
-      const size_t i0 = (size_t)d * v.ldc + c, i1 = (size_t)(d + step) * v.ldc + c;
+      const uint32_t i0 = nmx_row_off(d, v.ldc, c), i1 = nmx_row_off(d + step, v.ldc, c);
       leaf_load<NUTS, true>(v, A, i0, x0);
       leaf_load<NUTS, true>(v, A, i1, x1);
       leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
@@ -651,7 +651,7 @@ __device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float s
   }
   for (; d < d1; d += step) {
     LeafIn x0;
-    const size_t i0 = (size_t)d * v.ldc + c;
+    const uint32_t i0 = nmx_row_off(d, v.ldc, c);
     leaf_load<NUTS, PRE1>(v, A, i0, x0);
     leaf_store<NUTS, PRE1>(v, A, seff, i0, x0, red);
   }
@@ -677,37 +677,37 @@ struct ApplyIn {
 
 __device__ __forceinline__ bool turn_around(const Act& A) { return A.prep_leaf && A.new_dir != A.dirR; }
 
-__device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t idx, ApplyIn& x) {
+__device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32_t off, ApplyIn& x) {
   const Arena& a = *v.a;
   if (A.take_leaf || A.hmc_accept || A.prep_leaf) {
-    x.ze = AV(NMX_F_Z_EVAL)[idx];
-    x.ge = AV(NMX_F_G_EVAL)[idx];
+    x.ze = nmx_at(AV(NMX_F_Z_EVAL), off);
+    x.ge = nmx_at(AV(NMX_F_G_EVAL), off);
   }
   if (A.done_sub) {
-    x.rst = AV(NMX_F_RSUM)[idx];
-    x.rss = AV(NMX_F_RSUM_SUB)[idx];
+    x.rst = nmx_at(AV(NMX_F_RSUM), off);
+    x.rss = nmx_at(AV(NMX_F_RSUM_SUB), off);
   }
   if (A.take_biased && !A.take_leaf) {
-    x.zs = AV(NMX_F_ZSUB)[idx];
-    x.gs = AV(NMX_F_GSUB)[idx];
+    x.zs = nmx_at(AV(NMX_F_ZSUB), off);
+    x.gs = nmx_at(AV(NMX_F_GSUB), off);
   }
   const bool need_state = (A.iter_done || A.start_iter) && !A.take_biased && !A.hmc_accept;
   if (need_state) {
-    x.zp = AV(NMX_F_Z)[idx];
-    x.gp = AV(NMX_F_ZGRAD)[idx];
+    x.zp = nmx_at(AV(NMX_F_Z), off);
+    x.gp = nmx_at(AV(NMX_F_ZGRAD), off);
   }
   if (A.wf_update || A.finalize) {
-    x.wm = AV(NMX_F_WF_MEAN)[idx];
-    x.w2 = AV(NMX_F_WF_M2)[idx];
+    x.wm = nmx_at(AV(NMX_F_WF_MEAN), off);
+    x.w2 = nmx_at(AV(NMX_F_WF_M2), off);
   }
-  if (A.start_iter) x.ms = v.unit ? 1.0f : AV(NMX_F_MASS_SQRT)[idx];
-  if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : AV(NMX_F_INV_MASS)[idx];
+  if (A.start_iter) x.ms = v.unit ? 1.0f : nmx_at(AV(NMX_F_MASS_SQRT), off);
+  if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
   if (A.prep_leaf) {
     const int nd = A.new_dir;
-    x.rfn = (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx];
+    x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
     if (turn_around(A)) {
-      x.zfn = (nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx];
-      x.gfn = (nd ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx];
+      x.zfn = nmx_at((nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL)), off);
+      x.gfn = nmx_at((nd ? AV(NMX_F_GR) : AV(NMX_F_GL)), off);
     } else {
       x.zfn = x.ze;
       x.gfn = x.ge;
@@ -716,26 +716,26 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, size_t
 }
 
 // Returns the momentum KE partial (start_iter).
-__device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, float step_eff, int d, size_t idx,
+__device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, float step_eff, int d, uint32_t off,
                                              ApplyIn& x, float mom, float* samp, const int8_t* transform,
                                              const nmx_nuts_config& cfg) {
   const Arena& a = *v.a;
   if (A.take_leaf) {
-    AV(NMX_F_ZSUB)[idx] = x.ze;
-    AV(NMX_F_GSUB)[idx] = x.ge;
+    nmx_at(AV(NMX_F_ZSUB), off) = x.ze;
+    nmx_at(AV(NMX_F_GSUB), off) = x.ge;
     x.zs = x.ze;
     x.gs = x.ge;
   }
-  if (A.done_sub) AV(NMX_F_RSUM)[idx] = x.rst + x.rss;
+  if (A.done_sub) nmx_at(AV(NMX_F_RSUM), off) = x.rst + x.rss;
   if (A.take_biased) {
-    AV(NMX_F_Z)[idx] = x.zs;
-    AV(NMX_F_ZGRAD)[idx] = x.gs;
+    nmx_at(AV(NMX_F_Z), off) = x.zs;
+    nmx_at(AV(NMX_F_ZGRAD), off) = x.gs;
     x.zp = x.zs;
     x.gp = x.gs;
   }
   if (A.hmc_accept) {
-    AV(NMX_F_Z)[idx] = x.ze;
-    AV(NMX_F_ZGRAD)[idx] = x.ge;
+    nmx_at(AV(NMX_F_Z), off) = x.ze;
+    nmx_at(AV(NMX_F_ZGRAD), off) = x.ge;
     x.zp = x.ze;
     x.gp = x.ge;
   }
@@ -749,8 +749,8 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       const float delta_post = z - mean_new;
       x.wm = mean_new;
       x.w2 = x.w2 + delta_pre * delta_post;
-      AV(NMX_F_WF_MEAN)[idx] = x.wm;
-      AV(NMX_F_WF_M2)[idx] = x.w2;
+      nmx_at(AV(NMX_F_WF_MEAN), off) = x.wm;
+      nmx_at(AV(NMX_F_WF_M2), off) = x.w2;
     }
     if (A.finalize) {  // final_fn (:198-237)
       float cov = x.w2 / (float)(A.wfn - 1);
@@ -761,12 +761,12 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       }
       im = cov;
       x.ms = 1.0f / sqrtf(cov);
-      AV(NMX_F_INV_MASS)[idx] = cov;
-      AV(NMX_F_MASS_SQRT)[idx] = x.ms;
-      AV(NMX_F_WF_MEAN)[idx] = 0.0f;
-      AV(NMX_F_WF_M2)[idx] = 0.0f;
+      nmx_at(AV(NMX_F_INV_MASS), off) = cov;
+      nmx_at(AV(NMX_F_MASS_SQRT), off) = x.ms;
+      nmx_at(AV(NMX_F_WF_MEAN), off) = 0.0f;
+      nmx_at(AV(NMX_F_WF_M2), off) = 0.0f;
     }
-    if (samp) samp[idx] = transform_value(transform[d], z);
+    if (samp) nmx_at(samp, off) = transform_value(transform[d], z);
   }
   float ke0 = 0.0f;
   if (A.start_iter || A.prep_leaf) {
@@ -779,22 +779,22 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       const float z = x.zp;
       const float g = x.gp;
       ke0 = (im * r) * r;
-      AV(NMX_F_RSUM)[idx] = r;
+      nmx_at(AV(NMX_F_RSUM), off) = r;
       // both ends start at z; only the fixed end goes to the side arrays
-      (nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR))[idx] = z;
-      (nd ? AV(NMX_F_GL) : AV(NMX_F_GR))[idx] = g;
-      (nd ? AV(NMX_F_RL) : AV(NMX_F_RR))[idx] = r;
+      nmx_at((nd ? AV(NMX_F_ZL) : AV(NMX_F_ZR)), off) = z;
+      nmx_at((nd ? AV(NMX_F_GL) : AV(NMX_F_GR)), off) = g;
+      nmx_at((nd ? AV(NMX_F_RL) : AV(NMX_F_RR)), off) = r;
       const float rh = r - half * g;
-      (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
-      ZE[idx] = z + es * (im * rh);
+      nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
+      nmx_at(ZE, off) = z + es * (im * rh);
     } else {
       if (turn_around(A)) {
-        (A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL))[idx] = x.ze;
-        (A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL))[idx] = x.ge;
+        nmx_at((A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL)), off) = x.ze;
+        nmx_at((A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL)), off) = x.ge;
       }
       const float rh = x.rfn - half * x.gfn;
-      (nd ? AV(NMX_F_RR) : AV(NMX_F_RL))[idx] = rh;
-      ZE[idx] = x.zfn + es * (im * rh);
+      nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
+      nmx_at(ZE, off) = x.zfn + es * (im * rh);
     }
   }
   return ke0;
@@ -814,13 +814,13 @@ __device__ __forceinline__ float apply_block(const VecCtx& v, const Act& A, floa
 #pragma unroll
     for (int q = q0; q < q0 + BATCH; ++q) {
       const int d = 4 * blk + q;
-      if (d < v.D) apply_load(v, A, (size_t)d * v.ldc + c, x[q - q0]);
+      if (d < v.D) apply_load(v, A, nmx_row_off(d, v.ldc, c), x[q - q0]);
     }
 #pragma unroll
     for (int q = q0; q < q0 + BATCH; ++q) {
       const int d = 4 * blk + q;
       if (d < v.D)
-        ke0 += apply_store(v, A, step_eff, d, (size_t)d * v.ldc + c, x[q - q0], n[q], samp, transform, cfg);
+        ke0 += apply_store(v, A, step_eff, d, nmx_row_off(d, v.ldc, c), x[q - q0], n[q], samp, transform, cfg);
     }
   }
   return ke0;
@@ -847,7 +847,7 @@ __device__ __forceinline__ float apply_rows(const VecCtx& v, const Act& A, float
 #pragma unroll
     for (int q = 0; q < BATCH; ++q) {
       const int dq = d + q * step;
-      if (dq < v.D) apply_load(v, A, (size_t)dq * v.ldc + c, x[q]);
+      if (dq < v.D) apply_load(v, A, nmx_row_off(dq, v.ldc, c), x[q]);
     }
     float n[BATCH];
 #pragma unroll
@@ -864,7 +864,8 @@ __device__ __forceinline__ float apply_rows(const VecCtx& v, const Act& A, float
 #pragma unroll
     for (int q = 0; q < BATCH; ++q) {
       const int dq = d + q * step;
-      if (dq < v.D) ke0 += apply_store(v, A, step_eff, dq, (size_t)dq * v.ldc + c, x[q], n[q], samp, transform, cfg);
+      if (dq < v.D)
+        ke0 += apply_store(v, A, step_eff, dq, nmx_row_off(dq, v.ldc, c), x[q], n[q], samp, transform, cfg);
     }
   }
   return ke0;
@@ -1246,18 +1247,22 @@ __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, c
   const float* ZE = AV(NMX_F_Z_EVAL);
   float* GE = AV(NMX_F_G_EVAL);
   int d = d0;
+  const uint32_t ldc4 = (uint32_t)v.ldc << 2;
   for (; d < d1; d += step) {
-    const size_t i0 = (size_t)d * v.ldc + c;
+    const uint32_t i0 = nmx_row_off(d, v.ldc, c);
     LeafIn x0;
     leaf_load<NUTS, true, false>(v, A, i0, x0);
-    x0.g = m.row(ZE, v.ldc, c, d, gl, sums);
-    GE[i0] = x0.g;
+    x0.g = m.row(ZE, i0, ldc4, d, gl, sums);
+    nmx_at(GE, i0) = x0.g;
     leaf_store<NUTS, true>(v, A, seff, i0, x0, red);
   }
 }
 
+#ifndef NMX_LEAF_OCC
+#define NMX_LEAF_OCC 4  // waves per SIMD k_wide_leaf is compiled for (<= 128 VGPRs)
+#endif
 template <class M>
-__global__ __launch_bounds__(64 * WIDE_WAVES, 3) void k_wide_leaf(WideArgs W, M m, float* ppart) {
+__global__ __launch_bounds__(64 * WIDE_WAVES, NMX_LEAF_OCC) void k_wide_leaf(WideArgs W, M m, float* ppart) {
   constexpr int NR = NPART + M::NSUM;
   constexpr int WV = WIDE_WAVES;
   __shared__ float lds[NR * WV * 64];
@@ -1411,8 +1416,8 @@ __global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_rs(WideArgs W, M m, c
     const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
 #pragma unroll
     for (int i = 0; i < M::NSCALAR; ++i) {
-      const size_t idx = (size_t)m.scalar_row(i) * ldc + c;
-      AV(NMX_F_G_EVAL)[idx] = gs[i];
+      const uint32_t idx = nmx_row_off(m.scalar_row(i), ldc, c);
+      nmx_at(AV(NMX_F_G_EVAL), idx) = gs[i];
       LeafIn x;
       x.g = gs[i];
       if (is_nuts) {

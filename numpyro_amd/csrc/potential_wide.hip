@@ -57,7 +57,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_wide_part(M m, nmx_eval_batch ev
   const int r0 = m.lo() + blockIdx.y * SLICE, r1 = min(m.hi(), r0 + SLICE);
   if (act) {
     const typename M::Glob g = m.globals(ev.z, ldc, c);
-    for (int d = r0 + wv; d < r1; d += WAVES) ev.grad[(size_t)d * ldc + c] = m.row(ev.z, ldc, c, d, g, sums);
+    for (int d = r0 + wv; d < r1; d += WAVES) {
+      const uint32_t off = nmx_row_off(d, ldc, c);
+      nmx_at(ev.grad, off) = m.row(ev.z, off, (uint32_t)ldc << 2, d, g, sums);
+    }
   }
   wave_block_sum<NS>(sums, lds);
   if (act && wv == 0) {

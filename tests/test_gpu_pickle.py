@@ -25,9 +25,11 @@ ES = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
 
 @pytest.mark.parametrize("kernel", [HMC, NUTS])
 def test_pickle_hmc(device, kernel):
-    """test_pickle.py:86-96: samples survive a pickle round trip of the MCMC object."""
-    mcmc = MCMC(kernel(P.eight_schools), num_warmup=10, num_samples=10, num_chains=8)
-    mcmc.run(0, *ES)
+    """test_pickle.py:86-96 (normal_model, :59-60): samples survive a pickle round trip of the
+    MCMC object."""
+    args = (np.zeros(1, np.float32), np.ones(1, np.float32))
+    mcmc = MCMC(kernel(P.diag_normal), num_warmup=10, num_samples=10, num_chains=8)
+    mcmc.run(0, *args)
     m2 = pickle.loads(pickle.dumps(mcmc))
     for k, v in mcmc.get_samples().items():
         torch.testing.assert_close(m2.get_samples()[k], v, rtol=0, atol=0)
