@@ -39,10 +39,18 @@ COMMON_FLAGS = [
 ]
 
 
-# per-file flags: the covtype kernel's epilogue and residual split stay scalar VALU (the SLP
-# vectorizer would pair them into v_pk_*_f32, which issue slower beside MFMAs on gfx950;
-# potential_logreg.hip x3_epi_one)
-FILE_FLAGS = {"potential_logreg.hip": ["-fno-slp-vectorize"]}
+# per-file flags:
+# * the covtype kernel's epilogue and residual split stay scalar VALU (the SLP vectorizer would
+#   pair them into v_pk_*_f32, which issue slower beside MFMAs on gfx950; potential_logreg.hip
+#   x3_epi_one);
+# * no floating-point contraction in the step kernels and the small models' potentials: the
+#   same device function is inlined into several kernels (the launched step, the persistent
+#   schedule, the sync / async schedules), and whether the backend fuses a * b + c into an FMA
+#   depends on each kernel's code generation -- with contraction off every kernel rounds every
+#   product, so the schedules stay bitwise identical (and round like the NumPy oracle)
+FILE_FLAGS = {"potential_logreg.hip": ["-fno-slp-vectorize"],
+              "nuts.hip": ["-ffp-contract=off"],
+              "potential_small.hip": ["-ffp-contract=off"]}
 
 
 def _headers():
@@ -53,7 +61,7 @@ def _stale(obj: str, src: str, headers) -> bool:
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    return any(os.path.getmtime(p) > t for p in [src, *headers])
+    return any(os.path.getmtime(p) > t for p in [src, __file__, *headers])
 
 
 def _compile(src: str, obj: str, extra=()) -> None:

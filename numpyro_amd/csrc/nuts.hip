@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, c
 }
 
 #ifndef NMX_LEAF_OCC
-#define NMX_LEAF_OCC 4  // waves per SIMD k_wide_leaf is compiled for (<= 128 VGPRs)
+#define NMX_LEAF_OCC 3  // waves per SIMD k_wide_leaf is compiled for (4: <= 128 VGPRs, small spills, slower)
 #endif
 template <class M>
 __global__ __launch_bounds__(64 * WIDE_WAVES, NMX_LEAF_OCC) void k_wide_leaf(WideArgs W, M m, float* ppart) {

@@ -1,4 +1,5 @@
-"""Time the BNN potential alone vs the number of evaluated chains (all listed)."""
+"""Time the BNN potential alone vs the number of evaluated chains (all listed).
+usage: python scripts/bench_bnn.py [H] [C1,C2,...]"""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -7,8 +8,9 @@ from numpyro_amd.potentials import BNN
 
 X, Y = datasets.bnn_data(N=100, D_X=3)
 H = int(sys.argv[1]) if len(sys.argv) > 1 else 69
+CS = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 8, 64, 256, 1024, 2048]
 dev = torch.device("cuda:0")
-for C in (1, 8, 64, 256, 1024, 2048):
+for C in CS:
     ldc = (C + 63) // 64 * 64
     pot = BNN(X, Y, H)
     pot.bind(C, ldc, dev)
