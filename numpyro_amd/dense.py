@@ -251,6 +251,76 @@ class PooledCovariance:
 CHAIN_DENSE_MAX_D = 256
 
 
+class MassBlocks:
+    """Structured mass matrix (dense_mass=[("x", "y"), ...], hmc.py:239-252; blocks as
+    hmc_util.py:439-515 _initialize_mass_matrix builds them): one dense block per listed site
+    group, its coordinates in the group's order (the reference's z_block = tuple(z[k] for k in
+    site_names)), and one diagonal block over the remaining sites in sorted order.  Every block
+    adapts by its own Welford covariance; here the per-chain dense Welford of all coordinates is
+    masked to the blocks (its diagonal entries are the diagonal Welford's, bitwise: the same
+    product delta_pre * delta_post), and each dense block is factored in its own order, so the
+    whitening T_c is block-diagonal up to that ordering."""
+
+    def __init__(self, sites, groups):
+        import numpy as np
+
+        pos, o = {}, 0
+        for name, shape, _ in sites:
+            n = int(np.prod(shape, dtype=np.int64))
+            pos[name] = (o, n)
+            o += n
+        self.D = o
+        used, self.blocks = set(), []
+        for g in groups:
+            for n in g:
+                if n not in pos:
+                    raise ValueError(f"dense_mass names {n!r}, which is not a latent site ({sorted(pos)})")
+                if n in used:
+                    raise ValueError(f"site {n!r} appears in two dense_mass groups")
+                used.add(n)
+            self.blocks.append((tuple(g), self._idx(pos, g), True))
+        rest = tuple(sorted(set(pos) - used))
+        if rest:
+            self.blocks.append((rest, self._idx(pos, rest), False))
+
+    @staticmethod
+    def _idx(pos, names):
+        return torch.cat([torch.arange(pos[n][0], pos[n][0] + pos[n][1]) for n in names])
+
+    def mask(self, m):
+        """[C, D, D]: keep each dense block's entries and the diagonal block's diagonal."""
+        out = torch.zeros_like(m)
+        for _, idx, dense in self.blocks:
+            idx = idx.to(m.device)
+            if dense:
+                out[:, idx[:, None], idx[None, :]] = m[:, idx[:, None], idx[None, :]]
+            else:
+                out[:, idx, idx] = m[:, idx, idx]
+        return out
+
+    def factor(self, imm):
+        """T [C, D, D] with T T^T = imm for a block-structured imm: per dense block the upper
+        factor of the flipped Cholesky (hmc_util.py:224-231) in the block's order, per diagonal
+        entry the square root."""
+        T = torch.zeros_like(imm)
+        for _, idx, dense in self.blocks:
+            idx = idx.to(imm.device)
+            if dense:
+                sub = imm[:, idx[:, None], idx[None, :]]
+                T[:, idx[:, None], idx[None, :]] = torch.linalg.cholesky(sub.flip(-2, -1)).flip(-2, -1)
+            else:
+                T[:, idx, idx] = torch.sqrt(imm[:, idx, idx])
+        return T
+
+    def split(self, m):
+        """{site group: [C, n, n] (dense block, group order) or [C, n] (diagonal block)}."""
+        out = {}
+        for names, idx, dense in self.blocks:
+            idx = idx.to(m.device)
+            out[names] = m[:, idx[:, None], idx[None, :]] if dense else m[:, idx, idx]
+        return out
+
+
 def chain_dense_bytes(dim, num_chains):
     """Device bytes of per-chain dense mass state: T^T and T (f32), Welford m2 (f32), the
     float64 matrices held for HMCAdaptState / re-expression (inverse mass, T)."""
@@ -262,9 +332,10 @@ class ChainWhitening:
     every chain its own matrix as in the reference's vmapped adaptation (hmc.py:790-798).
     Holds T_c^T and T_c row-major for nmx_chain_matvec (forward / backward)."""
 
-    def __init__(self, dim: int, num_chains: int, device):
+    def __init__(self, dim: int, num_chains: int, device, blocks=None):
         self.D, self.C = int(dim), int(num_chains)
         self.device = torch.device(device)
+        self.blocks = blocks  # MassBlocks (structured mass) or None (one dense block)
         self.fwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T^T
         self.bwd = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=self.device)  # T
         self.version = 0
@@ -281,7 +352,11 @@ class ChainWhitening:
             imm = imm.expand(self.C, self.D, self.D)
         if imm.shape != (self.C, self.D, self.D):
             raise ValueError(f"inverse_mass_matrix must be [{self.C}, {self.D}, {self.D}]")
-        T = torch.linalg.cholesky(imm.flip(-2, -1)).flip(-2, -1)  # upper, T T^T = imm
+        if self.blocks is not None:
+            imm = self.blocks.mask(imm)
+            T = self.blocks.factor(imm)
+        else:
+            T = torch.linalg.cholesky(imm.flip(-2, -1)).flip(-2, -1)  # upper, T T^T = imm
         self.inverse_mass_matrix = imm.contiguous().clone()
         self.version += 1
         self.T = T
@@ -294,6 +369,8 @@ class ChainWhitening:
     def mass_matrix_sqrt(self):
         # tril_inv^-1 per chain (hmc_util.py:226-231 cov_inv_sqrt)
         eye = torch.eye(self.D, dtype=torch.float64, device=self.device).expand(self.C, self.D, self.D)
+        if self.blocks is not None:  # block-triangular up to the blocks' coordinate order
+            return torch.linalg.solve(self.T.transpose(-1, -2), eye)
         return torch.linalg.solve_triangular(self.T.transpose(-1, -2), eye, upper=False)
 
     def to_model(self, w, out, phase=None, num_chains=None, stream=0):
@@ -304,11 +381,15 @@ class ChainWhitening:
     def to_whitened(self, z):
         """w_c = T_c^-1 z_c for z [D, C]."""
         zc = z.to(torch.float64).t().unsqueeze(-1)  # [C, D, 1]
+        if self.blocks is not None:
+            return torch.linalg.solve(self.T, zc).squeeze(-1).t().to(torch.float32)
         return torch.linalg.solve_triangular(self.T, zc, upper=True).squeeze(-1).t().to(torch.float32)
 
     def grad_to_model(self, g_w):
         """g_z = T_c^-T g_w for g_w [D, C]."""
         gc = g_w.to(torch.float64).t().unsqueeze(-1)
+        if self.blocks is not None:
+            return torch.linalg.solve(self.T.transpose(-1, -2), gc).squeeze(-1).t().to(torch.float32)
         return torch.linalg.solve_triangular(self.T.transpose(-1, -2), gc, upper=False).squeeze(-1).t().to(
             torch.float32)
 
@@ -316,16 +397,17 @@ class ChainWhitening:
 class ChainWhitenedPotential(Potential):
     """U_w(w) = U(T_c w), grad_w = T_c^T grad U, per chain (nmx_chain_matvec around the model)."""
 
-    def __init__(self, base: Potential):
+    def __init__(self, base: Potential, blocks=None):
         self.base = base
         self.dim = base.dim
         self.sites = [(n, s, REAL) for n, s, _ in base.sites]
         self.whitening = None
+        self.blocks = blocks
 
     def _bind(self, C, ldc, device):
         self.base.bind(C, ldc, device)
         if self.whitening is None or self.whitening.device != device or self.whitening.C != C:
-            self.whitening = ChainWhitening(self.dim, C, device)
+            self.whitening = ChainWhitening(self.dim, C, device, self.blocks)
         self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self._batches = {}
@@ -363,12 +445,15 @@ class ChainWelford:
         check(lib().nmx_chain_welford(ptr(z), self.D, z.shape[-1], self.C, self.n, ptr(self.mean), ptr(self.m2),
                                       stream), "nmx_chain_welford")
 
-    def finalize(self, regularize=True):
-        """final_fn (hmc_util.py:198-237) per chain: cov [C, D, D] float64."""
+    def finalize(self, regularize=True, blocks=None):
+        """final_fn (hmc_util.py:198-237) per chain: cov [C, D, D] float64 (masked to the
+        blocks of a structured mass matrix: each block's own final_fn)."""
         n = self.n
         if n < 2:
             raise RuntimeError("dense adaptation needs at least 2 draws per window")
         cov = self.m2.to(torch.float64) / (n - 1)
+        if blocks is not None:
+            cov = blocks.mask(cov)
         if regularize:
             cov = (n / (n + 5.0)) * cov + 1e-3 * (5.0 / (n + 5.0)) * torch.eye(self.D, dtype=cov.dtype,
                                                                               device=cov.device)

@@ -75,6 +75,9 @@ class SamplerOptions:
     # per-chain dense mass: device bytes allowed for the matrices (dense.chain_dense_bytes)
     chain_dense_bytes: int = 64 << 30
     find_heuristic_step_size: bool = False
+    # structured mass (dense_mass=[("x", "y"), ...], hmc.py:239-252): site groups of the dense
+    # blocks; the remaining sites form one diagonal block
+    dense_blocks: list | None = None
 
 
 class Engine:
@@ -100,6 +103,12 @@ class Engine:
         # fit, one pooled matrix when asked for ("pooled"), one shared whitening when the
         # matrix is given and not adapted (every chain holds the same one: same semantics)
         self.chain_dense = self.dense and opts.dense_mass != "pooled" and bool(opts.adapt_mass_matrix)
+        self.blocks = None
+        if opts.dense_blocks:
+            from .dense import MassBlocks
+            if not self.chain_dense:
+                raise NotImplementedError("structured dense_mass needs adapt_mass_matrix=True (per-chain blocks)")
+            self.blocks = MassBlocks(potential.sites, opts.dense_blocks)
         if self.chain_dense:
             from .dense import CHAIN_DENSE_MAX_D, ChainWhitenedPotential, chain_dense_bytes
             need = chain_dense_bytes(potential.dim, num_chains)
@@ -108,7 +117,7 @@ class Engine:
                     f"per-chain dense mass matrices for {num_chains} chains of dimension {potential.dim} need "
                     f"{need / 2**30:.1f} GiB (limit {opts.chain_dense_bytes / 2**30:.0f} GiB, dim <= "
                     f"{CHAIN_DENSE_MAX_D}); use dense_mass='pooled' for one matrix adapted over all chains")
-            potential = ChainWhitenedPotential(potential)
+            potential = ChainWhitenedPotential(potential, self.blocks)
         elif self.dense:
             from .dense import WhitenedPotential
             potential = WhitenedPotential(potential)
@@ -462,7 +471,7 @@ class Engine:
                 del abuf, afld
             if b == win[1]:
                 if self.chain_dense:
-                    cov, mean = pool.finalize(self.opts.regularize_mass_matrix), None
+                    cov, mean = pool.finalize(self.opts.regularize_mass_matrix, self.blocks), None
                 else:
                     pool.all_reduce()
                     cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
@@ -590,9 +599,11 @@ class Engine:
             wt = self.potential.whitening
             key = (id(wt), wt.version)
             if self._mass_cache is None or self._mass_cache[0] != key:
-                self._mass_cache = (key, (wt.inverse_mass_matrix.to(torch.float32),
-                                          wt.mass_matrix_sqrt().to(torch.float32),
-                                          wt.mass_matrix_sqrt_inv().to(torch.float32).clone()))
+                mats = (wt.inverse_mass_matrix.to(torch.float32), wt.mass_matrix_sqrt().to(torch.float32),
+                        wt.mass_matrix_sqrt_inv().to(torch.float32).clone())
+                if self.blocks is not None:  # {site group: block} dicts, as HMCAdaptState holds them
+                    mats = tuple(self.blocks.split(m) for m in mats)
+                self._mass_cache = (key, mats)
             return self._mass_cache[1]
         ms = self.chain_state("mass_sqrt").clone()
         return self.chain_state("inv_mass").clone(), ms, 1.0 / ms

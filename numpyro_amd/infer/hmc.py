@@ -181,9 +181,15 @@ class HMC(MCMCKernel):
                 raise ValueError("dense_mass must be a bool, 'pooled' or a list of site groups")
             warnings.warn("dense_mass='pooled': one dense mass matrix is adapted from the draws of all chains "
                           "(not per chain as in numpyro); chains share it", stacklevel=2)
-        if isinstance(dense_mass, (list, tuple)) and len(dense_mass) > 0:
-            raise NotImplementedError("structured dense_mass (list of site groups) is not supported; "
-                                      "use dense_mass=True for a full dense mass matrix")
+        if isinstance(dense_mass, (list, tuple)):
+            # structured mass (hmc.py:239-252): dense blocks over the listed site groups, one
+            # diagonal block over the remaining sites; adapted per chain (dense.MassBlocks)
+            dense_mass = [tuple(g) for g in dense_mass]
+            if not all(len(g) > 0 and all(isinstance(n, str) for n in g) for g in dense_mass):
+                raise ValueError("dense_mass as a list holds tuples of site names, e.g. [('x', 'y')]")
+            if isinstance(inverse_mass_matrix, dict):
+                raise NotImplementedError("an inverse_mass_matrix dict of blocks: the blocks are adapted from "
+                                          "identity here; pass adapt_mass_matrix=True without inverse_mass_matrix")
         if model is not None and not (isinstance(model, FusedModel) or callable(model)):
             raise TypeError("`model` must be a model function (numpyro_amd.sample / plate / distributions, "
                             "mapped onto a fused kernel by numpyro_amd.frontend) or a fused model")
@@ -229,6 +235,7 @@ class HMC(MCMCKernel):
             algo=self._algo, step_size=self._step_size, adapt_step_size=self._adapt_step_size,
             adapt_mass_matrix=self._adapt_mass_matrix,
             dense_mass=self._dense_mass if self._dense_mass == "pooled" else bool(self._dense_mass),
+            dense_blocks=list(self._dense_mass) if isinstance(self._dense_mass, list) and self._dense_mass else None,
             target_accept_prob=self._target_accept_prob, max_tree_depth=md,
             trajectory_length=self._trajectory_length, num_steps=self._num_steps,
             regularize_mass_matrix=self._regularize_mass_matrix,

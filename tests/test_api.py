@@ -27,8 +27,8 @@ def test_kernel_argument_validation():
         NUTS(lambda: None).potential()  # no sample sites: no fused kernel for this structure
     with pytest.raises(TypeError):
         NUTS(potential_fn=lambda z: z)
-    with pytest.raises(NotImplementedError):
-        NUTS(P.eight_schools, dense_mass=[("mu", "tau")])
+    with pytest.raises(ValueError):
+        NUTS(P.eight_schools, dense_mass=[("mu", 3)])  # groups of site names (hmc.py:239-252)
     with pytest.raises(NotImplementedError):
         NUTS(P.eight_schools, kinetic_fn=lambda m, r: 0.0)
     with pytest.warns(UserWarning):
@@ -174,3 +174,38 @@ def test_pickling_kernels_models_and_states():
     assert type(st2) is HMCState and st2._engine is None and st2._layout == st._layout
     torch.testing.assert_close(st2._arena, st._arena)
     assert st2.adapt_state.rng_key == 7 and st2._whitening[1] is None
+
+
+def test_mass_blocks_structure():
+    """dense_mass=[("theta", "mu")] on eight schools (sites mu, tau, theta[8]): a dense block over
+    theta then mu in the group's order (z_block = tuple(z[k] for k in site_names),
+    hmc_util.py:448-456) and a diagonal block over the remaining ("tau",) (:469-477)."""
+    import torch
+
+    from numpyro_amd.dense import MassBlocks
+
+    pot = P.eight_schools.potential(8, np.ones(8), np.zeros(8))
+    mb = MassBlocks(pot.sites, [("theta", "mu")])
+    (g0, i0, d0), (g1, i1, d1) = mb.blocks
+    assert g0 == ("theta", "mu") and d0 and i0.tolist() == list(range(2, 10)) + [0]
+    assert g1 == ("tau",) and not d1 and i1.tolist() == [1]
+    rs = np.random.RandomState(0)
+    A = rs.randn(2, 10, 10)
+    cov = torch.tensor(A @ A.transpose(0, 2, 1) + 10 * np.eye(10))
+    m = mb.mask(cov)
+    assert float(m[:, 1, 0].abs().max()) == 0 and float(m[:, 1, 1].min()) > 0 and float(m[:, 0, 2].abs().min()) > 0
+    T = mb.factor(m)
+    torch.testing.assert_close(T @ T.transpose(-1, -2), m)
+    blk = mb.split(m)
+    assert blk[("theta", "mu")].shape == (2, 9, 9) and blk[("tau",)].shape == (2, 1)
+    # the dense block factor is the reference's flipped Cholesky in the block's own order
+    sub = blk[("theta", "mu")].numpy()[0]
+    Tb = np.linalg.cholesky(sub[::-1, ::-1])[::-1, ::-1]
+    np.testing.assert_allclose(T.numpy()[0][np.ix_(i0.numpy(), i0.numpy())], Tb, rtol=1e-10)
+    with pytest.raises(ValueError):
+        MassBlocks(pot.sites, [("theta",), ("theta", "mu")])
+    with pytest.raises(ValueError):
+        MassBlocks(pot.sites, [("beta",)])
+    assert NUTS(P.eight_schools, dense_mass=[]).options().dense_mass is False
+    o = NUTS(P.eight_schools, dense_mass=[("theta", "mu")]).options()
+    assert o.dense_mass is True and o.dense_blocks == [("theta", "mu")]

@@ -540,3 +540,91 @@ def test_per_chain_dense_adaptation_matches_oracle(device, model):
     print(f"[per-chain dense {model}] {match}/{C} chains reproduce the oracle's dense-mass transitions")
     _explain_mismatches(mism, f"per-chain dense {model}")
     assert match >= int(0.95 * C)
+
+
+def test_structured_dense_mass_matches_oracle(device):
+    """Structured mass (dense_mass=[("theta", "mu")], hmc.py:239-252) on eight schools: a dense
+    block over (theta, mu) in that order and a diagonal block over tau, adapted per chain over
+    W = 150 (middle window [75-99]).  (1) teacher-forced: the oracle's Welford + final_fn of
+    each block (hmc_util.py:439-515 builds the blocks, :133-239 adapts them) over the chain's
+    device draws reproduces the chain's adapted blocks; the state holds them as a dict keyed by
+    site group.  (2) from each chain's post-warmup state the oracle's dense-mass NUTS with the
+    block matrices scattered into full ones (M^-1 and mass_matrix_sqrt block by block, so the
+    momentum and kinetic energy are the reference's per-block ones) takes the device's next three
+    trees and draws for >= 90% of chains, every mismatch at a rounding-level tie."""
+    from numpyro_amd import datasets
+    from test_gpu_nuts import _explain_mismatches, _first_split
+
+    seed, C, W, D = 23, 64, 150, 10
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    groups = [("theta", "mu")]
+    # postprocess_fn = identity: the draws stay unconstrained (tau on the log scale)
+    mcmc = MCMC(NUTS(P.eight_schools, dense_mass=groups), num_warmup=W, num_samples=3, num_chains=C,
+                postprocess_fn=lambda z: z)
+    mcmc.warmup(seed, *args, collect_warmup=True)
+    eng = mcmc._engine
+    assert eng.chain_dense and eng.blocks is not None
+    ws = mcmc.get_samples(group_by_chain=True)
+    flat = lambda d: np.concatenate([d["mu"].cpu().numpy()[..., None], d["tau"].cpu().numpy()[..., None],  # noqa
+                                     d["theta"].cpu().numpy()], axis=-1)
+    draws = flat(ws).astype(np.float32)  # ravel order (mu, log tau, theta)
+    st = mcmc.post_warmup_state
+    imm = st.adapt_state.inverse_mass_matrix
+    assert set(imm) == {("theta", "mu"), ("tau",)}
+    dense_b = imm[("theta", "mu")].cpu().numpy().astype(np.float64)
+    diag_b = imm[("tau",)].cpu().numpy().astype(np.float64)
+    assert dense_b.shape == (C, 9, 9) and diag_b.shape == (C, 1)
+    order = list(range(2, 10)) + [0]  # (theta, mu) in ravel coordinates
+    _, upd_d, fin_d = H.welford_covariance(diagonal=False)
+    _, upd_g, fin_g = H.welford_covariance(diagonal=True)
+    for c in range(C):
+        sd = (np.zeros(9, np.float32), np.zeros((9, 9), np.float32), 0)
+        sg = (np.zeros(1, np.float32), np.zeros(1, np.float32), 0)
+        for t in range(75, 100):
+            sd = upd_d(draws[c, t, order], sd)
+            sg = upd_g(draws[c, t, [1]], sg)
+        np.testing.assert_allclose(dense_b[c], fin_d(sd, regularize=True)[0], rtol=1e-4, atol=1e-7,
+                                   err_msg=f"chain {c} dense block")
+        np.testing.assert_allclose(diag_b[c], fin_g(sg, regularize=True)[0], rtol=1e-5, err_msg=f"chain {c} tau")
+    # (2) sampling transitions from the post-warmup state
+    mcmc.run(seed, *args, extra_fields=("num_steps",))
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
+    zs = flat(mcmc.get_samples(True))
+    z0 = torch.cat([st.z["mu"][:, None], st.z["tau"][:, None], st.z["theta"]], 1).cpu().numpy()
+    g0, pe0 = st.z_grad.cpu().numpy(), st.potential_energy.cpu().numpy()
+    ss = st.adapt_state.step_size.cpu().numpy()
+    ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    match, mism = 0, []
+    for c in range(C):
+        imm_f = np.zeros((D, D), np.float32)
+        msq_f = np.zeros((D, D), np.float32)
+        i_b, sq_b, _ = H._initialize_mass_matrix(9, dense_b[c].astype(np.float32), True)
+        imm_f[np.ix_(order, order)] = i_b
+        msq_f[np.ix_(order, order)] = sq_b
+        i_t, sq_t, _ = H._initialize_mass_matrix(1, diag_b[c].astype(np.float32), False)
+        imm_f[1, 1], msq_f[1, 1] = i_t[0], sq_t[0]
+        o = H.NUTSOracle(pe_grad, D, W, step_size=float(ss[c]), adapt_step_size=False, adapt_mass_matrix=False,
+                         dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32))
+        wa = o.wa_init((z0[c],), None, np.float32(ss[c]), inverse_mass_matrix=np.eye(D, dtype=np.float32),
+                       mass_matrix_size=D)._replace(inverse_mass_matrix=imm_f, mass_matrix_sqrt=msq_f)
+        s = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
+                       0, np.float32(0), np.float32(0), False, wa, (seed, c))
+        ok, margins = [], []
+        for t in range(3):
+            H.DECISIONS = []
+            try:
+                s = o.sample(s)
+            finally:
+                d, H.DECISIONS = H.DECISIONS, None
+            margins.append(H.closest_decision(d))
+            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
+        t = _first_split(ok)
+        if t < 0:
+            match += 1
+        else:
+            mism.append((c, t, margins[t]))
+    print(f"[structured dense eight schools] {match}/{C} chains reproduce the oracle's block-mass transitions")
+    _explain_mismatches(mism, "structured dense eight schools")
+    assert match >= int(0.9 * C)
