@@ -49,16 +49,30 @@ struct NmxWideSV {
     return g;
   }
   // dU/ds_t of row d = 1 + t (GaussianRandomWalk stencil + StudentT(nu, 0, e^s) term)
-  // (off: nmx_row_off(d, ldc, c); ldc4 = 4 ldc, the byte stride between rows)
+  // (off: nmx_row_off(d, ldc, c); ldc4 = 4 ldc, the byte stride between rows).  row_load /
+  // row_eval split row() into its loads and its arithmetic (the pipelined leaf, nuts.hip).
+  struct RowIn {
+    float s, sp, sn, r;
+  };
+  __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t ldc4, int d, RowIn& x) const {
+    const int t = d - 1;
+    x.s = nmx_at(z, off);
+    x.sp = t > 0 ? nmx_at(z, off - ldc4) : 0.0f;
+    x.sn = t + 1 < T ? nmx_at(z, off + ldc4) : 0.0f;
+    x.r = ret[t];
+  }
   __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
                                        float* sums) const {
+    RowIn x;
+    row_load(z, off, ldc4, d, x);
+    return row_eval(x, d, g, sums);
+  }
+  __device__ __forceinline__ float row_eval(const RowIn& x, int d, const Glob& g, float* sums) const {
     const int t = d - 1;
-    const float s = nmx_at(z, off);
-    const float sp = t > 0 ? nmx_at(z, off - ldc4) : 0.0f;
-    const float sn = t + 1 < T ? nmx_at(z, off + ldc4) : 0.0f;
+    const float s = x.s, sp = x.sp, sn = x.sn;
     const float dd = s - sp;
     const float dn = t + 1 < T ? sn - s : 0.0f;
-    const float r = ret[t];
+    const float r = x.r;
     const float q = r * r * expf(-2.0f * s) * g.inv_nu;
     const float qq = q / (1.0f + q);
     sums[0] += dd * dd;
@@ -108,10 +122,21 @@ struct NmxWideFunnel {
     g.e = expf(-g.y);
     return g;
   }
-  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t, int, const Glob& g, float* sums) const {
-    const float x = nmx_at(z, off);
-    sums[0] += x * x;
-    return x * g.e;
+  struct RowIn {
+    float x;
+  };
+  __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
+    in.x = nmx_at(z, off);
+  }
+  __device__ __forceinline__ float row_eval(const RowIn& in, int, const Glob& g, float* sums) const {
+    sums[0] += in.x * in.x;
+    return in.x * g.e;
+  }
+  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
+                                       float* sums) const {
+    RowIn in;
+    row_load(z, off, ldc4, d, in);
+    return row_eval(in, d, g, sums);
   }
   __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
     const float K = (float)(dim - 1);
@@ -138,10 +163,21 @@ struct NmxWideFunnelNC {
     g.y = z[(size_t)(dim - 1) * ldc + c];
     return g;
   }
-  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t, int, const Glob&, float* sums) const {
-    const float x = nmx_at(z, off);
-    sums[0] += x * x;
-    return x;
+  struct RowIn {
+    float x;
+  };
+  __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
+    in.x = nmx_at(z, off);
+  }
+  __device__ __forceinline__ float row_eval(const RowIn& in, int, const Glob&, float* sums) const {
+    sums[0] += in.x * in.x;
+    return in.x;
+  }
+  __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
+                                       float* sums) const {
+    RowIn in;
+    row_load(z, off, ldc4, d, in);
+    return row_eval(in, d, g, sums);
   }
   __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
     gs[0] = g.y / 9.0f;

@@ -639,6 +639,25 @@ template <bool NUTS, int ROWS, bool PRE1 = (ROWS == 2)>
 __device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float seff, int d0, int d1, int step, int c,
                                           float* red) {
   int d = d0;
+  if constexpr (ROWS == 3) {
+    // software-pipelined: the next row's loads are issued before this row's stores, so two
+    // rows' loads are in flight through the whole loop (one row per round leaves the memory
+    // pipe idle while a row computes and stores)
+    if (d >= d1) return;
+    LeafIn cur;
+    uint32_t ic = nmx_row_off(d, v.ldc, c);
+    leaf_load<NUTS, true>(v, A, ic, cur);
+    for (; d < d1; d += step) {
+      const int dn = d + step;
+      const uint32_t in = nmx_row_off(dn, v.ldc, c);
+      LeafIn nxt;
+      if (dn < d1) leaf_load<NUTS, true>(v, A, in, nxt);
+      leaf_store<NUTS, true>(v, A, seff, ic, cur, red);
+      cur = nxt;
+      ic = in;
+    }
+    return;
+  }
   if constexpr (ROWS == 2) {
     for (; d + step < d1; d += 2 * step) {
       LeafIn x0, x1;
@@ -1049,8 +1068,11 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   if (A.leaf) {
     // one row per round with the row's checkpoints loaded ahead: 114 VGPRs, 4 waves per SIMD
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
-    if (is_nuts) leaf_rows<true, 1, true>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
-    else leaf_rows<false, 1, true>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
+#ifndef NMX_V1_ROWS
+#define NMX_V1_ROWS 1
+#endif
+    if (is_nuts) leaf_rows<true, NMX_V1_ROWS, true>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
+    else leaf_rows<false, NMX_V1_ROWS, true>(v, A, seff, d0 + wv, d1, WIDE_WAVES, c, red);
   }
   block_sum<WIDE_WAVES, NPART>(red, lds);
   if (wv == 0 && A.leaf) {
@@ -1248,6 +1270,36 @@ __device__ __forceinline__ void leaf_rows_model(const VecCtx& v, const Act& A, c
   float* GE = AV(NMX_F_G_EVAL);
   int d = d0;
   const uint32_t ldc4 = (uint32_t)v.ldc << 2;
+#ifndef NMX_LEAF_PIPE
+#define NMX_LEAF_PIPE 0
+#endif
+  if constexpr (NMX_LEAF_PIPE) {
+    // software-pipelined as leaf_rows<ROWS = 3>: the next row's leaf state and model inputs
+    // are loaded before this row's model arithmetic and stores
+    if (d >= d1) return;
+    LeafIn cur;
+    typename M::RowIn mc;
+    uint32_t ic = nmx_row_off(d, v.ldc, c);
+    leaf_load<NUTS, true, false>(v, A, ic, cur);
+    m.row_load(ZE, ic, ldc4, d, mc);
+    for (; d < d1; d += step) {
+      const int dn = d + step;
+      const uint32_t in = nmx_row_off(dn, v.ldc, c);
+      LeafIn nxt;
+      typename M::RowIn mn;
+      if (dn < d1) {
+        leaf_load<NUTS, true, false>(v, A, in, nxt);
+        m.row_load(ZE, in, ldc4, dn, mn);
+      }
+      cur.g = m.row_eval(mc, d, gl, sums);
+      nmx_at(GE, ic) = cur.g;
+      leaf_store<NUTS, true>(v, A, seff, ic, cur, red);
+      cur = nxt;
+      mc = mn;
+      ic = in;
+    }
+    return;
+  }
   for (; d < d1; d += step) {
     const uint32_t i0 = nmx_row_off(d, v.ldc, c);
     LeafIn x0;
