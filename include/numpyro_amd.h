@@ -10,7 +10,10 @@
  *  - extern "C", plain pointers and sizes; no torch types.  All pointers are device
  *    pointers unless named host_*.  `stream` is a hipStream_t passed as void*.
  *  - Chain-major SoA: a per-chain vector field is stored [D][ldc] (ldc >= C, ldc % 64 == 0),
- *    so lanes of a wave read consecutive chains.  Per-chain scalars are [ldc].
+ *    so lanes of a wave read consecutive chains.  Per-chain scalars are [ldc].  The arena of
+ *    the persistent wide schedule (nmx_nuts_run_wide) instead stores vector fields in chain
+ *    rows [ldc][D] (cfg->layout = NMX_LAYOUT_CHAIN_ROWS): one workgroup per chain reads the
+ *    chain's contiguous row.  Buffers passed in and out (init z, samples) are [D][ldc] always.
  *  - The library never allocates on the hot path: callers allocate the arena / workspace
  *    whose size the *_bytes() queries return.
  *  - Return value: NMX_OK or an error code; nmx_last_error() has the message.  Numerical
@@ -60,7 +63,9 @@ enum nmx_phase {
 };
 /* Potential kernels evaluate chains whose phase >= NMX_PH_LEAF. */
 
-/* Arena fields (SoA). Vector fields are [D][ldc] float; ckpt fields [max_depth][D][ldc]. */
+/* Arena fields (SoA). Vector fields are [D][ldc] float; ckpt fields [max_depth][D][ldc]
+ * ([ldc][D] and [max_depth][ldc][D] in the NMX_LAYOUT_CHAIN_ROWS layout; same sizes). */
+enum nmx_layout { NMX_LAYOUT_CHAIN_MINOR = 0, NMX_LAYOUT_CHAIN_ROWS = 1 };
 enum nmx_field {
   /* per-chain int32 scalars */
   NMX_F_PHASE = 0, NMX_F_ITER, NMX_F_DEPTH, NMX_F_SUB_N, NMX_F_DIR, NMX_F_TREE_N,
@@ -135,6 +140,9 @@ typedef struct nmx_nuts_config {
   int32_t ldc;                   /* round_up(C, 64) */
   int32_t parity;                /* launch parity: nmx_nuts_step appends LEAF chains to
                                     active list [parity] (and clears [parity ^ 1]) */
+  int32_t layout;                /* nmx_layout of the arena's vector fields: CHAIN_MINOR for
+                                    every entry point but nmx_nuts_run_wide, which needs
+                                    CHAIN_ROWS (reset / init / resume take either) */
 } nmx_nuts_config;
 
 /* D-slices of the wide step (0 when dim is small enough for the fused one-kernel step).
@@ -206,6 +214,21 @@ size_t nmx_nuts_wide_model_workspace_bytes(int dim, int num_chains);
 int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
                              const int8_t* transform, int model, const float* data, int n, void* workspace,
                              void* stream);
+
+/* Persistent per-chain schedule for the D-split models: ONE launch
+ * runs every remaining transition of [iter_begin, iter_end) of every chain (or max_steps
+ * leaves per chain; relaunch until counters[0] == num_chains), one workgroup per chain: the
+ * model's row gradients fused with the leapfrog end, a block reduction, the potential's
+ * finish and the tree / transition / adaptation logic, then the proposal / momentum / next
+ * position rows -- the whole of `potential(z_eval) -> nmx_nuts_step` per leaf without a host
+ * loop, D-slices or chain groups (a chain never waits for another).  Models and data as
+ * nmx_nuts_step_wide_model.  Needs cfg->layout = NMX_LAYOUT_CHAIN_ROWS (the arena written by
+ * nmx_nuts_reset / init_* with that layout) and cfg->sync_chains = 0 (the lockstep schedule
+ * is one launch per transition: iter_end = iter_begin + 1).  Sums are in an order fixed by
+ * dim, so draws do not depend on the number of chains or devices; they differ from the
+ * launched wide schedule in rounding.  samples [collection_size][D][ldc] as nmx_nuts_step. */
+int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                      const int8_t* transform, int model, const float* data, int n, int max_steps, void* stream);
 
 /* Persistent schedule for one-wave models (dim < 16): ONE launch runs
  * every remaining transition of [iter_begin, iter_end) of every chain -- each thread owns a

@@ -48,8 +48,19 @@ struct NmxWideSV {
     g.inv_nu = 1.0f / g.nu;
     return g;
   }
+  // the same from any layout: row r of the chain at byte offset off0 + r * stride4
+  __device__ __forceinline__ Glob globals_at(const float* z, uint32_t off0, uint32_t stride4) const {
+    Glob g;
+    g.a = nmx_at(z, off0);
+    g.b = nmx_at(z, off0 + (uint32_t)(T + 1) * stride4);
+    g.nu = expf(g.a);
+    g.inv_sig2 = expf(-2.0f * g.b);
+    g.inv_nu = 1.0f / g.nu;
+    return g;
+  }
   // dU/ds_t of row d = 1 + t (GaussianRandomWalk stencil + StudentT(nu, 0, e^s) term)
-  // (off: nmx_row_off(d, ldc, c); ldc4 = 4 ldc, the byte stride between rows).  row_load /
+  // (off: byte offset of the row; ldc4: the byte stride between rows -- 4 ldc in the
+  // chain-minor layout, 4 in the chain-row layout of the persistent wide kernel).  row_load /
   // row_eval split row() into its loads and its arithmetic (the pipelined leaf, nuts.hip).
   struct RowIn {
     float s, sp, sn, r;
@@ -122,6 +133,12 @@ struct NmxWideFunnel {
     g.e = expf(-g.y);
     return g;
   }
+  __device__ __forceinline__ Glob globals_at(const float* z, uint32_t off0, uint32_t stride4) const {
+    Glob g;
+    g.y = nmx_at(z, off0 + (uint32_t)(dim - 1) * stride4);
+    g.e = expf(-g.y);
+    return g;
+  }
   struct RowIn {
     float x;
   };
@@ -161,6 +178,11 @@ struct NmxWideFunnelNC {
   __device__ __forceinline__ Glob globals(const float* z, int ldc, int c) const {
     Glob g;
     g.y = z[(size_t)(dim - 1) * ldc + c];
+    return g;
+  }
+  __device__ __forceinline__ Glob globals_at(const float* z, uint32_t off0, uint32_t stride4) const {
+    Glob g;
+    g.y = nmx_at(z, off0 + (uint32_t)(dim - 1) * stride4);
     return g;
   }
   struct RowIn {

@@ -16,6 +16,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "nmx_api_internal.h"
 #include <stdlib.h>
 
@@ -65,11 +67,14 @@ size_t field_offset(int field, int ldc, int D, int MD, int iter_cap) {
   return off;
 }
 
-// Device view of the arena.
+// Device view of the arena.  The per-chain scalar fields are consecutive arrays of ldc
+// entries and the vector fields consecutive arrays of D * ldc (field_offset), so a field is
+// its group's base + index * stride: two pointers and two strides instead of a pointer per
+// field (a persistent kernel's loop would otherwise hold ~60 loop-invariant pointers).
 struct Arena {
-  int32_t* is[NUM_INT_SCALARS];
-  float* fs[NUM_FLOAT_SCALARS];
-  float* v[NUM_VECTORS];
+  char* sbase;       // field NMX_F_PHASE; scalar field f at sbase + (f - NMX_F_PHASE) * sstride
+  char* vbase;       // field NMX_F_Z; vector field f at vbase + (f - NMX_F_Z) * vstride
+  size_t sstride, vstride;
   float* ckr;
   float* ckrs;
   int32_t* active_idx;
@@ -80,19 +85,22 @@ struct Arena {
   float* tot;
 };
 
-#define AI(f) a.is[(f) - NMX_F_PHASE]
-#define AF(f) a.fs[(f) - NMX_F_STEP_SIZE]
-#define AV(f) a.v[(f) - NMX_F_Z]
+#define AI(f) reinterpret_cast<int32_t*>(a.sbase + (size_t)((f) - NMX_F_PHASE) * a.sstride)
+#define AF(f) reinterpret_cast<float*>(a.sbase + (size_t)((f) - NMX_F_PHASE) * a.sstride)
+#define AV(f) reinterpret_cast<float*>(a.vbase + (size_t)((f) - NMX_F_Z) * a.vstride)
+
+// the strided form above is exact: every scalar field spans ldc * 4 bytes and every vector
+// field D * ldc * 4, both multiples of ALIGN (ldc % 64 == 0), laid out in enum order
+static_assert(NMX_F_PHASE == 0 && NMX_F_STEP_SIZE == NMX_F_ACT_WFN + 1 && NMX_F_Z == NMX_F_PE_EVAL + 1,
+              "scalar fields must precede the vector fields contiguously");
 
 Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
   Arena a;
   char* b = (char*)base;
-  for (int f = NMX_F_PHASE; f <= NMX_F_ACT_WFN; ++f)
-    a.is[f - NMX_F_PHASE] = (int32_t*)(b + field_offset(f, ldc, D, MD, iter_cap));
-  for (int f = NMX_F_STEP_SIZE; f <= NMX_F_PE_EVAL; ++f)
-    a.fs[f - NMX_F_STEP_SIZE] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
-  for (int f = NMX_F_Z; f <= NMX_F_G_EVAL; ++f)
-    a.v[f - NMX_F_Z] = (float*)(b + field_offset(f, ldc, D, MD, iter_cap));
+  a.sbase = b + field_offset(NMX_F_PHASE, ldc, D, MD, iter_cap);
+  a.vbase = b + field_offset(NMX_F_Z, ldc, D, MD, iter_cap);
+  a.sstride = (size_t)ldc * 4;
+  a.vstride = (size_t)D * ldc * 4;
   a.ckr = (float*)(b + field_offset(NMX_F_CKPT_R, ldc, D, MD, iter_cap));
   a.ckrs = (float*)(b + field_offset(NMX_F_CKPT_RSUM, ldc, D, MD, iter_cap));
   a.active_idx = (int32_t*)(b + field_offset(NMX_F_ACTIVE_IDX, ldc, D, MD, iter_cap));
@@ -274,6 +282,25 @@ __device__ __forceinline__ int pack_act(const Act& A) {
          (A.dirR ? ACT_DIRR : 0) | (A.new_dir ? ACT_NEWDIR : 0) | (A.start_iter ? ACT_KE0_PENDING : 0);
 }
 
+// The step's decisions known before the leaf: from the chain's phase ph and its scalars.
+__device__ __forceinline__ void begin_act(const nmx_nuts_config& cfg, const ChainScalars& S, int ph, Act& A) {
+  A = Act{};
+  A.leaf = ph == NMX_PH_LEAF;
+  A.start_iter = ph == NMX_PH_START;
+  A.dirR = A.leaf ? S.dir : 0;
+  A.new_dir = A.dirR;
+  A.slot = -1;
+  A.imin = 1;
+  A.imax = 0;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  A.k = (A.leaf && is_nuts) ? S.sub_n : 0;
+  A.j = (A.leaf && is_nuts) ? S.depth : 0;
+  if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);  // :1036
+  A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
+  // the checkpoint rows a leaf touches exist: imax <= depth < max_depth_alloc
+  NMX_DCHECK(!(A.leaf && is_nuts) || (A.imax < cfg.max_depth_alloc && A.j < cfg.max_depth_alloc));
+}
+
 // Resolve WAIT (sync_chains) and set up the step's inputs.
 __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid,
                                           ChainScalars& S, Act& A) {
@@ -287,22 +314,8 @@ __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Aren
                         : cfg.num_chains;
     if (fin >= cfg.num_chains) ph = NMX_PH_START;
   }
-  A = Act{};
-  A.leaf = ph == NMX_PH_LEAF;
-  A.start_iter = ph == NMX_PH_START;
-  A.dirR = A.leaf ? S.dir : 0;
-  A.new_dir = A.dirR;
+  begin_act(cfg, S, ph, A);
   A.pe_eval = A.leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
-  A.slot = -1;
-  A.imin = 1;
-  A.imax = 0;
-  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
-  A.k = (A.leaf && is_nuts) ? S.sub_n : 0;
-  A.j = (A.leaf && is_nuts) ? S.depth : 0;
-  if (A.leaf && is_nuts) nmx_leaf_idx_to_ckpt_idxs(A.k, A.imin, A.imax);  // :1036
-  A.tree_chk = A.leaf && is_nuts && (A.k + 1 == (1 << A.j));
-  // the checkpoint rows a leaf touches exist: imax <= depth < max_depth_alloc
-  NMX_DCHECK(!(A.leaf && is_nuts) || (A.imax < cfg.max_depth_alloc && A.j < cfg.max_depth_alloc));
   return ph;
 }
 
@@ -593,20 +606,22 @@ __device__ __forceinline__ void leaf_load(const VecCtx& v, const Act& A, uint32_
 
 template <bool NUTS, bool PRE>
 __device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float seff, uint32_t off, const LeafIn& x,
-                                           float* red) {
+                                           float* red, bool st = true) {
+  // st = false: the sums only (the persistent wide kernel's scalar-site rows: every thread
+  // adds them to its totals, one thread stores)
   const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
   const float r = x.rf - half * x.g;
-  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
+  if (st) nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
   // the moving end's z / grad stay in Z_EVAL / G_EVAL (the frontier); apply_store saves
   // them into the side arrays only when the next doubling turns around
   const float im = x.im;
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
     const float rs = (A.k == 0) ? r : x.rs_old + r;
-    nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
-    if ((A.k & 1) == 0) {  // checkpoint update (:1040-1047)
+    if (st) nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
+    if (st && (A.k & 1) == 0) {  // checkpoint update (:1040-1047)
       nmx_at(a.ckr + A.imax * v.ck_stride, off) = r;
       nmx_at(a.ckrs + A.imax * v.ck_stride, off) = rs;
     }
@@ -735,9 +750,10 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32
 }
 
 // Returns the momentum KE partial (start_iter).
+// soff: offset of the row in the samples buffer ([S][D][ldc]; default: off, the arena's layout)
 __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, float step_eff, int d, uint32_t off,
                                              ApplyIn& x, float mom, float* samp, const int8_t* transform,
-                                             const nmx_nuts_config& cfg) {
+                                             const nmx_nuts_config& cfg, uint32_t soff = 0xFFFFFFFFu) {
   const Arena& a = *v.a;
   if (A.take_leaf) {
     nmx_at(AV(NMX_F_ZSUB), off) = x.ze;
@@ -785,7 +801,7 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       nmx_at(AV(NMX_F_WF_MEAN), off) = 0.0f;
       nmx_at(AV(NMX_F_WF_M2), off) = 0.0f;
     }
-    if (samp) nmx_at(samp, off) = transform_value(transform[d], z);
+    if (samp) nmx_at(samp, soff == 0xFFFFFFFFu ? off : soff) = transform_value(transform[d], z);
   }
   float ke0 = 0.0f;
   if (A.start_iter || A.prep_leaf) {
@@ -994,11 +1010,12 @@ __global__ __launch_bounds__(64) void k_nuts_persistent(StepArgs P, Pot pot, int
   const int c = blockIdx.x * SMALL_CPW + (threadIdx.x & 63) % SMALL_CPW;
   const bool evaluator = (threadIdx.x & 63) < SMALL_CPW;  // one lane per chain runs the potential
   const bool valid = c < P.cfg.num_chains;
-  const int* const phase = P.a.is[NMX_F_PHASE - NMX_F_PHASE];
+  const Arena& a = P.a;
+  const int* const phase = AI(NMX_F_PHASE);
   nmx_eval_batch ev;
-  ev.z = P.a.v[NMX_F_Z_EVAL - NMX_F_Z];
-  ev.grad = P.a.v[NMX_F_G_EVAL - NMX_F_Z];
-  ev.pe = P.a.fs[NMX_F_PE_EVAL - NMX_F_STEP_SIZE];
+  ev.z = AV(NMX_F_Z_EVAL);
+  ev.grad = AV(NMX_F_G_EVAL);
+  ev.pe = AF(NMX_F_PE_EVAL);
   ev.phase = nullptr;
   ev.active_idx = nullptr;
   ev.active_count = nullptr;
@@ -1068,6 +1085,12 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
   if (A.leaf) {
     // one row per round with the row's checkpoints loaded ahead: 114 VGPRs, 4 waves per SIMD
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
+#ifndef NMX_PX_B
+#define NMX_PX_B 2
+#endif
+#ifndef NMX_PX_CUT
+#define NMX_PX_CUT 0
+#endif
 #ifndef NMX_V1_ROWS
 #define NMX_V1_ROWS 1
 #endif
@@ -1494,22 +1517,282 @@ __global__ __launch_bounds__(64 * WIDE_SWAVES) void k_wide_rs(WideArgs W, M m, c
   end_step(cfg, a, c, valid, ph_in, S, A, false);
 }
 
+
+// ---- persistent per-chain schedule for the D-split models ----------
+// One workgroup of NT threads owns one chain (chain-row arena layout: the chain's rows are
+// contiguous, so the threads' accesses coalesce) and runs its leaves until the segment ends or
+// max_steps: the launched wide step's B / C / A kernels in one loop, with the chain's scalars
+// in registers (every thread runs the scalar logic on block-reduced sums, as the fused step's
+// lanes do; thread 0 writes).  Rows: thread t owns model rows lo + t, lo + t + NT, ... in both
+// phases and thread 0 the scalar-site rows, so a row is read and written by one thread only
+// within a leaf; the end-of-leaf barrier publishes the next positions (stencil neighbours and
+// scalar sites) to the other threads.  Sums: per thread in row order, the 64 lanes of a wave
+// by a butterfly, the waves in order, then the scalar-site rows -- fixed by (D, NT), NT by D.
+// The scalar-site rows' inputs are staged through LDS before the reduction's barrier: every
+// thread adds their terms to its totals, thread 0 alone stores them.
+
+// sum over a wave's 64 lanes; the butterfly gives every lane the same bits
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// the partial-sum entries a leaf reduces (uniform over the block): KE, the checkpoint pairs of
+// [imin, imax], the whole-tree pair at subtree completion, the model's sums (e >= NPART)
+__device__ __forceinline__ bool entry_used(const Act& A, bool nuts, int e) {
+  if (e == 0 || e >= NPART) return true;
+  if (!nuts) return false;
+  if (e >= 1 + 2 * MAXD) return A.tree_chk;
+  const int i = (e - 1) >> 1;
+  return i >= A.imin && i <= A.imax;
+}
+
+// stage 1 of the block sums: each wave's sum of every used entry -> lds[e * NW + wave]
+template <int NW, int N>
+__device__ __forceinline__ void wave_sums_to_lds(const float (&v)[N], float* lds, const Act& A, bool nuts) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < N; ++e)
+    if (entry_used(A, nuts, e)) {
+      const float t = wave_sum(v[e]);
+      if (lane == 0) lds[e * NW + wv] = t;
+    }
+}
+
+template <bool NUTS, int NT, int B, class M>
+__device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A, const M& m,
+                                                  const typename M::Glob& gl, float seff, uint32_t base, float* red) {
+  const Arena& a = *v.a;
+  const float* ZE = AV(NMX_F_Z_EVAL);
+  float* GE = AV(NMX_F_G_EVAL);
+  const int hi = m.hi();
+  for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B * NT) {
+    LeafIn x[B];
+    typename M::RowIn mi[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int d = d0 + q * NT;
+      if (d < hi) {
+        const uint32_t off = base + ((uint32_t)d << 2);
+        leaf_load<NUTS, true, false>(v, A, off, x[q]);
+        m.row_load(ZE, off, 4u, d, mi[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int d = d0 + q * NT;
+      if (d < hi) {
+        const uint32_t off = base + ((uint32_t)d << 2);
+        x[q].g = m.row_eval(mi[q], d, gl, red + NPART);
+        nmx_at(GE, off) = x[q].g;
+        leaf_store<NUTS, true>(v, A, seff, off, x[q], red);
+      }
+    }
+  }
+}
+
+// apply rows of thread t (model rows as in the leaf phase, then thread 0's scalar-site rows)
+template <int NT, int B, class M>
+__device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& A, const M& m, float step_eff,
+                                                   uint32_t base, int c, uint64_t seed, uint32_t gch, int it,
+                                                   float* samp, const int8_t* transform,
+                                                   const nmx_nuts_config& cfg) {
+  float ke0 = 0.0f;
+  const int hi = m.hi();
+  auto rows = [&](int d0, int dstep, int dend, auto bc) {
+    constexpr int BB = decltype(bc)::value;
+    for (; d0 < dend; d0 += BB * dstep) {
+      ApplyIn x[BB];
+      float n[BB];
+#pragma unroll
+      for (int q = 0; q < BB; ++q) {
+        const int d = d0 + q * dstep;
+        if (d < dend) apply_load(v, A, base + ((uint32_t)d << 2), x[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < BB; ++q) {
+        const int d = d0 + q * dstep;
+        n[q] = 0.0f;
+        if (A.start_iter && d < dend) {
+          float nb[4];
+          momentum_block(seed, gch, it, d >> 2, nb);
+          const int j = d & 3;
+          n[q] = j == 0 ? nb[0] : (j == 1 ? nb[1] : (j == 2 ? nb[2] : nb[3]));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < BB; ++q) {
+        const int d = d0 + q * dstep;
+        if (d < dend)
+          ke0 += apply_store(v, A, step_eff, d, base + ((uint32_t)d << 2), x[q], n[q], samp, transform, cfg,
+                             nmx_row_off(d, v.ldc, c));
+      }
+    }
+  };
+  rows(m.lo() + (int)threadIdx.x, NT, hi, std::integral_constant<int, B>{});
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < M::NSCALAR; ++i) {
+      const int d = m.scalar_row(i);
+      rows(d, 1, d + 1, std::integral_constant<int, 1>{});
+    }
+  }
+  return ke0;
+}
+
+template <int NT, int B, class M>
+__global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
+  constexpr int NW = NT / 64;
+  constexpr int NR = NPART + M::NSUM;
+  __shared__ float lds[NR * NW];
+  __shared__ float lds_ke[NW];
+  __shared__ float lds_sc[NPART];
+  __shared__ float lds_tot[NR + 1];  // block totals of the leaf's entries, then U
+  const StepArgs& P = Pk;
+  const nmx_nuts_config& cfg = P.cfg;
+  const Arena& a = P.a;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int D = cfg.dim, ldc = cfg.ldc;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+  ChainScalars S;
+  load_scalars(a, c, S);
+  if (S.phase == NMX_PH_DONE) return;
+  NMX_DCHECK(S.phase == NMX_PH_START || S.phase == NMX_PH_LEAF);
+  const uint32_t base = ((uint32_t)c * (uint32_t)D) << 2;  // byte offset of the chain's row 0
+  for (int step = 0; step < max_steps; ++step) {
+    // the field pointers are recomputed each leaf (cheap scalar arithmetic) rather than
+    // hoisted out of the loop: ~40 loop-invariant 64-bit pointers overflowed the SGPRs
+    Arena al = Pk.a;
+    asm volatile("" : "+s"(al.sbase), "+s"(al.vbase), "+s"(al.ckr), "+s"(al.ckrs), "+s"(al.sstride), "+s"(al.vstride));
+    size_t ck_stride = (size_t)D * ldc;
+    asm volatile("" : "+s"(ck_stride));
+    const VecCtx v{&al, ldc, D, ck_stride, cfg.unit_mass != 0};
+    Act A;
+    begin_act(cfg, S, S.phase, A);
+    if (A.leaf) {
+      const float seff = S.step_eff;
+      const typename M::Glob gl = m.globals_at(AV(NMX_F_Z_EVAL), base, 4u);
+      {
+        float red[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) red[i] = 0.0f;
+#if NMX_PX_CUT != 2
+        if (is_nuts) persist_leaf_rows<true, NT, B>(v, A, m, gl, seff, base, red);
+        else persist_leaf_rows<false, NT, B>(v, A, m, gl, seff, base, red);
+#endif
+        wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
+      }
+      __syncthreads();
+      if (wv == 0) {
+        // lane e: entry e's total over the waves (in wave order)
+        float tot = 0.0f;
+        if (lane < NR && entry_used(A, is_nuts, lane)) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) tot += lds[lane * NW + w];
+        }
+        // potential: U and the scalar-site gradients from the reduced sums (every lane alike)
+        float sums[M::NSUM];
+#pragma unroll
+        for (int k = 0; k < M::NSUM; ++k) sums[k] = __shfl(tot, NPART + k);
+        float gs[M::NSCALAR];
+        const float pe = m.fin(sums, gl, gs);
+        // the scalar-site rows' leapfrog end (thread 0 owns them in both phases); their terms
+        // join the totals after the rows'
+        if (lane == 0) {
+          float rs[NPART];
+#pragma unroll
+          for (int e = 0; e < NPART; ++e) rs[e] = 0.0f;
+#pragma unroll
+          for (int i = 0; i < M::NSCALAR; ++i) {
+            const uint32_t off = base + ((uint32_t)m.scalar_row(i) << 2);
+            nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
+            LeafIn x;
+            x.g = gs[i];
+            if (is_nuts) {
+              leaf_load<true, true, false>(v, A, off, x);
+              leaf_store<true, true>(v, A, seff, off, x, rs);
+            } else {
+              leaf_load<false, true, false>(v, A, off, x);
+              leaf_store<false, true>(v, A, seff, off, x, rs);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < NPART; ++e)
+            if (entry_used(A, is_nuts, e)) lds_sc[e] = rs[e];
+          lds_tot[NR] = pe;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < NPART && entry_used(A, is_nuts, lane)) tot += lds_sc[lane];
+        if (lane < NR) lds_tot[lane] = tot;
+      }
+      __syncthreads();
+      A.pe_eval = lds_tot[NR];
+    }
+#if NMX_PX_CUT != 3
+    leaf_phase(cfg, S, A, A.leaf ? 0.5f * lds_tot[0] : 0.0f, seed, gch);
+    tree_phase(
+        cfg, S, A, [&](int i, int side) { return lds_tot[1 + 2 * i + side]; },
+        [&](int side) { return lds_tot[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, tid == 0);
+#endif
+    const bool vec2 = A.take_leaf || A.done_sub || A.take_biased || A.hmc_accept || A.iter_done || A.start_iter ||
+                      A.prep_leaf;
+    float ke0 = 0.0f;
+    if (vec2) {
+      float* const samp = (A.slot >= 0 && P.samples) ? P.samples + (size_t)A.slot * D * ldc : nullptr;
+#if NMX_PX_CUT != 1
+      ke0 = persist_apply_rows<NT, B>(v, A, m, S.step_eff, base, c, seed, gch, S.it, samp, P.transform, cfg);
+#endif
+    }
+    if (A.start_iter) {
+      const float t = wave_sum(ke0);
+      if (lane == 0) lds_ke[wv] = t;
+    }
+    __syncthreads();  // this leaf's rows are written: the next leaf reads its neighbours' positions
+    if (A.start_iter) {
+      float t = 0.0f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += lds_ke[w];
+      S.E0 = S.pe + 0.5f * t;  // build_tree :1130
+      S.energy = S.E0;         // proposal energy of the initial tree (:1137)
+    }
+    if (A.fin_done) {
+      if (tid == 0) atomicAdd(&a.counters[0], 1);
+      break;
+    }
+  }
+  if (tid == 0) {
+    Arena al = Pk.a;  // addresses recomputed here, not kept live from load_scalars through the loop
+    asm volatile("" : "+s"(al.sbase), "+s"(al.sstride));
+    store_scalars(al, c, S);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
-// Reset / init kernels
+// Reset / init kernels (either arena layout: vidx)
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ size_t vidx(const nmx_nuts_config& cfg, int d, int c) {
+  return cfg.layout == NMX_LAYOUT_CHAIN_ROWS ? (size_t)c * cfg.dim + d : (size_t)d * cfg.ldc + c;
+}
+
 __global__ void k_nuts_reset(Arena a, nmx_nuts_config cfg, float step_size, const float* imm) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int ldc = cfg.ldc;
   if (c < ldc) {
     const bool valid = c < cfg.num_chains;
-    for (int f = 0; f < NUM_INT_SCALARS; ++f) a.is[f][c] = 0;
-    for (int f = 0; f < NUM_FLOAT_SCALARS; ++f) a.fs[f][c] = 0.0f;
+    for (int f = 0; f < NUM_INT_SCALARS; ++f) AI(NMX_F_PHASE + f)[c] = 0;
+    for (int f = 0; f < NUM_FLOAT_SCALARS; ++f) AF(NMX_F_STEP_SIZE + f)[c] = 0.0f;
     AI(NMX_F_PHASE)[c] = valid ? NMX_PH_NEEDINIT : NMX_PH_DONE;
     AF(NMX_F_STEP_SIZE)[c] = step_size;
     AF(NMX_F_STEP_EFF)[c] = step_size;
     AF(NMX_F_DA_PROX)[c] = logf(10.0f * step_size);  // warmup_adapter init_fn :576
     for (int d = 0; d < cfg.dim; ++d) {
-      const size_t idx = (size_t)d * ldc + c;
+      const size_t idx = vidx(cfg, d, c);
       const float im = imm ? imm[d] : 1.0f;
       AV(NMX_F_INV_MASS)[idx] = im;
       // _initialize_mass_matrix diag branch (:507-512): sqrt_inv = sqrt(imm), sqrt = 1/that
@@ -1527,14 +1810,13 @@ __global__ void k_nuts_init_draw(Arena a, nmx_nuts_config cfg, int attempt, floa
   if (c >= cfg.num_chains) return;
   if (AI(NMX_F_PHASE)[c] != NMX_PH_NEEDINIT) return;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
-  const int ldc = cfg.ldc;
   for (int blk = 0; 4 * blk < cfg.dim; ++blk) {
     const nmx_u4 x = nmx_rng(cfg.seed, gch, 0, NMX_EV_INIT, blk, (uint32_t)attempt);
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int d = 4 * blk + q;
-      if (d < cfg.dim) AV(NMX_F_Z_EVAL)[(size_t)d * ldc + c] = (2.0f * radius) * nmx_u01(w[q]) - radius;
+      if (d < cfg.dim) AV(NMX_F_Z_EVAL)[vidx(cfg, d, c)] = (2.0f * radius) * nmx_u01(w[q]) - radius;
     }
   }
   AI(NMX_F_PHASE)[c] = NMX_PH_INITEVAL;
@@ -1543,8 +1825,8 @@ __global__ void k_nuts_init_draw(Arena a, nmx_nuts_config cfg, int attempt, floa
 __global__ void k_nuts_init_from(Arena a, nmx_nuts_config cfg, const float* z) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cfg.num_chains) return;
-  const int ldc = cfg.ldc;
-  for (int d = 0; d < cfg.dim; ++d) AV(NMX_F_Z_EVAL)[(size_t)d * ldc + c] = z[(size_t)d * ldc + c];
+  const int ldc = cfg.ldc;  // z is [D][ldc] in either arena layout
+  for (int d = 0; d < cfg.dim; ++d) AV(NMX_F_Z_EVAL)[vidx(cfg, d, c)] = z[(size_t)d * ldc + c];
   AI(NMX_F_PHASE)[c] = NMX_PH_INITEVAL;
 }
 
@@ -1553,13 +1835,12 @@ __global__ void k_nuts_init_check(Arena a, nmx_nuts_config cfg) {
   if (c >= cfg.num_chains) return;
   const int ph = AI(NMX_F_PHASE)[c];
   if (ph == NMX_PH_INITEVAL) {
-    const int ldc = cfg.ldc;
     const float pe = AF(NMX_F_PE_EVAL)[c];
     bool ok = isfinite(pe);
-    for (int d = 0; d < cfg.dim; ++d) ok = ok && isfinite(AV(NMX_F_G_EVAL)[(size_t)d * ldc + c]);
+    for (int d = 0; d < cfg.dim; ++d) ok = ok && isfinite(AV(NMX_F_G_EVAL)[vidx(cfg, d, c)]);
     if (ok) {
       for (int d = 0; d < cfg.dim; ++d) {
-        const size_t idx = (size_t)d * ldc + c;
+        const size_t idx = vidx(cfg, d, c);
         AV(NMX_F_Z)[idx] = AV(NMX_F_Z_EVAL)[idx];
         AV(NMX_F_ZGRAD)[idx] = AV(NMX_F_G_EVAL)[idx];
       }
@@ -1708,6 +1989,15 @@ int validate(const nmx_nuts_config* cfg) {
     return nmx_fail(NMX_ERR_INVALID, "HMC needs num_steps or trajectory_length");
   if (cfg->ldc != ldc_of(cfg->num_chains))
     return nmx_fail(NMX_ERR_INVALID, "cfg.ldc must be round_up(num_chains, 64) = %d", ldc_of(cfg->num_chains));
+  if (cfg->layout != NMX_LAYOUT_CHAIN_MINOR && cfg->layout != NMX_LAYOUT_CHAIN_ROWS)
+    return nmx_fail(NMX_ERR_INVALID, "layout must be NMX_LAYOUT_CHAIN_MINOR(0) or NMX_LAYOUT_CHAIN_ROWS(1)");
+  return NMX_OK;
+}
+
+// the launched schedules index vectors [D][ldc]
+int need_chain_minor(const nmx_nuts_config* cfg, const char* what) {
+  if (cfg->layout != NMX_LAYOUT_CHAIN_MINOR)
+    return nmx_fail(NMX_ERR_INVALID, "%s needs the chain-minor arena layout (NMX_LAYOUT_CHAIN_MINOR)", what);
   return NMX_OK;
 }
 
@@ -1782,6 +2072,7 @@ extern "C" int nmx_nuts_init_check(const nmx_nuts_config* cfg, void* arena, void
 extern "C" int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_heuristic_begin"))) return st;
   Arena a = arena_of(cfg, arena);
   hipLaunchKernelGGL(k_heur_begin, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a, *cfg);
   return nmx_check_launch("k_heur_begin");
@@ -1790,6 +2081,7 @@ extern "C" int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void
 extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_heuristic_propose"))) return st;
   Arena a = arena_of(cfg, arena);
   if (hipMemsetAsync(a.counters + 2, 0, 4, (hipStream_t)stream) != hipSuccess)
     return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
@@ -1801,6 +2093,7 @@ extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, vo
 extern "C" int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_heuristic_finish"))) return st;
   Arena a = arena_of(cfg, arena);
   if (hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream) != hipSuccess)
     return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
@@ -1823,6 +2116,7 @@ extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float
                                   int max_steps, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_nuts_run_small"))) return st;
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
@@ -1856,6 +2150,7 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
                              const int8_t* transform, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_nuts_step"))) return st;
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
@@ -1911,6 +2206,7 @@ extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena,
                                         void* workspace, void* stream) {
   int st = validate(cfg);
   if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_nuts_step_wide_model"))) return st;
   if (!arena || !workspace) return nmx_fail(NMX_ERR_INVALID, "arena / workspace is NULL");
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
@@ -1940,5 +2236,74 @@ extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena,
       return launch_wide_model(w, NmxWideFunnelNC{n}, ws, cfg->ldc, s);
     default:
       return nmx_fail(NMX_ERR_INVALID, "step_wide_model: unknown model %d", model);
+  }
+}
+
+namespace {
+// threads per chain of the persistent wide kernel, from dim only (the sums' order depends on
+// it; NMX_PERSIST_NT overrides for kernel experiments)
+int persist_nt(int dim) {
+  if (const char* e = getenv("NMX_PERSIST_NT")) {
+    const int v = atoi(e);
+    if (v == 256 || v == 512 || v == 1024) return v;
+  }
+  return dim <= 1024 ? 256 : 512;
+}
+
+template <class M>
+int launch_persistent(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
+  const dim3 grid(args.cfg.num_chains);
+  switch (persist_nt(args.cfg.dim)) {
+    case 256:
+      hipLaunchKernelGGL((k_wide_persistent<256, NMX_PX_B, M>), grid, dim3(256), 0, s, args, m, max_steps);
+      break;
+    case 512:
+      hipLaunchKernelGGL((k_wide_persistent<512, 2, M>), grid, dim3(512), 0, s, args, m, max_steps);
+      break;
+    default:
+      hipLaunchKernelGGL((k_wide_persistent<1024, 2, M>), grid, dim3(1024), 0, s, args, m, max_steps);
+  }
+  return nmx_check_launch("k_wide_persistent");
+}
+}  // namespace
+
+extern "C" int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
+                                 const int8_t* transform, int model, const float* data, int n, int max_steps,
+                                 void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
+  if (cfg->layout != NMX_LAYOUT_CHAIN_ROWS)
+    return nmx_fail(NMX_ERR_INVALID, "run_wide needs the chain-row arena layout (NMX_LAYOUT_CHAIN_ROWS)");
+  if (cfg->sync_chains)
+    return nmx_fail(NMX_ERR_INVALID, "run_wide: per-chain async only (lockstep: one launch per transition)");
+  // samples may be NULL: the per-transition fields alone are collected
+  if (cfg->collection_size > 0 && (!fields || !transform))
+    return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
+  if (max_steps <= 0) return nmx_fail(NMX_ERR_INVALID, "run_wide: max_steps must be positive");
+  // 32-bit byte offsets within a field
+  if ((size_t)cfg->ldc * cfg->dim * 4 > 0xFFFFFFF0ull)
+    return nmx_fail(NMX_ERR_INVALID, "run_wide: a vector field exceeds 4 GiB");
+  StepArgs args;
+  args.a = arena_of(cfg, arena);
+  args.cfg = *cfg;
+  args.samples = samples;
+  args.fields = fields;
+  args.transform = transform;
+  hipStream_t s = (hipStream_t)stream;
+  switch (model) {
+    case NMX_WIDE_STOCHASTIC_VOLATILITY:
+      if (!data || n <= 1 || n + 2 != cfg->dim)
+        return nmx_fail(NMX_ERR_INVALID, "run_wide: stochastic volatility needs returns[T], dim == T + 2");
+      return launch_persistent(args, NmxWideSV{data, n}, max_steps, s);
+    case NMX_WIDE_FUNNEL:
+      if (n != cfg->dim || n < 2) return nmx_fail(NMX_ERR_INVALID, "run_wide: funnel needs n == dim >= 2");
+      return launch_persistent(args, NmxWideFunnel{n}, max_steps, s);
+    case NMX_WIDE_FUNNEL_NONCENTERED:
+      if (n != cfg->dim || n < 2)
+        return nmx_fail(NMX_ERR_INVALID, "run_wide: funnel_noncentered needs n == dim >= 2");
+      return launch_persistent(args, NmxWideFunnelNC{n}, max_steps, s);
+    default:
+      return nmx_fail(NMX_ERR_INVALID, "run_wide: unknown model %d", model);
   }
 }

@@ -89,6 +89,9 @@ class Engine:
     # D-split models: the step fused with the potential (nmx_nuts_step_wide_model; False: the
     # launched potential + step loop, which tests compare it with)
     fused_wide = True
+    # D-split models with diagonal mass: the persistent per-chain schedule (nmx_nuts_run_wide,
+    # chain-row arena layout); False: the launched wide schedules above
+    wide_persistent = True
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
@@ -147,6 +150,13 @@ class Engine:
         self.constrain_samples = True
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
+        # chain-row arena layout for the persistent wide schedule (decided once: the arena's
+        # layout is part of a resumable state).  The step-size search runs on the launched
+        # kernels, which index [D][ldc]: with it, the launched schedule.
+        self.crow = (self.wide_persistent and not self.dense and not opts.find_heuristic_step_size
+                     and lib().nmx_nuts_num_slices(self.D) > 0
+                     and getattr(self.potential, "wide_model", None) is not None
+                     and self.potential.wide_model() is not None)
 
     # ------------------------------------------------------------------ arena
     def _alloc(self, iter_capacity: int):
@@ -174,9 +184,10 @@ class Engine:
         raw = self.arena[off.value:off.value + nb.value]
         t = raw.view(torch.int32 if name in native.INT_FIELDS else torch.float32)
         if name in native.VECTOR_FIELDS:
-            t = t.view(self.D, self.ldc)
+            # chain-row layout: stored [ldc][D], viewed [D, ldc] like the other layout
+            t = t.view(self.ldc, self.D).t() if self.crow else t.view(self.D, self.ldc)
         elif name in native.CKPT_FIELDS:
-            t = t.view(self.md, self.D, self.ldc)
+            t = t.view(self.md, self.ldc, self.D).transpose(1, 2) if self.crow else t.view(self.md, self.D, self.ldc)
         self._views[name] = t
         return t
 
@@ -216,6 +227,7 @@ class Engine:
         c.collect_thinning = int(thinning)
         c.collection_size = int(collection_size)
         c.ldc = self.ldc
+        c.layout = native.LAYOUT_CHAIN_ROWS if self.crow else native.LAYOUT_CHAIN_MINOR
 
     # ------------------------------------------------------------------ phases
     def initialize(self, seed: int, num_warmup: int, init_params=None, radius: float = 2.0,
@@ -247,7 +259,7 @@ class Engine:
             zt = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device)
             zt[:, :self.C] = z.t()
             check(lib().nmx_nuts_init_from(ctypes.byref(self.cfg), ptr(self.arena), ptr(zt), s))
-            self.potential.evaluate(self.eval_batch, s)
+            self._evaluate_all(s)
             check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
             bad = int(self.view("counters")[1].item())
             if bad:
@@ -257,7 +269,7 @@ class Engine:
             for attempt in range(INIT_ATTEMPTS):
                 check(lib().nmx_nuts_init_draw(ctypes.byref(self.cfg), ptr(self.arena), attempt,
                                                float(radius), s))
-                self.potential.evaluate(self.eval_batch, s)
+                self._evaluate_all(s)
                 check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
                 if int(self.view("counters")[1].item()) == 0:
                     break
@@ -271,6 +283,20 @@ class Engine:
         if self._heuristic():
             self._find_step_size(True, s)
         self.generation = next(_generations)
+
+    def _evaluate_all(self, s):
+        """The potential at z_eval of every chain with phase >= LEAF (initial points).  The
+        potential kernels take [D][ldc] positions: a chain-row arena is evaluated through
+        transposed copies."""
+        if not self.crow:
+            self.potential.evaluate(self.eval_batch, s)
+            return
+        zt = self.view("z_eval").contiguous()
+        gt = torch.zeros_like(zt)
+        b = EvalBatch(z=ptr(zt), grad=ptr(gt), pe=ptr(self.view("pe_eval")), phase=ptr(self.view("phase")),
+                      active_idx=None, active_count=None, num_chains=self.C, ldc=self.ldc)
+        self.potential.evaluate(b, s)
+        self.view("g_eval").copy_(gt)
 
     # ------------------------------------------------------------------ dense mass
     def _heuristic(self):
@@ -501,6 +527,8 @@ class Engine:
         cfgp = ctypes.byref(self.cfg)
         arena = ptr(self.arena)
         tr = self._collect_codes()
+        if self.crow:
+            return self._run_wide_persistent(a, b, seed, cstart, thinning, S, samples, fields, s, max_launches)
         check(lib().nmx_nuts_resume(cfgp, arena, s), "nmx_nuts_resume")
         small = self._persistent_model()
         if small is not None:
@@ -567,6 +595,32 @@ class Engine:
                 raise RuntimeError(f"chains did not finish within {max_launches} leapfrog launches")
         return launches
 
+    def _run_wide_persistent(self, a, b, seed, cstart, thinning, S, samples, fields, s, max_launches):
+        """nmx_nuts_run_wide: one launch runs every chain through [a, b) (relaunched while
+        some chain hit the leaf bound, e.g. long HMC trajectories).  The lockstep schedule
+        (sync_chains) is one launch per transition: no chain starts transition t + 1 before
+        every chain finished t, and each chain's computation is the same as unsynchronised."""
+        model, data, n = self.potential.wide_model()
+        tr = self._collect_codes()
+        sp, fp, tp, dp = ptr(samples) if samples.shape[0] else None, ptr(fields), ptr(tr), ptr(data)
+        run = lib().nmx_nuts_run_wide
+        spans = [(t, t + 1) for t in range(a, b)] if self.sync_chains else [(a, b)]
+        launches = 0
+        for t0, t1 in spans:
+            self._fill_cfg(t0, t1, self.num_warmup, seed, cstart, thinning, S)
+            self.cfg.sync_chains = 0
+            cfgp = ctypes.byref(self.cfg)
+            check(lib().nmx_nuts_resume(cfgp, ptr(self.arena), s), "nmx_nuts_resume")
+            max_steps = (t1 - t0) * ((1 << self.md) + 2) + 16
+            while True:
+                check(run(cfgp, ptr(self.arena), sp, fp, tp, model, dp, n, max_steps, s), "nmx_nuts_run_wide")
+                launches += 1
+                if int(self.view("counters")[0].item()) >= self.C:
+                    break
+                if max_launches is not None and launches * max_steps >= max_launches:
+                    raise RuntimeError(f"chains did not finish within {max_launches} leapfrog steps")
+        return launches
+
     def _grow_finished(self, n):
         # re-layout the arena with a larger sync-counter table, keeping all chain state
         old = self.arena
@@ -623,7 +677,7 @@ class Engine:
         """What a state's arena copy must match to be resumed by this engine (a pickled
         state is resumed by the engine of an unpickled MCMC / kernel in another process)."""
         return (type(self.model_potential).__name__, self.C, self.D, self.md, self.chain_offset, self.dense,
-                self.chain_dense, self.opts.algo)
+                self.chain_dense, self.opts.algo, self.crow)
 
     def chain_state(self, name):
         """Per-chain view without padding: scalars [C], vectors [C, D]."""

@@ -75,7 +75,11 @@ class NutsConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64), ("chain_offset", ctypes.c_int64),
         ("collect_start", ctypes.c_int32), ("collect_thinning", ctypes.c_int32),
         ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32), ("parity", ctypes.c_int32),
+        ("layout", ctypes.c_int32),
     ]
+
+
+LAYOUT_CHAIN_MINOR, LAYOUT_CHAIN_ROWS = 0, 1  # enum nmx_layout
 
 
 SMALL_DIAG_NORMAL, SMALL_EIGHT_SCHOOLS = 1, 2  # nmx_nuts_run_small models
@@ -114,6 +118,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_heuristic_propose": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_heuristic_finish": (c_int, [_cfgp, c_vp, c_int, c_vp]),
     "nmx_nuts_run_small": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
+    "nmx_nuts_run_wide": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp]),
     "nmx_predict_logreg": (c_int, [c_vp, ctypes.c_int64, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_predict_normal": (c_int, [c_vp, c_vp, c_int, c_int, ctypes.c_uint64, c_vp, c_vp]),
     "nmx_predict_bnn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),

@@ -148,6 +148,7 @@ def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None,
         if pot_ms > 0:  # launched loop: the potential kernels alone (read z, write grad)
             out["roofline"]["potential_GBs"] = round(bytes_per_leapfrog * ns / (pot_ms * 1e-3) / 1e9, 1)
         out["fused_wide"] = launches == 0
+        out["schedule"] = "persistent" if getattr(eng, "crow", False) else ("fused" if launches == 0 else "launched")
     print(json.dumps(out), flush=True)
     return mcmc
 
@@ -163,13 +164,15 @@ def main():
     p.add_argument("--max-tree-depth", type=int, default=10)
     p.add_argument("--dense", type=int, default=1)
     p.add_argument("--launched", action="store_true", help="wide models: potential + step loop (A/B)")
+    p.add_argument("--fused", action="store_true", help="wide models: the launched fused step, not the persistent one")
     p.add_argument("--lib", default=None, help="A/B: load this build of libnumpyro_amd.so")
     a = p.parse_args()
     if a.lib:
         native.LIB_PATH = os.path.abspath(a.lib)
-    if a.launched:
+    if a.launched or a.fused:
         from numpyro_amd.engine import Engine
-        Engine.fused_wide = False
+        Engine.wide_persistent = False
+        Engine.fused_wide = not a.launched
     if a.what == "gemm":
         D = int(a.rest[0]) if a.rest else 10000
         C = int(a.rest[1]) if len(a.rest) > 1 else 4096

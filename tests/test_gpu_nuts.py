@@ -327,6 +327,14 @@ def test_adaptation_matches_oracle(device, model, dim, C):
                             np.float32(sn["mean_acc"][c]), False, wa, (seed, c))
             ok, margins = [], []
             for k in range(K):
+                if k > 0:
+                    # the step size the device adapted to (teacher-forced): dual averaging
+                    # restarted at t = 0 multiplies accept-probability rounding by 20 sqrt(t)
+                    # (2.6e-4 relative drift measured), which moves later trajectories by more
+                    # than rounding; the restart checks the transitions, the teacher-forced
+                    # check above the adapter
+                    st = st._replace(adapt_state=st.adapt_state._replace(
+                        step_size=np.float32(dev["step_size"][c, e + k - 1])))
                 H.DECISIONS = []
                 try:
                     st = o.sample(st)
@@ -447,41 +455,60 @@ def _wide_model_case(which):
     return (900,), P.funnel_reparam, "x_decentered"
 
 
-@pytest.mark.parametrize("which", ["sv", "funnel", "funnel_reparam"])
+@pytest.mark.parametrize("which", ["sv", "funnel", "funnel_reparam", "funnel_reparam_hmc"])
 def test_wide_model_step_matches_launched_loop(device, which, monkeypatch):
-    """nmx_nuts_step_wide_model (the model's row gradients fused with the leapfrog end, the
-    potential finished in the reduction's last block: three launches per leaf) against the
-    launched potential + nmx_nuts_step loop (six).  Same arithmetic per coordinate; U, the
-    scalar-site gradients and the dot products are summed in another fixed order, so the two
-    agree to rounding: fixed step size, the discrete paths of >= 90% of chains and their draws
-    to 1e-3 (fp32 rounding grows along SV's long trajectories as in the oracle comparisons)."""
+    """The two fused schedules of a D-split model against the launched potential +
+    nmx_nuts_step loop (six launches per leaf): nmx_nuts_step_wide_model (the model's row
+    gradients fused with the leapfrog end, the potential finished in the reduction's last
+    block: three launches per leaf) and the persistent per-chain nmx_nuts_run_wide (one launch
+    per run, chain-row arena).  Same arithmetic per coordinate; U, the scalar-site gradients
+    and the dot products are summed in other fixed orders, so they agree to rounding: fixed
+    step size, the discrete paths of >= 90% of chains and their draws to 1e-3 (fp32 rounding
+    grows along SV's long trajectories as in the oracle comparisons)."""
     from numpyro_amd.engine import Engine
 
+    hmc = which.endswith("_hmc")
+    which = which.replace("_hmc", "")
     args, fm, site = _wide_model_case(which)
     kw = dict(step_size={"sv": 0.005, "funnel": 0.05, "funnel_reparam": 0.3}[which], adapt_step_size=False,
               adapt_mass_matrix=False)
-    out = {}
-    for fused in (False, True):
+    if which == "sv":
+        kw["max_tree_depth"] = 7  # fp32 rounding differences grow along SV's 1023-leaf trees
+    if hmc:
+        kw.update(kernel_cls=HMC, num_steps=7)
+    out, launches = {}, {}
+    for mode, (fused, pers) in {"launched": (False, False), "fused": (True, False), "persistent": (True, True)}.items():
         monkeypatch.setattr(Engine, "fused_wide", fused)
+        monkeypatch.setattr(Engine, "wide_persistent", pers)
         mcmc, _ = _run_engine(args, fm, 96, 0, 3, 21, **kw)
-        out[fused] = (mcmc.get_samples(True)[site].cpu().numpy(),
-                      mcmc.get_extra_fields(True)["num_steps"].cpu().numpy(),
-                      mcmc.get_extra_fields(True)["potential_energy"].cpu().numpy())
-    (x0, n0, u0), (x1, n1, u1) = out[False], out[True]
-    same = np.all(n0 == n1, axis=1) & np.all(np.isclose(x0, x1, rtol=1e-3, atol=1e-3).reshape(96, -1), axis=1)
-    print(f"[wide model {which}] {int(same.sum())}/96 chains: same tree sizes and draws as the launched loop")
-    assert same.sum() >= 86  # the oracle tests' bar (>= 90%) for these stiff targets
-    # U agrees where the draws agree closely (at 1e-3-close draws U itself can move by ~1e-2
-    # relative: |grad U| ~ 1e2-1e3 along SV's random walk)
-    close = same & np.all(np.isclose(x0, x1, rtol=1e-5, atol=1e-5).reshape(96, -1), axis=1)
-    # (U ~ 1e2 is the cancellation of sums of ~700 terms whose magnitudes add to ~1e4, summed in
-    # another order, at draws equal to 1e-5 with |grad U| ~ 1e3: ~1e-1 absolute)
-    np.testing.assert_allclose(u1[close], u0[close], rtol=1e-4, atol=0.2)
+        out[mode] = (mcmc.get_samples(True)[site].cpu().numpy(),
+                     mcmc.get_extra_fields(True)["num_steps"].cpu().numpy(),
+                     mcmc.get_extra_fields(True)["potential_energy"].cpu().numpy())
+        launches[mode] = mcmc.last_run_stats["launches"]
+    assert launches["persistent"] <= 2 < launches["fused"]  # one launch runs the whole segment
+    x0, n0, u0 = out["launched"]
+    for mode in ("fused", "persistent"):
+        x1, n1, u1 = out[mode]
+        same = np.all(n0 == n1, axis=1) & np.all(np.isclose(x0, x1, rtol=1e-3, atol=1e-3).reshape(96, -1), axis=1)
+        print(f"[wide model {which}{' hmc' if hmc else ''} {mode}] {int(same.sum())}/96 chains: same tree sizes "
+              "and draws as the launched loop")
+        assert same.sum() >= 86  # the oracle tests' bar (>= 90%) for these stiff targets
+        # U agrees where the draws agree closely (at 1e-3-close draws U itself can move by ~1e-2
+        # relative: |grad U| ~ 1e2-1e3 along SV's random walk)
+        close = same & np.all(np.isclose(x0, x1, rtol=1e-5, atol=1e-5).reshape(96, -1), axis=1)
+        # (U ~ 1e2 is the cancellation of sums of ~700 terms whose magnitudes add to ~1e4, summed in
+        # another order, at draws equal to 1e-5 with |grad U| ~ 1e3: ~1e-1 absolute)
+        np.testing.assert_allclose(u1[close], u0[close], rtol=1e-4, atol=0.2)
 
 
-def test_wide_model_step_invariances(device):
-    """The fused wide-model step keeps the engine's invariances bitwise: sync == async, and
-    two chain shards reproduce the unsharded run (sums in an order fixed by D only)."""
+@pytest.mark.parametrize("persistent", [True, False])
+def test_wide_model_step_invariances(device, persistent, monkeypatch):
+    """Both fused wide-model schedules keep the engine's invariances bitwise: sync == async
+    (the persistent kernel's lockstep schedule is one launch per transition), and two chain
+    shards reproduce the unsharded run (sums in an order fixed by D only)."""
+    from numpyro_amd.engine import Engine
+
+    monkeypatch.setattr(Engine, "wide_persistent", persistent)
     args, fm, site = _wide_model_case("sv")
     a, _ = _run_engine(args, fm, 96, 30, 10, 4, sync=False)
     b, _ = _run_engine(args, fm, 96, 30, 10, 4, sync=True)
