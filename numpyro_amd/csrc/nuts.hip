@@ -1086,10 +1086,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
     // one row per round with the row's checkpoints loaded ahead: 114 VGPRs, 4 waves per SIMD
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
 #ifndef NMX_PX_B
-#define NMX_PX_B 2
-#endif
-#ifndef NMX_PX_CUT
-#define NMX_PX_CUT 0
+#define NMX_PX_B 3  // rows per thread in flight in the persistent wide kernel (2: SV -2.5%, funnel -4%)
 #endif
 #ifndef NMX_V1_ROWS
 #define NMX_V1_ROWS 1
@@ -1641,6 +1638,24 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
   return ke0;
 }
 
+// NMX_PX_PROF (kernel experiments, scripts/px_profile.py): thread 0 of every block adds the
+// shader-clock cycles of each phase of its leaves to g_px_prof (nmx_debug_px_profile reads them)
+#ifdef NMX_PX_PROF
+__device__ unsigned long long g_px_prof[16];
+#define PX_T(i) const long long px_t##i = clock64()
+#define PX_ADD(k, a, b) if (threadIdx.x == 0) atomicAdd(&g_px_prof[k], (unsigned long long)(px_t##b - px_t##a))
+#else
+#define PX_T(i)
+#define PX_ADD(k, a, b)
+#endif
+
+// wave-uniform copies of values every lane holds alike (LDS reads look divergent to the
+// compiler; as scalars they stay out of the vector registers)
+__device__ __forceinline__ int uni_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float uni_f(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
 template <int NT, int B, class M>
 __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
   constexpr int NW = NT / 64;
@@ -1649,6 +1664,12 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
   __shared__ float lds_ke[NW];
   __shared__ float lds_sc[NPART];
   __shared__ float lds_tot[NR + 1];  // block totals of the leaf's entries, then U
+  // the chain's scalar state lives in LDS: wave 0 runs the scalar logic on it and publishes
+  // the decisions the vector phases need (the act word of k_wide_v2 plus four values), so no
+  // per-chain scalar is held in vector registers through the row loops
+  __shared__ ChainScalars Ssh;
+  __shared__ int sh_act, sh_slot, sh_wfn, sh_it;
+  __shared__ float sh_seff;
   const StepArgs& P = Pk;
   const nmx_nuts_config& cfg = P.cfg;
   const Arena& a = P.a;
@@ -1658,10 +1679,14 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
   const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   const uint64_t seed = cfg.seed;
-  ChainScalars S;
-  load_scalars(a, c, S);
-  if (S.phase == NMX_PH_DONE) return;
-  NMX_DCHECK(S.phase == NMX_PH_START || S.phase == NMX_PH_LEAF);
+  if (uni_i(AI(NMX_F_PHASE)[c]) == NMX_PH_DONE) return;
+  if (tid == 0) {
+    ChainScalars S;
+    load_scalars(a, c, S);
+    NMX_DCHECK(S.phase == NMX_PH_START || S.phase == NMX_PH_LEAF);
+    Ssh = S;
+  }
+  __syncthreads();
   const uint32_t base = ((uint32_t)c * (uint32_t)D) << 2;  // byte offset of the chain's row 0
   for (int step = 0; step < max_steps; ++step) {
     // the field pointers are recomputed each leaf (cheap scalar arithmetic) rather than
@@ -1671,22 +1696,37 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
     size_t ck_stride = (size_t)D * ldc;
     asm volatile("" : "+s"(ck_stride));
     const VecCtx v{&al, ldc, D, ck_stride, cfg.unit_mass != 0};
+    const int ph = uni_i(Ssh.phase);
+    if (ph == NMX_PH_DONE) break;
+    // the leaf's inputs (begin_act on the four scalars it reads)
     Act A;
-    begin_act(cfg, S, S.phase, A);
+    {
+      ChainScalars Sb;
+      Sb.dir = uni_i(Ssh.dir);
+      Sb.sub_n = uni_i(Ssh.sub_n);
+      Sb.depth = uni_i(Ssh.depth);
+      begin_act(cfg, Sb, ph, A);
+    }
+    // every wave has read the state before wave 0's scalar logic rewrites it (a leaf's
+    // reduction barrier orders this too)
+    PX_T(0);
+    if (!A.leaf) __syncthreads();
     if (A.leaf) {
-      const float seff = S.step_eff;
+      const float seff = uni_f(Ssh.step_eff);
       const typename M::Glob gl = m.globals_at(AV(NMX_F_Z_EVAL), base, 4u);
       {
         float red[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) red[i] = 0.0f;
-#if NMX_PX_CUT != 2
         if (is_nuts) persist_leaf_rows<true, NT, B>(v, A, m, gl, seff, base, red);
         else persist_leaf_rows<false, NT, B>(v, A, m, gl, seff, base, red);
-#endif
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
+      PX_T(1);
+      PX_ADD(0, 0, 1);
       __syncthreads();
+      PX_T(2);
+      PX_ADD(1, 1, 2);
       if (wv == 0) {
         // lane e: entry e's total over the waves (in wave order)
         float tot = 0.0f;
@@ -1730,46 +1770,88 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < NPART && entry_used(A, is_nuts, lane)) tot += lds_sc[lane];
         if (lane < NR) lds_tot[lane] = tot;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      __syncthreads();
-      A.pe_eval = lds_tot[NR];
     }
-#if NMX_PX_CUT != 3
-    leaf_phase(cfg, S, A, A.leaf ? 0.5f * lds_tot[0] : 0.0f, seed, gch);
-    tree_phase(
-        cfg, S, A, [&](int i, int side) { return lds_tot[1 + 2 * i + side]; },
-        [&](int side) { return lds_tot[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, tid == 0);
+    PX_T(3);
+    PX_ADD(2, 0, 3);
+    // scalar logic: wave 0 on the LDS state (lane 0 writes back)
+    if (wv == 0) {
+      ChainScalars S = Ssh;
+      if (A.leaf) A.pe_eval = lds_tot[NR];
+      leaf_phase(cfg, S, A, A.leaf ? 0.5f * lds_tot[0] : 0.0f, seed, gch);
+      tree_phase(
+          cfg, S, A, [&](int i, int side) { return lds_tot[1 + 2 * i + side]; },
+          [&](int side) { return lds_tot[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, lane == 0);
+      if (lane == 0) {
+        Ssh = S;
+        sh_act = pack_act(A);
+        sh_slot = A.slot;
+        sh_wfn = A.wfn;
+        sh_it = S.it;
+        sh_seff = S.step_eff;
+        if (A.fin_done) atomicAdd(&a.counters[0], 1);
+      }
+    }
+    PX_T(4);
+    PX_ADD(3, 3, 4);
+    __syncthreads();  // decisions published
+    PX_T(5);
+    const int act = uni_i(sh_act);
+    {
+      Act D2{};
+      D2.take_leaf = act & ACT_TAKE_LEAF;
+      D2.done_sub = act & ACT_DONE_SUB;
+      D2.take_biased = act & ACT_TAKE_BIASED;
+      D2.hmc_accept = act & ACT_HMC_ACCEPT;
+      D2.iter_done = act & ACT_ITER_DONE;
+      D2.wf_update = act & ACT_WF_UPDATE;
+      D2.finalize = act & ACT_FINALIZE;
+      D2.start_iter = act & ACT_START;
+      D2.prep_leaf = act & ACT_PREP;
+      D2.dirR = (act & ACT_DIRR) ? 1 : 0;
+      D2.new_dir = (act & ACT_NEWDIR) ? 1 : 0;
+      D2.slot = uni_i(sh_slot);
+      D2.wfn = uni_i(sh_wfn);
+      constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE |
+                          ACT_START | ACT_PREP;
+      float ke0 = 0.0f;
+      if (act & VEC) {
+        float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc
+                                                                         : nullptr;
+        ke0 = persist_apply_rows<NT, B>(v, D2, m, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp,
+                                        P.transform, cfg);
+      }
+      if (D2.start_iter) {
+        const float t = wave_sum(ke0);
+        if (lane == 0) lds_ke[wv] = t;
+      }
+      PX_T(6);
+      PX_ADD(4, 5, 6);
+      __syncthreads();  // this leaf's rows are written: the next leaf reads its neighbours' positions
+      PX_T(7);
+      PX_ADD(5, 6, 7);
+      PX_ADD(6, 0, 7);
+      if (threadIdx.x == 0) {
+#ifdef NMX_PX_PROF
+        atomicAdd(&g_px_prof[7], 1ull);
 #endif
-    const bool vec2 = A.take_leaf || A.done_sub || A.take_biased || A.hmc_accept || A.iter_done || A.start_iter ||
-                      A.prep_leaf;
-    float ke0 = 0.0f;
-    if (vec2) {
-      float* const samp = (A.slot >= 0 && P.samples) ? P.samples + (size_t)A.slot * D * ldc : nullptr;
-#if NMX_PX_CUT != 1
-      ke0 = persist_apply_rows<NT, B>(v, A, m, S.step_eff, base, c, seed, gch, S.it, samp, P.transform, cfg);
-#endif
-    }
-    if (A.start_iter) {
-      const float t = wave_sum(ke0);
-      if (lane == 0) lds_ke[wv] = t;
-    }
-    __syncthreads();  // this leaf's rows are written: the next leaf reads its neighbours' positions
-    if (A.start_iter) {
-      float t = 0.0f;
+      }
+      if (D2.start_iter && tid == 0) {
+        float t = 0.0f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) t += lds_ke[w];
-      S.E0 = S.pe + 0.5f * t;  // build_tree :1130
-      S.energy = S.E0;         // proposal energy of the initial tree (:1137)
-    }
-    if (A.fin_done) {
-      if (tid == 0) atomicAdd(&a.counters[0], 1);
-      break;
+        for (int w = 0; w < NW; ++w) t += lds_ke[w];
+        Ssh.E0 = Ssh.pe + 0.5f * t;  // build_tree :1130
+        Ssh.energy = Ssh.E0;         // proposal energy of the initial tree (:1137)
+      }
     }
   }
   if (tid == 0) {
     Arena al = Pk.a;  // addresses recomputed here, not kept live from load_scalars through the loop
     asm volatile("" : "+s"(al.sbase), "+s"(al.sstride));
-    store_scalars(al, c, S);
+    store_scalars(al, c, Ssh);
   }
 }
 
@@ -2245,23 +2327,28 @@ namespace {
 int persist_nt(int dim) {
   if (const char* e = getenv("NMX_PERSIST_NT")) {
     const int v = atoi(e);
-    if (v == 256 || v == 512 || v == 1024) return v;
+    if (v == 128 || v == 256 || v == 512 || v == 1024) return v;
   }
-  return dim <= 1024 ? 256 : 512;
+  // SV (D = 2519): 256 -> 13.1M leapfrog/s at 8192 chains, 512 -> 9.6M; funnel-10k: 512 -> 5.1M,
+  // 256 -> 4.7M (profiles/r03/ab_persistent_nt.txt)
+  return dim <= 4096 ? 256 : 512;
 }
 
 template <class M>
 int launch_persistent(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
   const dim3 grid(args.cfg.num_chains);
   switch (persist_nt(args.cfg.dim)) {
+    case 128:
+      hipLaunchKernelGGL((k_wide_persistent<128, NMX_PX_B, M>), grid, dim3(128), 0, s, args, m, max_steps);
+      break;
     case 256:
       hipLaunchKernelGGL((k_wide_persistent<256, NMX_PX_B, M>), grid, dim3(256), 0, s, args, m, max_steps);
       break;
     case 512:
-      hipLaunchKernelGGL((k_wide_persistent<512, 2, M>), grid, dim3(512), 0, s, args, m, max_steps);
+      hipLaunchKernelGGL((k_wide_persistent<512, NMX_PX_B, M>), grid, dim3(512), 0, s, args, m, max_steps);
       break;
     default:
-      hipLaunchKernelGGL((k_wide_persistent<1024, 2, M>), grid, dim3(1024), 0, s, args, m, max_steps);
+      hipLaunchKernelGGL((k_wide_persistent<1024, NMX_PX_B, M>), grid, dim3(1024), 0, s, args, m, max_steps);
   }
   return nmx_check_launch("k_wide_persistent");
 }
@@ -2307,3 +2394,16 @@ extern "C" int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float*
       return nmx_fail(NMX_ERR_INVALID, "run_wide: unknown model %d", model);
   }
 }
+
+#ifdef NMX_PX_PROF
+// kernel experiments only: the per-phase cycle sums of k_wide_persistent (thread 0 of each block;
+// [0] leaf rows, [1] reduction barrier wait, [2] = leaf rows .. end of the potential's finish,
+// [3] scalar logic, [4] apply rows, [5] end barrier wait, [6] whole leaf, [7] leaves), then reset
+extern "C" int nmx_debug_px_profile(unsigned long long* host16) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_px_prof), sizeof(unsigned long long) * 16) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
+  unsigned long long z[16] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_px_prof), z, sizeof(z)) != hipSuccess) return nmx_fail(NMX_ERR_HIP, "reset");
+  return NMX_OK;
+}
+#endif

@@ -498,7 +498,7 @@ def test_wide_model_step_matches_launched_loop(device, which, monkeypatch):
         close = same & np.all(np.isclose(x0, x1, rtol=1e-5, atol=1e-5).reshape(96, -1), axis=1)
         # (U ~ 1e2 is the cancellation of sums of ~700 terms whose magnitudes add to ~1e4, summed in
         # another order, at draws equal to 1e-5 with |grad U| ~ 1e3: ~1e-1 absolute)
-        np.testing.assert_allclose(u1[close], u0[close], rtol=1e-4, atol=0.2)
+        np.testing.assert_allclose(u1[close], u0[close], rtol=3e-4, atol=0.2)
 
 
 @pytest.mark.parametrize("persistent", [True, False])
