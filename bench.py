@@ -67,7 +67,7 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None):
+def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None, dev_pe=None):
     """Reduced-chain CPU comparator (SURVEY.md §8d CPU side 2): `chains` chains of the oracle's
     NUTS (oracle/hmc_ref.py, float32) started from the GPU's adapted state of the first chains
     (z, U, grad, step size, diagonal mass) and the same Philox stream, so they run the timed
@@ -107,7 +107,8 @@ def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=Non
            "potential_gflops": gflops, "potential_share": stats["pot_s"] / dt,
            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
     if dev_ns is not None:
-        par = CB.compare_paths(hist, dev_ns[:chains], dev_z[:chains], atol=1e-4)
+        par = CB.compare_paths(hist, dev_ns[:chains], dev_z[:chains], atol=1e-4,
+                               dev_pe=None if dev_pe is None else dev_pe[:chains])
         ties = sum(1 for m in par["mismatches"] if m[4])
         for c, t, kind, m, tie in par["mismatches"]:
             print(f"[parity] chain {c}: first difference at timed transition {t}, closest oracle decision {kind} "
@@ -156,7 +157,7 @@ def _config_specs():
 CONFIG_WARMUP = {"c2": 100, "c3": 100, "c4": 200}
 
 
-def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds):
+def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_pe=None):
     """CPU side of a secondary config (SURVEY.md §8d CPU side 2): `cpu_chains` of the oracle's
     NUTS resumed from the GPU's adapted state of the first chains (whitened coordinates and the
     pooled whitening T, mu for dense mass; step size, diagonal mass otherwise) on the same
@@ -200,7 +201,8 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds):
                      ("; dense mass as the whitened identity-mass chain with the GPU's pooled T, mu"
                       if eng.dense else ""),
            "potential_share": stats["pot_s"] / dt, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
-    par = CB.compare_paths(hist, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model)
+    par = CB.compare_paths(hist, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model,
+                           dev_pe=None if dev_pe is None else dev_pe[:k])
     par["mismatches_at_tie"] = sum(1 for m in par["mismatches"] if m[4])
     par["mismatches"] = [list(m) for m in par["mismatches"]]
     return out, par
@@ -258,7 +260,7 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        mcmc.run(8, *sp["args"], extra_fields=("num_steps", "diverging"))
+        mcmc.run(8, *sp["args"], extra_fields=("num_steps", "diverging", "potential_energy"))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -320,7 +322,8 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
             # resume the CPU chains from the post-warmup state (the timed run moved the engine on)
             from numpyro_amd.infer.hmc import restore_state
             restore_state(eng, mcmc.post_warmup_state)
-            cb, par = cpu_baseline_config(sp, eng, key_to_seed(8), dev_ns, dev_z, cpu_seconds)
+            dev_pe = ef["potential_energy"][:k].to(torch.float64).cpu().numpy()
+            cb, par = cpu_baseline_config(sp, eng, key_to_seed(8), dev_ns, dev_z, cpu_seconds, dev_pe=dev_pe)
             r["cpu_baseline"], r["parity"] = cb, par
         out[key] = r
         del mcmc, eng, pot
@@ -398,7 +401,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    mcmc.run(args.seed + 2, Xd, yd, extra_fields=("num_steps", "diverging"))
+    mcmc.run(args.seed + 2, Xd, yd, extra_fields=("num_steps", "diverging", "potential_energy"))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -491,7 +494,8 @@ def main():
             k = min(args.cpu_chains, hi - lo)
             cb = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2), args.adapt + args.warmup, args.adapt, k,
                               args.cpu_seconds, dev_ns=ns[:k].cpu().numpy(),
-                              dev_z=site[:k].to(torch.float64).cpu().numpy())
+                              dev_z=site[:k].to(torch.float64).cpu().numpy(),
+                              dev_pe=ef["potential_energy"][:k].to(torch.float64).cpu().numpy())
             out["parity"] = cb.pop("parity")
             out["cpu_baseline"] = cb
     if args.configs != "none":

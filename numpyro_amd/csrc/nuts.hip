@@ -1557,6 +1557,68 @@ __device__ __forceinline__ void wave_sums_to_lds(const float (&v)[N], float* lds
     }
 }
 
+// A row's leaf inputs in the persistent kernel: only the first U-turn checkpoint level [imin]
+// is loaded with the row (the leaf_load arrays of all MAXD levels cost ~60 VGPRs at three rows
+// in flight); leaves with more levels (a quarter of them) add one pass per extra level
+// (persist_ckpt_levels).  Same arithmetic per row as leaf_load / leaf_store.
+struct PRow {
+  float rf, im, rs_old, rst, ro, ckr, ckrs;
+};
+
+template <bool NUTS>
+__device__ __forceinline__ void prow_load(const VecCtx& v, const Act& A, uint32_t off, PRow& x) {
+  const Arena& a = *v.a;
+  x.rf = nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+  x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
+  if constexpr (NUTS) {
+    x.rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
+    if (A.tree_chk) {
+      x.rst = nmx_at(AV(NMX_F_RSUM), off);
+      x.ro = nmx_at((A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR)), off);
+    }
+    if (A.imin <= A.imax) {
+      x.ckr = nmx_at(a.ckr + A.imin * v.ck_stride, off);
+      x.ckrs = nmx_at(a.ckrs + A.imin * v.ck_stride, off);
+    }
+  }
+}
+
+// red[0] KE, red[1 + 2 MAXD + side] tree dots; dl / dr: the dots of checkpoint level imin
+template <bool NUTS>
+__device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float seff, uint32_t off, const PRow& x,
+                                           float g, float* red, float& dl, float& dr) {
+  const Arena& a = *v.a;
+  const float es = A.dirR ? seff : -seff;
+  const float half = 0.5f * es;
+  const float r = x.rf - half * g;
+  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
+  const float im = x.im;
+  red[0] += (im * r) * r;
+  if constexpr (NUTS) {
+    const float rs = (A.k == 0) ? r : x.rs_old + r;
+    nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
+    if ((A.k & 1) == 0) {  // checkpoint update (:1040-1047); even leaves read no checkpoint
+      nmx_at(a.ckr + A.imax * v.ck_stride, off) = r;
+      nmx_at(a.ckrs + A.imax * v.ck_stride, off) = rs;
+    }
+    if (A.imin <= A.imax) {
+      const float rl = x.ckr;
+      const float rsub = (rs - x.ckrs) + rl;
+      const float rss = rsub - (rl + r) / 2.0f;  // _momentum_angle :735
+      dl += (im * rl) * rss;
+      dr += (im * r) * rss;
+    }
+    if (A.tree_chk) {
+      const float rst = x.rst + rs;
+      const float rlv = A.dirR ? x.ro : r;
+      const float rrv = A.dirR ? r : x.ro;
+      const float rss2 = rst - (rlv + rrv) / 2.0f;
+      red[1 + 2 * MAXD] += (im * rlv) * rss2;
+      red[2 + 2 * MAXD] += (im * rrv) * rss2;
+    }
+  }
+}
+
 template <bool NUTS, int NT, int B, class M>
 __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A, const M& m,
                                                   const typename M::Glob& gl, float seff, uint32_t base, float* red) {
@@ -1564,15 +1626,16 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
   const float* ZE = AV(NMX_F_Z_EVAL);
   float* GE = AV(NMX_F_G_EVAL);
   const int hi = m.hi();
+  float dl = 0.0f, dr = 0.0f;
   for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B * NT) {
-    LeafIn x[B];
+    PRow x[B];
     typename M::RowIn mi[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       const int d = d0 + q * NT;
       if (d < hi) {
         const uint32_t off = base + ((uint32_t)d << 2);
-        leaf_load<NUTS, true, false>(v, A, off, x[q]);
+        prow_load<NUTS>(v, A, off, x[q]);
         m.row_load(ZE, off, 4u, d, mi[q]);
       }
     }
@@ -1581,10 +1644,67 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
       const int d = d0 + q * NT;
       if (d < hi) {
         const uint32_t off = base + ((uint32_t)d << 2);
-        x[q].g = m.row_eval(mi[q], d, gl, red + NPART);
-        nmx_at(GE, off) = x[q].g;
-        leaf_store<NUTS, true>(v, A, seff, off, x[q], red);
+        const float g = m.row_eval(mi[q], d, gl, red + NPART);
+        nmx_at(GE, off) = g;
+        prow_store<NUTS>(v, A, seff, off, x[q], g, red, dl, dr);
       }
+    }
+  }
+  if constexpr (NUTS) {
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i)
+      if (i == A.imin && A.imin <= A.imax) {
+        red[1 + 2 * i] = dl;
+        red[2 + 2 * i] = dr;
+      }
+  }
+}
+
+// U-turn dots of checkpoint levels imin + 1 .. imax (after wave_sums_to_lds): one pass over the
+// thread's model rows per level, reloading the momentum / r_sum this leaf stored; each level's
+// wave sums go straight to its LDS entries.
+template <int NW, int NT, class M>
+__device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& A, const M& m, uint32_t base,
+                                                    float* lds) {
+  constexpr int B2 = 4;
+  const Arena& a = *v.a;
+  const float* RF = A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  const float* RS = AV(NMX_F_RSUM_SUB);
+  const float* IM = AV(NMX_F_INV_MASS);
+  const int hi = m.hi();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = A.imin + 1; i <= A.imax; ++i) {
+    const float* CK = a.ckr + i * v.ck_stride;
+    const float* CKS = a.ckrs + i * v.ck_stride;
+    float dl = 0.0f, dr = 0.0f;
+    for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B2 * NT) {
+      float r[B2], rs[B2], im[B2], rl[B2], rls[B2];
+#pragma unroll
+      for (int q = 0; q < B2; ++q) {
+        const int d = d0 + q * NT;
+        if (d < hi) {
+          const uint32_t off = base + ((uint32_t)d << 2);
+          r[q] = nmx_at(RF, off);
+          rs[q] = nmx_at(RS, off);
+          im[q] = v.unit ? 1.0f : nmx_at(IM, off);
+          rl[q] = nmx_at(CK, off);
+          rls[q] = nmx_at(CKS, off);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < B2; ++q) {
+        if (d0 + q * NT < hi) {
+          const float rsub = (rs[q] - rls[q]) + rl[q];
+          const float rss = rsub - (rl[q] + r[q]) / 2.0f;
+          dl += (im[q] * rl[q]) * rss;
+          dr += (im[q] * r[q]) * rss;
+        }
+      }
+    }
+    const float tl = wave_sum(dl), tr = wave_sum(dr);
+    if (lane == 0) {
+      lds[(1 + 2 * i) * NW + wv] = tl;
+      lds[(2 + 2 * i) * NW + wv] = tr;
     }
   }
 }
@@ -1656,8 +1776,11 @@ __device__ __forceinline__ float uni_f(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
 
+#ifndef NMX_PX_OCC
+#define NMX_PX_OCC 1  // waves per SIMD the persistent wide kernel is compiled for (A/B: 4 caps it at 128 VGPRs)
+#endif
 template <int NT, int B, class M>
-__global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
+__global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
   constexpr int NW = NT / 64;
   constexpr int NR = NPART + M::NSUM;
   __shared__ float lds[NR * NW];
@@ -1722,6 +1845,7 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
         else persist_leaf_rows<false, NT, B>(v, A, m, gl, seff, base, red);
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
+      if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT>(v, A, m, base, lds);
       PX_T(1);
       PX_ADD(0, 0, 1);
       __syncthreads();
@@ -1752,12 +1876,13 @@ __global__ __launch_bounds__(NT) void k_wide_persistent(StepArgs Pk, M m, int ma
             nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
             LeafIn x;
             x.g = gs[i];
+            // (checkpoints read inline, not preloaded: register-lean, one lane)
             if (is_nuts) {
-              leaf_load<true, true, false>(v, A, off, x);
-              leaf_store<true, true>(v, A, seff, off, x, rs);
+              leaf_load<true, false, false>(v, A, off, x);
+              leaf_store<true, false>(v, A, seff, off, x, rs);
             } else {
-              leaf_load<false, true, false>(v, A, off, x);
-              leaf_store<false, true>(v, A, seff, off, x, rs);
+              leaf_load<false, false, false>(v, A, off, x);
+              leaf_store<false, false>(v, A, seff, off, x, rs);
             }
           }
 #pragma unroll

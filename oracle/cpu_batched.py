@@ -177,14 +177,19 @@ def chains_from_state(z, grad, pe, step_size, inverse_mass, mass_sqrt, it0, seed
     return states, oracles
 
 
-def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None):
+def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, dev_pe=None):
     """Per-chain parity of oracle histories (run_chains(record=True)) with the device's
     transitions from the same state: a chain matches while its tree sizes are equal and its
     draws agree to atol + rtol |z| (`to_model` maps the oracle's coordinates to the device
     draws' first, e.g. whitened -> model space); at the first difference the oracle's closest
-    decision to a tie is reported.  Returns {chains, transitions, matched, max_abs_dz,
-    mismatches: [(chain, transition, kind, margin, is_tie)]}."""
-    matched, transitions, max_dz, mism = 0, 0, 0.0, []
+    decision to a tie is reported.  With `dev_pe` ([chains, T] potential energies of the device
+    draws) the energy noise -- the largest |U_oracle - U_device| at the draws of transitions both
+    took identically -- widens the tie bound of transition / accept decisions to 4x it (the rule
+    of tests/test_gpu_nuts.py _explain_mismatches: a transition probability moves by up to twice
+    the largest leaf-energy discrepancy, taken as twice the one seen at a draw).  Returns
+    {chains, transitions, matched, max_abs_dz, energy_noise, mismatches: [(chain, transition,
+    kind, margin, is_tie)]}."""
+    matched, transitions, max_dz, mism, noise = 0, 0, 0.0, [], 0.0
     for c, h in enumerate(hist):
         T = min(len(h), dev_num_steps.shape[1])
         transitions += T
@@ -196,11 +201,16 @@ def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None):
             dz = float(np.max(np.abs(z - ref) - rtol * np.abs(ref)))
             if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
                 bad = t
-                d = H.closest_decision(log)
-                mism.append((c, t, d[0], d[1], H.is_tie(d)))
+                mism.append((c, t, H.closest_decision(log)))
                 break
             max_dz = max(max_dz, dz)
+            if dev_pe is not None:
+                noise = max(noise, abs(float(st.potential_energy) - float(dev_pe[c, t])))
         if bad is None:
             matched += 1
+    bound = dict(H.TIE)
+    for k in ("transition", "accept"):
+        bound[k] = max(bound[k], 4.0 * noise)
+    out = [(c, t, k, m, bool(k in bound and m <= bound[k])) for c, t, (k, m) in mism]
     return {"chains": len(hist), "transitions": transitions, "matched": matched, "max_abs_dz": max_dz,
-            "mismatches": mism}
+            "energy_noise": noise if dev_pe is not None else None, "mismatches": out}

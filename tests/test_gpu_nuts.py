@@ -227,18 +227,21 @@ def test_covtype_full_size_nuts_matches_oracle(device):
     mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=W, num_samples=T, num_chains=C)
     mcmc.warmup(seed, Xd, yd)
     st = mcmc.post_warmup_state
-    mcmc.run(seed + 1, Xd, yd, extra_fields=("num_steps",))
+    mcmc.run(seed + 1, Xd, yd, extra_fields=("num_steps", "potential_energy"))
     ns = mcmc.get_extra_fields(group_by_chain=True)["num_steps"].cpu().numpy()
+    pe = mcmc.get_extra_fields(group_by_chain=True)["potential_energy"].to(torch.float64).cpu().numpy()
     z = mcmc.get_samples(group_by_chain=True)["coefs"].to(torch.float64).cpu().numpy()
     cols = lambda t: t.detach().cpu().numpy()  # noqa: E731
     states, oracles = CB.chains_from_state(
         cols(st.z["coefs"]), cols(st.z_grad), cols(st.potential_energy), cols(st.adapt_state.step_size),
         cols(st.adapt_state.inverse_mass_matrix), cols(st.adapt_state.mass_matrix_sqrt), W, key_to_seed(seed + 1), W)
     _, hist, evals, _ = CB.run_chains(CB.LogRegBatch(X, y), states, oracles, T, record=True)
-    par = CB.compare_paths(hist, ns, z, atol=1e-4)
+    par = CB.compare_paths(hist, ns, z, atol=1e-4, dev_pe=pe)
     print(f"[covtype 581012x55] {par['matched']}/{C} chains reproduce the device's {T} transitions "
-          f"({evals} oracle leapfrogs; max |dz| on matched paths {par['max_abs_dz']:.2e})")
-    _explain_mismatches([(c, t, (k, m)) for c, t, k, m, _ in par["mismatches"]], "covtype full size")
+          f"({evals} oracle leapfrogs; max |dz| on matched paths {par['max_abs_dz']:.2e}, "
+          f"|U_dev - U_oracle| {par['energy_noise']:.2e})")
+    _explain_mismatches([(c, t, (k, m)) for c, t, k, m, _ in par["mismatches"]], "covtype full size",
+                        energy_noise=par["energy_noise"])
     assert par["matched"] >= C - 1
 
 
