@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
     // one row per round with the row's checkpoints loaded ahead: 114 VGPRs, 4 waves per SIMD
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
 #ifndef NMX_PX_B
-#define NMX_PX_B 3  // rows per thread in flight in the persistent wide kernel (2: SV -2.5%, funnel -4%)
+#define NMX_PX_B 2  // rows per thread in flight in the persistent wide kernel (profiles/r03/ab_persistent_occ.txt)
 #endif
 #ifndef NMX_V1_ROWS
 #define NMX_V1_ROWS 1
@@ -1777,7 +1777,7 @@ __device__ __forceinline__ float uni_f(float x) {
 }
 
 #ifndef NMX_PX_OCC
-#define NMX_PX_OCC 1  // waves per SIMD the persistent wide kernel is compiled for (A/B: 4 caps it at 128 VGPRs)
+#define NMX_PX_OCC 4  // waves per SIMD the kernel is compiled for: <= 128 VGPRs (3 waves: SV 8192 20.0M vs 24.2M)
 #endif
 template <int NT, int B, class M>
 __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
