@@ -53,6 +53,8 @@ def parse():
                         "dense, c3 BNN dense, c4 stochastic volatility; 'none' skips); c2/c3 are one-GPU configs "
                         "and run at --gpus 1 only, c4 shards its 8192 chains over the ranks")
     p.add_argument("--lib", default=None, help="(experiments) load this build of the library instead")
+    p.add_argument("--chain-groups", type=int, default=None,
+                   help="(experiments) chain groups on their own streams (Engine.chain_groups)")
     return p.parse_args()
 
 
@@ -246,13 +248,13 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
         eng = mcmc._engine
         pot = eng.potential
         orig_eval, evs = pot.evaluate, []
-        stream = torch.cuda.current_stream()
 
-        def timed_eval(ev, s, _orig=orig_eval):
+        def timed_eval(ev, s, *rest, _orig=orig_eval):
+            st = _ext_stream(s)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            _orig(ev, s)
-            b.record(stream)
+            a.record(st)
+            _orig(ev, s, *rest)
+            b.record(st)
             evs.append((a, b))
 
         pot.evaluate = timed_eval
@@ -335,6 +337,18 @@ def _identity(z):
     return z
 
 
+_STREAMS = {}
+
+
+def _ext_stream(s):
+    """torch handle of a raw hipStream_t (the engine's launch streams) for recording events."""
+    import torch
+
+    if s not in _STREAMS:
+        _STREAMS[s] = torch.cuda.ExternalStream(s)
+    return _STREAMS[s]
+
+
 def main():
     t_start = time.perf_counter()
     args = parse()
@@ -346,6 +360,10 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.chain_groups is not None:
+        from numpyro_amd.engine import Engine
+
+        Engine.chain_groups = args.chain_groups
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -382,17 +400,18 @@ def main():
     mcmc.num_samples = args.steps
     eng = mcmc._engine
     pot = eng.potential
-    # time the potential launches inside the timed region with events on its stream
-    stream = torch.cuda.current_stream()
+    # time the potential launches inside the timed region with events on the stream each is
+    # launched on (chain groups use one stream each)
     evs = []
     orig_eval = pot.evaluate
 
-    def timed_eval(ev, s):
+    def timed_eval(ev, s, *rest):
+        st = _ext_stream(s)
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        orig_eval(ev, s)
-        b.record(stream)
+        a.record(st)
+        orig_eval(ev, s, *rest)
+        b.record(st)
         evs.append((a, b))
 
     pot.evaluate = timed_eval
@@ -469,7 +488,8 @@ def main():
                        "num_chains": args.chains, "rows": args.rows, "dim": int(X.shape[1]),
                        "adapt_transitions": args.adapt, "design": args.design,
                        "parallelism": f"chains sharded {world}-way (no data-path collective)",
-                       "schedule": "lockstep" if args.sync_chains else "per-chain async"},
+                       "schedule": "lockstep" if args.sync_chains else "per-chain async",
+                       "chain_groups": eng._groups()},
             "useful_leapfrogs": useful,
             "mean_tree_size": useful / (args.chains * args.steps),
             "divergent_frac": divergent / (args.chains * args.steps),

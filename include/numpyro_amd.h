@@ -87,8 +87,9 @@ enum nmx_field {
   NMX_F_CKPT_R, NMX_F_CKPT_RSUM,
   /* compacted list of LEAF chains for the next potential launch, int32 [2][ldc] by parity */
   NMX_F_ACTIVE_IDX,
-  /* device counters int32[16]: [0] chains DONE, [1] chains NEEDINIT, [2],[3] active-list
-   * lengths for parity 0/1, [4..] reserved */
+  /* device counters int32[16]: [0] chains DONE, [1] chains NEEDINIT, [2 + 2 g + parity]
+   * active-list lengths of chain group g (nmx_nuts_config.num_groups), [10 + g] chains of
+   * group g DONE (num_groups > 1), [14..] reserved */
   NMX_F_COUNTERS,
   /* sync_chains: int32[iter_capacity] #chains that finished transition iter_begin + i */
   NMX_F_FINISHED,
@@ -143,6 +144,15 @@ typedef struct nmx_nuts_config {
   int32_t layout;                /* nmx_layout of the arena's vector fields: CHAIN_MINOR for
                                     every entry point but nmx_nuts_run_wide, which needs
                                     CHAIN_ROWS (reset / init / resume take either) */
+  int32_t num_groups;            /* chain groups of the launched fused step (dim <= 256), 0/1:
+                                    one group.  Group g holds chains [g G, min((g + 1) G, C)),
+                                    G = ceil(C / num_groups), num_groups in {1, 2, 4}; each
+                                    group has its own pair of compacted lists (entries
+                                    [g G, ...) of each parity list, lengths counters[2 + 2 g +
+                                    parity]), so groups step and evaluate independently, e.g.
+                                    on two streams that overlap one group's step with the
+                                    other's potential.  A chain's results do not depend on it. */
+  int32_t group;                 /* the group nmx_nuts_step advances (0 .. num_groups - 1) */
 } nmx_nuts_config;
 
 /* D-slices of the wide step (0 when dim is small enough for the fused one-kernel step).

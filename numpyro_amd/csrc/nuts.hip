@@ -112,6 +112,22 @@ Arena make_arena(void* base, int ldc, int D, int MD, int iter_cap) {
   return a;
 }
 
+// chain groups of the launched fused step (nmx_nuts_config.num_groups)
+__host__ __device__ __forceinline__ int group_count(const nmx_nuts_config& cfg) {
+  return cfg.num_groups > 1 ? cfg.num_groups : 1;
+}
+__host__ __device__ __forceinline__ int group_size(const nmx_nuts_config& cfg) {
+  const int g = group_count(cfg);
+  return (cfg.num_chains + g - 1) / g;
+}
+__host__ __device__ __forceinline__ int group_first(const nmx_nuts_config& cfg) {
+  return group_count(cfg) > 1 ? cfg.group * group_size(cfg) : 0;
+}
+// index of the group's list-length counter of a parity
+__host__ __device__ __forceinline__ int list_counter(const nmx_nuts_config& cfg, int parity) {
+  return 2 + 2 * (group_count(cfg) > 1 ? cfg.group : 0) + parity;
+}
+
 struct StepArgs {
   Arena a;
   nmx_nuts_config cfg;
@@ -537,7 +553,10 @@ __device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena
                                          const ChainScalars& S, const Act& A, bool list = true) {
   if (valid) {
     if (S.phase != ph_in || A.leaf || A.start_iter || A.iter_done) store_scalars(a, c, S);
-    if (A.fin_done) atomicAdd(&a.counters[0], 1);
+    if (A.fin_done) {
+      atomicAdd(&a.counters[0], 1);
+      if (group_count(cfg) > 1) atomicAdd(&a.counters[10 + cfg.group], 1);  // the group's own count
+    }
     if (A.fin_wait) {
       const int fs = A.fin_t - cfg.iter_begin;
       if (fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
@@ -552,12 +571,13 @@ __device__ __forceinline__ void end_step(const nmx_nuts_config& cfg, const Arena
   const uint64_t m = __ballot(pend);
   if (m) {
     int base = 0;
-    if (lane == __builtin_ctzll(m)) base = atomicAdd(&a.counters[2 + cfg.parity], __builtin_popcountll(m));
+    if (lane == __builtin_ctzll(m))
+      base = atomicAdd(&a.counters[list_counter(cfg, cfg.parity)], __builtin_popcountll(m));
     base = __shfl(base, __builtin_ctzll(m));
     if (pend) {
       const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
-      NMX_DCHECK(pos < cfg.num_chains);
-      a.active_idx[(size_t)cfg.parity * cfg.ldc + pos] = c;
+      NMX_DCHECK(pos < group_size(cfg));
+      a.active_idx[(size_t)cfg.parity * cfg.ldc + group_first(cfg) + pos] = c;
     }
   }
 }
@@ -926,16 +946,16 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
   const int wv = threadIdx.x >> 6;
   const int cl = lane % CPW;
   const int vw = wv * SUBS + lane / CPW;
-  const int c = blockIdx.x * CPW + cl;
+  const int c = group_first(cfg) + blockIdx.x * CPW + cl;
   const int ldc = cfg.ldc;
   const int D = cfg.dim;
-  const bool valid = c < cfg.num_chains;
+  const bool valid = c < cfg.num_chains && c < group_first(cfg) + group_size(cfg);
   const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   const uint64_t seed = cfg.seed;
   // active list [parity ^ 1] was consumed by the previous potential launch; clear it for
   // the next step (which appends to it).  List [parity] was cleared by the previous step.
-  if (LIST && blockIdx.x == 0 && threadIdx.x == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+  if (LIST && blockIdx.x == 0 && threadIdx.x == 0) a.counters[list_counter(cfg, cfg.parity ^ 1)] = 0;
 
   ChainScalars S;
   Act A;
@@ -2198,6 +2218,9 @@ int validate(const nmx_nuts_config* cfg) {
     return nmx_fail(NMX_ERR_INVALID, "cfg.ldc must be round_up(num_chains, 64) = %d", ldc_of(cfg->num_chains));
   if (cfg->layout != NMX_LAYOUT_CHAIN_MINOR && cfg->layout != NMX_LAYOUT_CHAIN_ROWS)
     return nmx_fail(NMX_ERR_INVALID, "layout must be NMX_LAYOUT_CHAIN_MINOR(0) or NMX_LAYOUT_CHAIN_ROWS(1)");
+  if (cfg->num_groups < 0 || cfg->num_groups == 3 || cfg->num_groups > 4)
+    return nmx_fail(NMX_ERR_INVALID, "num_groups must be 0, 1, 2 or 4");
+  if (cfg->group < 0 || cfg->group >= group_count(*cfg)) return nmx_fail(NMX_ERR_INVALID, "group out of range");
   return NMX_OK;
 }
 
@@ -2280,6 +2303,7 @@ extern "C" int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_heuristic_begin"))) return st;
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_begin: one chain group only");
   Arena a = arena_of(cfg, arena);
   hipLaunchKernelGGL(k_heur_begin, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a, *cfg);
   return nmx_check_launch("k_heur_begin");
@@ -2289,6 +2313,7 @@ extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, vo
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_heuristic_propose"))) return st;
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_propose: one chain group only");
   Arena a = arena_of(cfg, arena);
   if (hipMemsetAsync(a.counters + 2, 0, 4, (hipStream_t)stream) != hipSuccess)
     return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
@@ -2301,6 +2326,7 @@ extern "C" int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_heuristic_finish"))) return st;
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_finish: one chain group only");
   Arena a = arena_of(cfg, arena);
   if (hipMemsetAsync(a.counters + 1, 0, 4, (hipStream_t)stream) != hipSuccess)
     return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
@@ -2324,6 +2350,7 @@ extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_nuts_run_small"))) return st;
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_nuts_run_small: one chain group only");
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
@@ -2372,6 +2399,8 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
   hipStream_t s = (hipStream_t)stream;
   if (cfg->parity != 0 && cfg->parity != 1) return nmx_fail(NMX_ERR_INVALID, "parity must be 0 or 1");
   const int ns = num_slices(cfg->dim);
+  if (ns > 0 && group_count(*cfg) > 1)
+    return nmx_fail(NMX_ERR_INVALID, "chain groups: the fused step only (dim <= 256)");
   if (ns > 0) {
     WideArgs w{args, ns, slice_width(cfg->dim)};
     hipLaunchKernelGGL(k_wide_v1, dim3(grid, ns), dim3(64 * WIDE_WAVES), 0, s, w);
@@ -2380,10 +2409,12 @@ extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* sam
     hipLaunchKernelGGL(k_wide_v2, dim3(grid, ns), dim3(64 * V2_WAVES), 0, s, w);
     return nmx_check_launch("k_nuts_step (wide)");
   }
+  // the blocks cover the launch's chain group (all chains with one group)
+  const int gchains = group_count(*cfg) > 1 ? group_size(*cfg) : cfg->ldc;
   if (tpc_for_dim(cfg->dim) == 1)
-    hipLaunchKernelGGL((k_nuts_step<1, SMALL_CPW>), dim3(cfg->ldc / SMALL_CPW), dim3(64), 0, s, args);
+    hipLaunchKernelGGL((k_nuts_step<1, SMALL_CPW>), dim3((gchains + SMALL_CPW - 1) / SMALL_CPW), dim3(64), 0, s, args);
   else
-    hipLaunchKernelGGL((k_nuts_step<8, STEP_CPW>), dim3(cfg->ldc / STEP_CPW), dim3(512), 0, s, args);
+    hipLaunchKernelGGL((k_nuts_step<8, STEP_CPW>), dim3((gchains + STEP_CPW - 1) / STEP_CPW), dim3(512), 0, s, args);
   return nmx_check_launch("k_nuts_step");
 }
 
@@ -2414,6 +2445,7 @@ extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena,
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_nuts_step_wide_model"))) return st;
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_nuts_step_wide_model: one chain group only");
   if (!arena || !workspace) return nmx_fail(NMX_ERR_INVALID, "arena / workspace is NULL");
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
@@ -2487,6 +2519,7 @@ extern "C" int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float*
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
   if (cfg->layout != NMX_LAYOUT_CHAIN_ROWS)
     return nmx_fail(NMX_ERR_INVALID, "run_wide needs the chain-row arena layout (NMX_LAYOUT_CHAIN_ROWS)");
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "run_wide: one chain group only");
   if (cfg->sync_chains)
     return nmx_fail(NMX_ERR_INVALID, "run_wide: per-chain async only (lockstep: one launch per transition)");
   // samples may be NULL: the per-transition fields alone are collected

@@ -92,6 +92,10 @@ class Engine:
     # D-split models with diagonal mass: the persistent per-chain schedule (nmx_nuts_run_wide,
     # chain-row arena layout); False: the launched wide schedules above
     wide_persistent = True
+    # launched fused step (dim <= 256): chain groups stepped on their own streams so that one
+    # group's latency-bound step and potential tail overlap another group's potential
+    # (nmx_nuts_config.num_groups; 1: one stream)
+    chain_groups = 2
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
@@ -145,6 +149,7 @@ class Engine:
         self.generation = None
         self._pool = None  # dense pooled adaptation: (window, PooledCovariance) across run() calls
         self._wide_ws = None  # nmx_nuts_step_wide_model workspace (zero-filled once)
+        self._side_streams = []  # chain groups 1.. (created on first use)
         self._mass_cache = None  # dense: (whitening version, HMCAdaptState mass fields)
         # False: collected draws stay unconstrained (MCMC(postprocess_fn=...) maps them itself)
         self.constrain_samples = True
@@ -547,6 +552,9 @@ class Engine:
                     return launches
                 if max_launches is not None and launches * max_steps >= max_launches:
                     raise RuntimeError(f"chains did not finish within {max_launches} leapfrog steps")
+        groups = self._groups()
+        if groups > 1:
+            return self._run_groups(groups, samples, fields, tr, poll_every, s, max_launches)
         done = self.view("counters")[0:1]
         host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         ev = torch.cuda.Event()
@@ -593,6 +601,86 @@ class Engine:
             pending = True
             if max_launches is not None and launches >= max_launches:
                 raise RuntimeError(f"chains did not finish within {max_launches} leapfrog launches")
+        return launches
+
+    def _groups(self):
+        """Chain groups of the launched fused step (1: none): dim <= 256 models whose potential
+        keeps a workspace per concurrently evaluated group, at >= 128 chains per group."""
+        G = int(self.chain_groups)
+        if G <= 1 or self.dense or self.crow or lib().nmx_nuts_num_slices(self.D) > 0:
+            return 1
+        if getattr(self.potential, "slots", 1) < G or self.C < 128 * G:
+            return 1
+        return G
+
+    def _run_groups(self, G, samples, fields, tr, poll_every, s, max_launches):
+        """The launched loop with chain groups (nmx_nuts_config.num_groups): group g's potential
+        and step launches go to stream g (the caller's stream for g = 0), each group with its
+        own compacted lists and DONE count, so a group's latency-bound step, finalize and run
+        tail overlap the other groups' potential.  A chain's computation does not depend on its
+        group: draws are bitwise those of the one-stream loop."""
+        main = torch.cuda.ExternalStream(s, device=self.device)
+        while len(self._side_streams) < G - 1:
+            self._side_streams.append(torch.cuda.Stream(device=self.device))
+        streams = [main] + self._side_streams[:G - 1]
+        raw = [s] + [int(st.cuda_stream) for st in streams[1:]]
+        start = torch.cuda.Event()
+        start.record(main)
+        for st in streams[1:]:
+            st.wait_event(start)  # after the resume / setup issued on the caller's stream
+        gsz = (self.C + G - 1) // G
+        sizes = [max(0, min(gsz, self.C - g * gsz)) for g in range(G)]
+        step = lib().nmx_nuts_step
+        arena = ptr(self.arena)
+        sp, fp, tp = ptr(samples) if samples.shape[0] else None, ptr(fields), ptr(tr)
+        idx, cnt = ptr(self.view("active_idx")), ptr(self.view("counters"))
+        z, gr, pe, ph = (ptr(self.view(n)) for n in ("z_eval", "g_eval", "pe_eval", "phase"))
+        counters = self.view("counters")
+        cfgs, lists, par = [], [], [0] * G
+        for g in range(G):
+            c = NutsConfig.from_buffer_copy(self.cfg)
+            c.num_groups, c.group, c.parity = G, g, 0
+            cfgs.append(c)
+            lists.append([EvalBatch(z=z, grad=gr, pe=pe, phase=ph, active_idx=idx + 4 * (p * self.ldc + g * gsz),
+                                    active_count=cnt + 4 * (2 + 2 * g + p), num_chains=max(sizes[g], 1),
+                                    ldc=self.ldc) for p in (0, 1)])
+            check(step(ctypes.byref(c), arena, sp, fp, tp, raw[g]), "nmx_nuts_step")
+        evaluate = self.potential.evaluate
+        hosts = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(G)]
+        evs = [torch.cuda.Event() for _ in range(G)]
+        pending, live = [False] * G, [sizes[g] > 0 for g in range(G)]
+        launches = 0
+        while any(live):
+            for _ in range(poll_every):
+                for g in range(G):
+                    if not live[g]:
+                        continue
+                    evaluate(lists[g][par[g]], raw[g], g)
+                    par[g] ^= 1
+                    cfgs[g].parity = par[g]
+                    check(step(ctypes.byref(cfgs[g]), arena, sp, fp, tp, raw[g]), "nmx_nuts_step")
+            launches += poll_every
+            for g in range(G):
+                if not live[g]:
+                    continue
+                if pending[g]:
+                    evs[g].synchronize()
+                    done_g = int(hosts[g][0])
+                    if done_g >= sizes[g]:
+                        live[g] = False
+                        continue
+                    for b in lists[g]:  # finished chains never re-enter the group's lists
+                        b.num_chains = sizes[g] - done_g
+                with torch.cuda.stream(streams[g]):
+                    hosts[g].copy_(counters[10 + g:11 + g], non_blocking=True)
+                    evs[g].record(streams[g])
+                pending[g] = True
+            if max_launches is not None and launches >= max_launches:
+                raise RuntimeError(f"chains did not finish within {max_launches} leapfrog launches")
+        for st in streams[1:]:  # the caller's stream continues after every group's work
+            j = torch.cuda.Event()
+            j.record(st)
+            main.wait_event(j)
         return launches
 
     def _run_wide_persistent(self, a, b, seed, cstart, thinning, S, samples, fields, s, max_launches):

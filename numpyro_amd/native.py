@@ -75,7 +75,7 @@ class NutsConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64), ("chain_offset", ctypes.c_int64),
         ("collect_start", ctypes.c_int32), ("collect_thinning", ctypes.c_int32),
         ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32), ("parity", ctypes.c_int32),
-        ("layout", ctypes.c_int32),
+        ("layout", ctypes.c_int32), ("num_groups", ctypes.c_int32), ("group", ctypes.c_int32),
     ]
 
 

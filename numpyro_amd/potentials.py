@@ -142,6 +142,9 @@ class LogisticRegression(Potential):
         self.sites = [("coefs", (self.dim,), REAL)]
         self.packed = None
 
+    # workspaces: one per chain group evaluated concurrently (Engine chain groups, one stream each)
+    slots = 4
+
     def _bind(self, C, ldc, device):
         if self.packed is None or self.packed.device != device:
             X = _dev(self.X_in, device)
@@ -154,10 +157,16 @@ class LogisticRegression(Potential):
             del X, y
         wb = lib().nmx_logreg_workspace_bytes(self.N, self.dim, C)
         self.workspace = torch.empty(wb, dtype=torch.uint8, device=device)
+        self._more_ws = []  # slots 1.. (allocated on first use)
 
-    def evaluate(self, ev, stream):
+    def evaluate(self, ev, stream, slot=0):
+        ws = self.workspace
+        if slot:
+            while len(self._more_ws) < slot:
+                self._more_ws.append(torch.empty_like(self.workspace))
+            ws = self._more_ws[slot - 1]
         check(lib().nmx_logreg_pe_grad(ptr(self.packed), self.N, self.dim, ctypes.byref(ev),
-                                       ptr(self.workspace), stream), "nmx_logreg_pe_grad")
+                                       ptr(ws), stream), "nmx_logreg_pe_grad")
 
     def flops_per_eval(self, num_chains):
         """Algorithmic FLOPs of one evaluation (two GEMMs): 4 N D C."""

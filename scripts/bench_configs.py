@@ -78,15 +78,16 @@ class Timed:
     def __init__(self, pot):
         self.pot, self.orig, self.events = pot, pot.evaluate, []
         self.on = False
+        self.streams = {}
         pot.evaluate = self
 
-    def __call__(self, ev, s):
+    def __call__(self, ev, s, *rest):
         if not self.on:
-            return self.orig(ev, s)
-        st = torch.cuda.current_stream()  # the stream `s` belongs to (native.stream_ptr())
+            return self.orig(ev, s, *rest)
+        st = self.streams.setdefault(s, torch.cuda.ExternalStream(s))  # the launch stream
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
-        self.orig(ev, s)
+        self.orig(ev, s, *rest)
         b.record(st)
         self.events.append((a, b))
 

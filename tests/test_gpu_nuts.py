@@ -782,3 +782,24 @@ def test_frontend_models_run_like_fused_models(device, which):
     for k in sa:
         np.testing.assert_array_equal(sa[k].cpu().numpy(), sb[k].cpu().numpy(), err_msg=k)
     np.testing.assert_array_equal(na.cpu().numpy(), nb.cpu().numpy())
+
+
+@pytest.mark.parametrize("groups,C,sync", [(2, 256, False), (4, 512, False), (2, 256, True)])
+def test_chain_groups_are_bitwise_the_one_stream_loop(device, groups, C, sync, monkeypatch):
+    """Chain groups (nmx_nuts_config.num_groups): the launched fused step and the covtype
+    potential per group on its own stream, each group with its own compacted lists and DONE
+    count.  A chain's computation does not depend on its group or on how the streams
+    interleave: draws, tree sizes and energies equal the one-stream loop bitwise."""
+    from numpyro_amd.engine import Engine
+
+    X, y = datasets.covtype_synthetic(n_rows=4000, seed=1)
+    out = {}
+    for G in (1, groups):
+        monkeypatch.setattr(Engine, "chain_groups", G)
+        mcmc, _ = _run_engine((X, y), P.logistic_regression, C, 30, 12, 3, sync=sync)
+        assert mcmc._engine._groups() == G
+        ef = mcmc.get_extra_fields(True)
+        out[G] = (mcmc.get_samples(True)["coefs"].cpu().numpy(), ef["num_steps"].cpu().numpy(),
+                  ef["potential_energy"].cpu().numpy())
+    for a, b in zip(out[1], out[groups]):
+        np.testing.assert_array_equal(a, b)
