@@ -344,6 +344,9 @@ def _ext_stream(s):
     """torch handle of a raw hipStream_t (the engine's launch streams) for recording events."""
     import torch
 
+    cur = torch.cuda.current_stream()
+    if s == cur.cuda_stream:  # (the null stream is 0: an ExternalStream of it records elsewhere)
+        return cur
     if s not in _STREAMS:
         _STREAMS[s] = torch.cuda.ExternalStream(s)
     return _STREAMS[s]

@@ -94,8 +94,10 @@ class Engine:
     wide_persistent = True
     # launched fused step (dim <= 256): chain groups stepped on their own streams so that one
     # group's latency-bound step and potential tail overlap another group's potential
-    # (nmx_nuts_config.num_groups; 1: one stream)
-    chain_groups = 2
+    # (nmx_nuts_config.num_groups; 1: one stream).  Measured slower for covtype (each group's
+    # potential streams the whole X: 512 chains 0.745M / 0.673M leapfrog/s at 2 / 4 groups vs
+    # 0.875M, 4096 chains 1.322M / 1.263M vs 1.369M; profiles/r03/ab_chain_groups.txt): off.
+    chain_groups = 1
 
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):

@@ -84,7 +84,9 @@ class Timed:
     def __call__(self, ev, s, *rest):
         if not self.on:
             return self.orig(ev, s, *rest)
-        st = self.streams.setdefault(s, torch.cuda.ExternalStream(s))  # the launch stream
+        st = torch.cuda.current_stream()  # the launch stream (its own for chain groups > 0)
+        if s != st.cuda_stream:
+            st = self.streams.setdefault(s, torch.cuda.ExternalStream(s))
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
         self.orig(ev, s, *rest)
