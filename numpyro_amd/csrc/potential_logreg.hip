@@ -771,7 +771,10 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
 // Launches over at most this many 128-chain groups (a NUTS run's tail: one workgroup per split
 // and CU) run the role-split form k_logreg_x3_roles (bitwise equal): 0.083 vs 0.105 ms per
 // evaluation at 16-64 chains, incl. the finalize.
-constexpr int X3_TAIL_TILES = 2;
+#ifndef NMX_X3_TAIL_TILES
+#define NMX_X3_TAIL_TILES 2
+#endif
+constexpr int X3_TAIL_TILES = NMX_X3_TAIL_TILES;
 
 int check_ev(const nmx_eval_batch* ev) {
   if (!ev || !ev->z || !ev->grad || !ev->pe) return nmx_fail(NMX_ERR_INVALID, "eval batch has NULL pointers");
