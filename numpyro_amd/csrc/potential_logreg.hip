@@ -304,9 +304,132 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
   }
 }
 
+// GEMM2's X^T operand of a tile taken from its GEMM1 image (the A pieces: lane r + 32 h of piece
+// (plane, kb) holds X[r][16 kb + 8 h .. + 7]) with gfx950's transposed LDS read
+// ds_read_b64_tr_b16 (cdna_hip_programming.md T10: lane 4q + p of a 16-lane group supplies the
+// address of row q, columns 4p .. 4p + 3 of a 4 x 16 block; lane i receives column i), so the
+// B pieces (X^T in fragment order, the other half of the packed tile) need not be streamed.
+// Fragment (plane, dt, s) of lane L = (d = L & 31, h = L >> 5) is X[16 s + 8 jh + 4 h + q][32 dt +
+// d] for j = 4 jh + q: exactly the B piece's bytes, so the products are bitwise the same.
+// The reads are inline asm (a compiler-visible LDS read after the ring's DMA issue gets a
+// vmcnt(0) wait that would drain the prefetch, as for x3_labels); x3_tr_wait before use.
+template <int KB, int DT>
+__device__ __forceinline__ void x3_gemm2_tr_load(const char* aslot, bf16x8 (&fb)[3][DT][2]) {
+  static_assert(KB >= 2 * DT, "the GEMM1 image must cover GEMM2's 32 DT columns");
+  const int L = threadIdx.x & 63;
+  const int p = L & 3, q = (L >> 2) & 3, g1 = (L >> 4) & 1, h = L >> 5;
+  const unsigned base = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)aslot) + g1 * 1024 +
+                        (q + 32 * (p >> 1) + 4 * h) * 16 + 8 * (p & 1);
+#pragma unroll
+  for (int plane = 0; plane < 3; ++plane)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        typedef short s4 __attribute__((ext_vector_type(4)));
+        s4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                     : "=&v"(lo), "=&v"(hi)
+                     : "v"(base), "i"((plane * KB + 2 * dt) * 1024 + (16 * sidx) * 16),
+                       "i"((plane * KB + 2 * dt) * 1024 + (16 * sidx + 8) * 16));
+        const s4 lh[2] = {lo, hi};
+        bf16x8 f;
+        __builtin_memcpy(&f, lh, 16);
+        fb[plane][dt][sidx] = f;
+      }
+}
+template <int DT>
+__device__ __forceinline__ void x3_tr_wait(bf16x8 (&fb)[3][DT][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int plane = 0; plane < 3; ++plane)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) asm volatile("" : "+v"(fb[plane][dt][sidx]));
+}
+// x3_gemm2 with the operands read just in time (three fragments per (s, dt), 12 VGPRs instead
+// of 48 held across GEMM1: the main kernel's register budget)
+template <int KB, int DT>
+__device__ __forceinline__ void x3_gemm2_tr(const char* aslot, const float (&res)[16], f32x16 (&g)[DT]) {
+  static_assert(KB >= 2 * DT, "the GEMM1 image must cover GEMM2's 32 DT columns");
+  const int L = threadIdx.x & 63;
+  const int p = L & 3, q = (L >> 2) & 3, g1 = (L >> 4) & 1, h = L >> 5;
+  const unsigned base = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)aslot) + g1 * 1024 +
+                        (q + 32 * (p >> 1) + 4 * h) * 16 + 8 * (p & 1);
+#pragma unroll
+  for (int sidx = 0; sidx < 2; ++sidx) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = res[8 * sidx + j];
+    bf16x8 r1, r2, r3;
+    split3(v, r1, r2, r3);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      s4 t[6];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %6 offset:%7\n\tds_read_b64_tr_b16 %1, %6 offset:%8\n\t"
+          "ds_read_b64_tr_b16 %2, %6 offset:%9\n\tds_read_b64_tr_b16 %3, %6 offset:%10\n\t"
+          "ds_read_b64_tr_b16 %4, %6 offset:%11\n\tds_read_b64_tr_b16 %5, %6 offset:%12\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5])
+          : "v"(base), "i"((0 * KB + 2 * dt) * 1024 + 16 * sidx * 16), "i"((0 * KB + 2 * dt) * 1024 + (16 * sidx + 8) * 16),
+            "i"((1 * KB + 2 * dt) * 1024 + 16 * sidx * 16), "i"((1 * KB + 2 * dt) * 1024 + (16 * sidx + 8) * 16),
+            "i"((2 * KB + 2 * dt) * 1024 + 16 * sidx * 16), "i"((2 * KB + 2 * dt) * 1024 + (16 * sidx + 8) * 16));
+      bf16x8 b1, b2, b3;
+      __builtin_memcpy(&b1, &t[0], 16);
+      __builtin_memcpy(&b2, &t[2], 16);
+      __builtin_memcpy(&b3, &t[4], 16);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
+    }
+  }
+}
+
+// x3_gemm2 on register operands (same products in the same order)
+template <int DT>
+__device__ __forceinline__ void x3_gemm2_regs(const bf16x8 (&fb)[3][DT][2], const float (&res)[16],
+                                              f32x16 (&g)[DT]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = res[8 * s + j];
+    bf16x8 r1, r2, r3;
+    split3(v, r1, r2, r3);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16x8 b1 = fb[0][dt][s], b2 = fb[1][dt][s], b3 = fb[2][dt][s];
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
+    }
+  }
+}
+
 // Software-pipelined: GEMM1 of tile k+1 is issued beside the epilogue of tile k (they are
 // independent), then GEMM2 of tile k.  SCHED 0 adds the igrouplp placement hints below.
 //
+#ifndef NMX_X3_TR
+#define NMX_X3_TR 0
+#endif
+// the main kernel's GEMM2 operand from transposed reads of the GEMM1 image (needs KB >= 2 DT)
+template <int KB, int DT>
+constexpr bool x3_tr() { return NMX_X3_TR && KB >= 2 * DT; }
+template <int KB, int DT>
+inline size_t x3_lds_bytes() {
+  constexpr int NA = 3 * KB, NP = 3 * KB + 6 * DT + 1;
+  return x3_tr<KB, DT>() ? (size_t)(3 * NA + 2) * 1024 : (size_t)2 * NP * 1024;
+}
+
 template <int KB, int DT, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
                                         nmx_eval_batch ev, float* __restrict__ gpart,
@@ -359,11 +482,17 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
     // Split rings: GEMM1 reads only the A part of a tile (pieces < 3 KB), GEMM2 and the labels
     // only the B part.  Iteration k reads A(k+1) and B(k) while A(k+2) and B(k+1) fill, so two
     // slots of each part suffice: 2 x (12 + 13) KB for covtype, three workgroups per CU.
+    // TR (x3_tr<KB, DT>()): GEMM2 reads X^T from the GEMM1 image by transposed LDS reads, so
+    // only the A pieces and the labels are streamed (half the bytes); the A ring then keeps
+    // tile k for GEMM2(k) beside tile k+1 (GEMM1) and tile k+2 landing: 3 slots, and B slots
+    // hold the label piece only (3 x 12 + 2 x 1 KB)
     constexpr int NA = 3 * KB, NBP = NP - NA;
+    constexpr bool TR = x3_tr<KB, DT>();
+    constexpr int ASL = TR ? 3 : 2, BSZ = TR ? 1 : NBP;
     char* aring = lds;
-    char* bring = lds + 2 * NA * 1024;
+    char* bring = lds + ASL * NA * 1024;
     auto issue_a = [&](int k) {
-      char* dst = aring + (k & 1) * NA * 1024;
+      char* dst = aring + (k % ASL) * NA * 1024;
 #pragma unroll
       for (int j = 0; j < (NA + 3) / 4; ++j) {
         const int i = wu + 4 * j;
@@ -373,13 +502,19 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
       }
     };
     auto issue_b = [&](int k) {
-      char* dst = bring + (k & 1) * NBP * 1024;
+      char* dst = bring + (k & 1) * BSZ * 1024;
+      if constexpr (TR) {
+        if (wu == 3)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)dst, 16, lane * 16,
+                                                   (unsigned)((k * NP + NP - 1) * 1024), 0, 0);
+      } else {
 #pragma unroll
-      for (int j = 0; j < (NBP + 3) / 4; ++j) {
-        const int i = wu + 4 * j;
-        if (i < NBP)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
-                                                   lane * 16, (unsigned)((k * NP + NA + i) * 1024), 0, 0);
+        for (int j = 0; j < (NBP + 3) / 4; ++j) {
+          const int i = wu + 4 * j;
+          if (i < NBP)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024),
+                                                     16, lane * 16, (unsigned)((k * NP + NA + i) * 1024), 0, 0);
+        }
       }
     };
     if (nt > 0) {
@@ -400,17 +535,18 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         if (k + 2 < nt) issue_a(k + 2);
         if (k + 1 < nt) issue_b(k + 1);
         if (!active) return;
-        const char* bs = bring + (k & 1) * NBP * 1024;
+        const char* bs = bring + (k & 1) * BSZ * 1024;
         f32x4 y4[4];
-        x3_labels(bs + (NBP - 1) * 1024, h, y4);
+        x3_labels(bs + (BSZ - 1) * 1024, h, y4);
         x3_labels_wait(y4);
         // GEMM1 of tile k+1 (a stale slot past the last tile: computed, never used) beside
         // the epilogue of tile k
-        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) & 1) * NA * 1024) + lane;
+        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % ASL) * NA * 1024) + lane;
         float res[16];
         nxt = x3_gemm1<KB>(fa, z1, z2, z3);
         x3_epilogue(acc, y4, res, pe);
-        x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
+        if constexpr (TR) x3_gemm2_tr<KB, DT>(aring + (k % ASL) * NA * 1024, res, g);
+        else x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
         if constexpr (SCHED == 0) {
           // scheduling hints (LLVM igrouplp): each GEMM1(k+1) MFMA followed by 5 VALU (tile k's
           // epilogue and the first split half), each GEMM2(k) MFMA by 3 (the second split half),
@@ -515,10 +651,16 @@ constexpr int X3_ROLE_WAVES = 8;
 // and 4 measured equal (the tail launch streams the 465 MB of split tiles at ~7 TB/s)
 constexpr int X3_ROLE_PA = 2;
 
+// A-ring slots of the tail form: tiles k - 1 (GEMM2 of the B waves, transposed reads of the
+// GEMM1 image), k + 1 (GEMM1 of the A waves) and k + PA landing
+template <int PA>
+constexpr int x3_roles_aslots() { return PA + 2; }
+
 template <int KB, int DT, int PA>
 inline size_t x3_roles_lds_bytes() {
-  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB, NBP = NP - NA;
-  return (size_t)(PA * NA + (PA + 1) * NBP) * 1024 + (size_t)2 * 4 * 4096;
+  constexpr int NA = 3 * KB;
+  // A ring, the label ring (one 1-KB piece per tile, PA + 1 slots), the residual ring
+  return (size_t)(x3_roles_aslots<PA>() * NA + (PA + 1)) * 1024 + (size_t)2 * 4 * 4096;
 }
 
 template <int KB, int DT, int PA>
@@ -526,7 +668,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
                                                                          int64_t ntiles, int D, int S, int Gt,
                                                                          nmx_eval_batch ev, float* __restrict__ gpart,
                                                                          double* __restrict__ pepart) {
-  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB, NBP = NP - NA;
+  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB;
   static_assert(KB == 4, "role-split tail form: D in (48, 64]");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x;
@@ -556,12 +698,15 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
   const int nt = (int)(t1 - t0);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
-  constexpr int PB = PA + 1;
+  // The tail launch is bound by streaming X (~7 TB/s): it reads each tile's GEMM1 image and its
+  // labels only, and the B waves take GEMM2's X^T operand from the GEMM1 image by transposed LDS
+  // reads (x3_gemm2_tr_load), so the B pieces (half the packed bytes) stay in HBM.
+  constexpr int PB = PA + 1, PAS = x3_roles_aslots<PA>();
   char* aring = lds;
-  char* bring = lds + PA * NA * 1024;
-  char* rring = bring + PB * NBP * 1024;  // [slot][tile][4 KB]
+  char* bring = lds + PAS * NA * 1024;  // labels: [slot][1 KB]
+  char* rring = bring + PB * 1024;      // [slot][tile][4 KB]
   auto issue_a = [&](int k) {
-    char* dst = aring + (k % PA) * NA * 1024;
+    char* dst = aring + (k % PAS) * NA * 1024;
 #pragma unroll
     for (int j = 0; j < (NA + X3_ROLE_WAVES - 1) / X3_ROLE_WAVES; ++j) {
       const int i = w + X3_ROLE_WAVES * j;
@@ -570,15 +715,10 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
                                                  lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
     }
   };
-  auto issue_b = [&](int k) {
-    char* dst = bring + (k % PB) * NBP * 1024;
-#pragma unroll
-    for (int j = 0; j < (NBP + X3_ROLE_WAVES - 1) / X3_ROLE_WAVES; ++j) {
-      const int i = w + X3_ROLE_WAVES * j;
-      if (i < NBP)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
-                                                 lane * 16, (unsigned)((k * NP + NA + i) * 1024), 0, 0);
-    }
+  auto issue_b = [&](int k) {  // the label piece (the last of the tile)
+    if (w == X3_ROLE_WAVES - 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(bring + (k % PB) * 1024),
+                                               16, lane * 16, (unsigned)((k * NP + NP - 1) * 1024), 0, 0);
   };
   char* const rmine = rring + t * 4096 + lane * 16;  // + slot * 4 * 4096
 
@@ -611,9 +751,9 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         if (k + PA - 1 < nt) issue_b(k + PA - 1);
         if (!active) return;
         f32x4 y4[4];
-        x3_labels(bring + (k % PB) * NBP * 1024 + (NBP - 1) * 1024, h, y4);
+        x3_labels(bring + (k % PB) * 1024, h, y4);
         x3_labels_wait(y4);
-        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % PA) * NA * 1024) + lane;
+        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % PAS) * NA * 1024) + lane;
         float res[16];
         // hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with row
         // pairs of tile k's epilogue; sched_barrier(0) pins the order; the operations and their
@@ -671,9 +811,12 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
 #pragma unroll
       for (int r = 0; r < 16; ++r) g[dt][r] = 0.0f;
     auto gemm2 = [&](int k) {  // GEMM2 of tile k
+      bf16x8 fb[3][DT][2];
+      x3_gemm2_tr_load<KB, DT>(aring + (k % PAS) * NA * 1024, fb);
       float res[16];
-      x3_res_load(rmine + (k & 1) * 4 * 4096, res);
-      x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bring + (k % PB) * NBP * 1024) - NA * 64 + lane, res, g);
+      x3_res_load(rmine + (k & 1) * 4 * 4096, res);  // (waits for every LDS read, the above too)
+      x3_tr_wait<DT>(fb);
+      x3_gemm2_regs<DT>(fb, res, g);
     };
     if (nt > 0) {
       issue_a(0);
@@ -831,7 +974,6 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   double* pepart = (double*)((char*)workspace + ((size_t)S * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
   const int64_t nt = x3_ntiles(n_rows);
   const int KB = x3_kb(dim);
-  const size_t lds = (size_t)2 * x3_np(dim) * 1024;
   const char* Xq = (const char*)packed + x3_offset();
   const int nb = std::min(ev->num_chains, ev->ldc);  // batch positions that can hold a chain
   const int Gt = (nb + 127) / 128;
@@ -841,13 +983,17 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
                        (x3_roles_lds_bytes<4, 2, X3_ROLE_PA>()), s, Xq,
                        nt, dim, S, Gt, *ev, gpart, pepart);
   else if (KB == 4)
-    hipLaunchKernelGGL((k_logreg_x3<4, 2, 3, 0>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<4, 2, 3, 0>), grid, blk, (x3_lds_bytes<4, 2>()), s, Xq, nt, dim, S, Gt, *ev,
+                       gpart, pepart);
   else if (KB == 3)
-    hipLaunchKernelGGL((k_logreg_x3<3, 2, 3, 0>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<3, 2, 3, 0>), grid, blk, (x3_lds_bytes<3, 2>()), s, Xq, nt, dim, S, Gt, *ev,
+                       gpart, pepart);
   else if (KB == 2)
-    hipLaunchKernelGGL((k_logreg_x3<2, 1, 3, 0>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<2, 1, 3, 0>), grid, blk, (x3_lds_bytes<2, 1>()), s, Xq, nt, dim, S, Gt, *ev,
+                       gpart, pepart);
   else
-    hipLaunchKernelGGL((k_logreg_x3<1, 1, 3, 0>), grid, blk, lds, s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<1, 1, 3, 0>), grid, blk, (x3_lds_bytes<1, 1>()), s, Xq, nt, dim, S, Gt, *ev,
+                       gpart, pepart);
   if (int st = nmx_check_launch("k_logreg_x3")) return st;
   const double* wcol = (const double*)packed;
   const double shift = -(double)(nt * X3_ROWS - n_rows) * 0.6931471805599453;

@@ -18,6 +18,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NUMPYRO_AMD_DEBUG=1: the debug build (bounds / invariant checks, numpyro_amd.build(debug=True))
 LIB_PATH = os.path.join(_HERE, "_lib", "libnumpyro_amd_debug.so" if os.environ.get("NUMPYRO_AMD_DEBUG") == "1"
                         else "libnumpyro_amd.so")
+# kernel experiments: another in-tree build of the same library (scripts/ab_build.py variants)
+if os.environ.get("NUMPYRO_AMD_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["NUMPYRO_AMD_LIB"])
 
 _lib = None
 
