@@ -364,6 +364,12 @@ int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, con
                      int ldo, void* stream);
 int nmx_unpack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
                        int ldo, const float* pe_in, float* pe_out, void* stream);
+/* The same compaction for a chain-row arena field in ([ldc][dim] rows, NMX_LAYOUT_CHAIN_ROWS):
+ * pack_rows: out[d][p] = in[list[p]][d]; unpack_rows: out[list[p]][d] = in[d][p] (+ pe). */
+int nmx_pack_rows(const float* in, int ldc, int dim, const int32_t* list, const int32_t* count, float* out,
+                  int ldo, void* stream);
+int nmx_unpack_rows(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
+                    int ldc, const float* pe_in, float* pe_out, void* stream);
 /* Per-chain dense mass matrices (the reference's per-chain adaptation, hmc.py:790-798 vmapped
  * init_kernel; hmc_util.py:133-239 welford_covariance(diagonal=False)), dim <= 256.
  * nmx_chain_matvec: out[a][c] = sum_b M[c][b][a] in[b][c] for the listed chains (list/count),

@@ -314,6 +314,49 @@ __global__ __launch_bounds__(256) void k_unpack(const float* __restrict__ in, in
   if (pe_in && blockIdx.x == 0 && threadIdx.x < 64) pe_out[c] = pe_in[p];
 }
 
+// The same for a chain-row arena ([ldc][D] rows, nmx_nuts_config.layout = CHAIN_ROWS): a
+// 64 x 64 transpose through LDS per block, coalesced on both sides.
+constexpr int TR_TILE = 64;
+__global__ __launch_bounds__(256) void k_pack_rows(const float* __restrict__ in, int D,
+                                                   const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                                   float* __restrict__ out, int ldo) {
+  __shared__ float t[TR_TILE][TR_TILE + 1];
+  const int n = *count;
+  const int p0 = blockIdx.y * TR_TILE, d0 = blockIdx.x * TR_TILE;
+  if (p0 >= n) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < TR_TILE; i += 4) {  // row (chain) p0 + i, coordinates d0 + lane
+    const int p = p0 + i, d = d0 + lane;
+    if (p < n && d < D) t[i][lane] = in[(size_t)list[p] * D + d];
+  }
+  __syncthreads();
+  for (int i = w; i < TR_TILE; i += 4) {  // coordinate d0 + i, positions p0 + lane
+    const int p = p0 + lane, d = d0 + i;
+    if (p < n && d < D) out[(size_t)d * ldo + p] = t[lane][i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ in, int ldi, int D,
+                                                     const int32_t* __restrict__ list,
+                                                     const int32_t* __restrict__ count, float* __restrict__ out,
+                                                     const float* __restrict__ pe_in, float* __restrict__ pe_out) {
+  __shared__ float t[TR_TILE][TR_TILE + 1];
+  const int n = *count;
+  const int p0 = blockIdx.y * TR_TILE, d0 = blockIdx.x * TR_TILE;
+  if (p0 >= n) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < TR_TILE; i += 4) {  // coordinate d0 + i, positions p0 + lane
+    const int p = p0 + lane, d = d0 + i;
+    if (p < n && d < D) t[lane][i] = in[(size_t)d * ldi + p];
+  }
+  __syncthreads();
+  for (int i = w; i < TR_TILE; i += 4) {  // chain list[p0 + i], coordinates d0 + lane
+    const int p = p0 + i, d = d0 + lane;
+    if (p < n && d < D) out[(size_t)list[p] * D + d] = t[i][lane];
+  }
+  if (pe_in && blockIdx.x == 0 && threadIdx.x < 64 && p0 + lane < n) pe_out[list[p0 + lane]] = pe_in[p0 + lane];
+}
+
 // ---------------------------------------------------------------------------------------
 // Split-bf16 chain products (f32-accurate on the bf16 matrix cores; the scheme of the covtype
 // kernel, potential_logreg.hip "Split-bf16 kernel"): every f32 operand as three bf16 terms,
@@ -525,6 +568,24 @@ extern "C" int nmx_unpack_columns(const float* in, int ldi, int dim, const int32
   hipLaunchKernelGGL(k_unpack, dim3((dim + PACK_ROWS - 1) / PACK_ROWS, ldi / 64), dim3(256), 0,
                      (hipStream_t)stream, in, ldi, dim, list, count, out, ldo, pe_in, pe_out);
   return nmx_check_launch("k_unpack");
+}
+
+extern "C" int nmx_pack_rows(const float* in, int ldc, int dim, const int32_t* list, const int32_t* count,
+                             float* out, int ldo, void* stream) {
+  if (!in || !list || !count || !out || dim <= 0 || ldo % 64 || ldc <= 0)
+    return nmx_fail(NMX_ERR_INVALID, "pack_rows: bad arguments");
+  hipLaunchKernelGGL(k_pack_rows, dim3((dim + TR_TILE - 1) / TR_TILE, (ldo + TR_TILE - 1) / TR_TILE), dim3(256), 0,
+                     (hipStream_t)stream, in, dim, list, count, out, ldo);
+  return nmx_check_launch("k_pack_rows");
+}
+
+extern "C" int nmx_unpack_rows(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count,
+                               float* out, int ldc, const float* pe_in, float* pe_out, void* stream) {
+  if (!in || !list || !count || !out || dim <= 0 || ldi % 64 || ldc <= 0 || (pe_in && !pe_out))
+    return nmx_fail(NMX_ERR_INVALID, "unpack_rows: bad arguments");
+  hipLaunchKernelGGL(k_unpack_rows, dim3((dim + TR_TILE - 1) / TR_TILE, (ldi + TR_TILE - 1) / TR_TILE), dim3(256), 0,
+                     (hipStream_t)stream, in, ldi, dim, list, count, out, pe_in, pe_out);
+  return nmx_check_launch("k_unpack_rows");
 }
 
 extern "C" int nmx_dense_padded_dim(int D) { return (D + TM - 1) / TM * TM; }

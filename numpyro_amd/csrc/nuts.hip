@@ -1796,6 +1796,65 @@ __device__ __forceinline__ float uni_f(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
 
+// Leaf inputs of the scalar-site rows, prefetched into LDS by the last wave at the start of a
+// leaf (one value per lane, written after its own rows), so that the potential's finish in
+// wave 0 runs their leapfrog end without a memory round trip.  Entry f of row i: 0 momentum of
+// the moving end, 1 inverse mass, 2 subtree r_sum, 3 tree r_sum, 4 the other end's momentum,
+// 5 + l / 5 + MAXD + l checkpoint momentum / r_sum of level l.
+constexpr int SPRE = 5 + 2 * MAXD;
+
+__device__ __forceinline__ const float* spre_src(const VecCtx& v, const Act& A, bool nuts, int f) {
+  const Arena& a = *v.a;
+  if (f == 0) return A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  if (f == 1) return v.unit ? nullptr : AV(NMX_F_INV_MASS);
+  if (!nuts) return nullptr;
+  if (f == 2) return A.k == 0 ? nullptr : AV(NMX_F_RSUM_SUB);
+  if (f == 3) return A.tree_chk ? AV(NMX_F_RSUM) : nullptr;
+  if (f == 4) return A.tree_chk ? (A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR)) : nullptr;
+  const int l = f < 5 + MAXD ? f - 5 : f - 5 - MAXD;
+  if (l < A.imin || l > A.imax) return nullptr;
+  return (f < 5 + MAXD ? a.ckr : a.ckrs) + l * v.ck_stride;
+}
+
+// leaf_load + leaf_store of one scalar-site row from its prefetched inputs (same arithmetic)
+template <bool NUTS>
+__device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float seff, uint32_t off, float g,
+                                          const float* pre, float* red) {
+  const Arena& a = *v.a;
+  const float es = A.dirR ? seff : -seff;
+  const float half = 0.5f * es;
+  const float r = pre[0] - half * g;
+  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
+  const float im = v.unit ? 1.0f : pre[1];
+  red[0] += (im * r) * r;
+  if constexpr (NUTS) {
+    const float rs = (A.k == 0) ? r : pre[2] + r;
+    nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
+    if ((A.k & 1) == 0) {
+      nmx_at(a.ckr + A.imax * v.ck_stride, off) = r;
+      nmx_at(a.ckrs + A.imax * v.ck_stride, off) = rs;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+      if (i >= A.imin && i <= A.imax) {
+        const float rl = pre[5 + i];
+        const float rsub = (rs - pre[5 + MAXD + i]) + rl;
+        const float rss = rsub - (rl + r) / 2.0f;
+        red[1 + 2 * i] += (im * rl) * rss;
+        red[2 + 2 * i] += (im * r) * rss;
+      }
+    }
+    if (A.tree_chk) {
+      const float rst = pre[3] + rs;
+      const float rlv = A.dirR ? pre[4] : r;
+      const float rrv = A.dirR ? r : pre[4];
+      const float rss2 = rst - (rlv + rrv) / 2.0f;
+      red[1 + 2 * MAXD] += (im * rlv) * rss2;
+      red[2 + 2 * MAXD] += (im * rrv) * rss2;
+    }
+  }
+}
+
 #ifndef NMX_PX_OCC
 #define NMX_PX_OCC 4  // waves per SIMD the kernel is compiled for: <= 128 VGPRs (3 waves: SV 8192 20.0M vs 24.2M)
 #endif
@@ -1807,6 +1866,8 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
   __shared__ float lds_ke[NW];
   __shared__ float lds_sc[NPART];
   __shared__ float lds_tot[NR + 1];  // block totals of the leaf's entries, then U
+  __shared__ float lds_pre[M::NSCALAR * SPRE];  // prefetched scalar-site row inputs
+  static_assert(M::NSCALAR * SPRE <= 64, "one lane per prefetched value");
   // the chain's scalar state lives in LDS: wave 0 runs the scalar logic on it and publishes
   // the decisions the vector phases need (the act word of k_wide_v2 plus four values), so no
   // per-chain scalar is held in vector registers through the row loops
@@ -1856,6 +1917,17 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     if (!A.leaf) __syncthreads();
     if (A.leaf) {
       const float seff = uni_f(Ssh.step_eff);
+      // the last wave prefetches the scalar-site rows' inputs (stored to LDS after its rows)
+      float pv = 0.0f;
+      bool pl = false;
+      if (wv == NW - 1 && lane < M::NSCALAR * SPRE) {
+        const int i = lane / SPRE, f = lane % SPRE;
+        const float* src = spre_src(v, A, is_nuts, f);
+        if (src) {
+          pv = nmx_at(src, base + ((uint32_t)m.scalar_row(i) << 2));
+          pl = true;
+        }
+      }
       const typename M::Glob gl = m.globals_at(AV(NMX_F_Z_EVAL), base, 4u);
       {
         float red[NR];
@@ -1866,6 +1938,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
       if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT>(v, A, m, base, lds);
+      if (pl) lds_pre[lane] = pv;
       PX_T(1);
       PX_ADD(0, 0, 1);
       __syncthreads();
@@ -1894,16 +1967,8 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
           for (int i = 0; i < M::NSCALAR; ++i) {
             const uint32_t off = base + ((uint32_t)m.scalar_row(i) << 2);
             nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
-            LeafIn x;
-            x.g = gs[i];
-            // (checkpoints read inline, not preloaded: register-lean, one lane)
-            if (is_nuts) {
-              leaf_load<true, false, false>(v, A, off, x);
-              leaf_store<true, false>(v, A, seff, off, x, rs);
-            } else {
-              leaf_load<false, false, false>(v, A, off, x);
-              leaf_store<false, false>(v, A, seff, off, x, rs);
-            }
+            if (is_nuts) spre_leaf<true>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs);
+            else spre_leaf<false>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs);
           }
 #pragma unroll
           for (int e = 0; e < NPART; ++e)
@@ -2000,6 +2065,185 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
   }
 }
 
+
+// ---- launched per-chain step for a chain-row arena -------------------
+// The D-split models behind a batched potential (dense mass: the whitening GEMMs couple the
+// chains between leaves, so the persistent kernel does not apply) keep the launched loop, but
+// its step runs as the persistent kernel's leaf body on a chain-row arena: one workgroup per
+// chain, the potential's gradient read from g_eval instead of computed, the scalar state from
+// and to the arena, the chain appended to the compacted list when its next leaf is pending.
+// Replaces the four D-slice kernels (V1, R, S, V2), whose chain groups move at the pace of
+// their slowest chain.  Same per-chain arithmetic as the persistent kernel.
+struct RowsAll {
+  int dim;
+  static constexpr int NSCALAR = 0;
+  NMX_HD int lo() const { return 0; }
+  NMX_HD int hi() const { return dim; }
+  NMX_HD int scalar_row(int) const { return 0; }
+};
+
+template <int NT, int B>
+__global__ __launch_bounds__(NT, NMX_PX_OCC) void k_chain_step(StepArgs Pk) {
+  constexpr int NW = NT / 64;
+  __shared__ float lds[NPART * NW];
+  __shared__ float lds_tot[NPART];
+  __shared__ float lds_ke[NW];
+  __shared__ int sh_act, sh_slot, sh_wfn, sh_it;
+  __shared__ float sh_seff, sh_pe;
+  const StepArgs& P = Pk;
+  const nmx_nuts_config& cfg = P.cfg;
+  const Arena& a = P.a;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the list of the other parity was consumed by the last potential launch: clear it for the next step
+  if (blockIdx.x == 0 && tid == 0) a.counters[2 + (cfg.parity ^ 1)] = 0;
+  const int D = cfg.dim, ldc = cfg.ldc;
+  const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const uint64_t seed = cfg.seed;
+  int ph = uni_i(AI(NMX_F_PHASE)[c]);
+  if (ph == NMX_PH_DONE) return;
+  if (ph == NMX_PH_WAIT) {  // sync_chains: start once every chain finished the transition
+    const int slot_w = uni_i(AI(NMX_F_ITER)[c]) - 1 - cfg.iter_begin;
+    const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
+                        ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : cfg.num_chains;
+    if (uni_i(fin) < cfg.num_chains) return;
+    ph = NMX_PH_START;
+  }
+  Act A;
+  {
+    ChainScalars Sb;
+    Sb.dir = uni_i(AI(NMX_F_DIR)[c]);
+    Sb.sub_n = uni_i(AI(NMX_F_SUB_N)[c]);
+    Sb.depth = uni_i(AI(NMX_F_DEPTH)[c]);
+    begin_act(cfg, Sb, ph, A);
+  }
+  const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
+  const uint32_t base = ((uint32_t)c * (uint32_t)D) << 2;
+  const RowsAll rows{D};
+  if (A.leaf) {
+    const float seff = uni_f(AF(NMX_F_STEP_EFF)[c]);
+    const float* GE = AV(NMX_F_G_EVAL);
+    {
+      float red[NPART];
+#pragma unroll
+      for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+      float dl = 0.0f, dr = 0.0f;
+      for (int d0 = tid; d0 < D; d0 += B * NT) {
+        PRow x[B];
+        float g[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int d = d0 + q * NT;
+          if (d < D) {
+            const uint32_t off = base + ((uint32_t)d << 2);
+            g[q] = nmx_at(GE, off);
+            if (is_nuts) prow_load<true>(v, A, off, x[q]);
+            else prow_load<false>(v, A, off, x[q]);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int d = d0 + q * NT;
+          if (d < D) {
+            const uint32_t off = base + ((uint32_t)d << 2);
+            if (is_nuts) prow_store<true>(v, A, seff, off, x[q], g[q], red, dl, dr);
+            else prow_store<false>(v, A, seff, off, x[q], g[q], red, dl, dr);
+          }
+        }
+      }
+      if (is_nuts) {
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i)
+          if (i == A.imin && A.imin <= A.imax) {
+            red[1 + 2 * i] = dl;
+            red[2 + 2 * i] = dr;
+          }
+      }
+      wave_sums_to_lds<NW, NPART>(red, lds, A, is_nuts);
+    }
+    if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT>(v, A, rows, base, lds);
+    __syncthreads();
+    if (wv == 0) {
+      float tot = 0.0f;
+      if (lane < NPART && entry_used(A, is_nuts, lane)) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) tot += lds[lane * NW + w];
+      }
+      if (lane < NPART) lds_tot[lane] = tot;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  // scalar logic: wave 0 (lane 0 writes the state back, the counters and the list entry)
+  if (wv == 0) {
+    ChainScalars S;
+    load_scalars(a, c, S);
+    A.pe_eval = A.leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
+    leaf_phase(cfg, S, A, A.leaf ? 0.5f * lds_tot[0] : 0.0f, seed, gch);
+    tree_phase(
+        cfg, S, A, [&](int i, int side) { return lds_tot[1 + 2 * i + side]; },
+        [&](int side) { return lds_tot[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, lane == 0);
+    if (lane == 0) {
+      store_scalars(a, c, S);
+      sh_act = pack_act(A);
+      sh_slot = A.slot;
+      sh_wfn = A.wfn;
+      sh_it = S.it;
+      sh_seff = S.step_eff;
+      sh_pe = S.pe;
+      if (A.fin_done) atomicAdd(&a.counters[0], 1);
+      if (A.fin_wait) {
+        const int fs = A.fin_t - cfg.iter_begin;
+        if (fs >= 0 && fs < cfg.iter_capacity) atomicAdd(&a.finished[fs], 1);
+      }
+      if (A.start_iter || A.prep_leaf) {  // the next leaf is pending: list it for the potential
+        const int pos = atomicAdd(&a.counters[2 + cfg.parity], 1);
+        NMX_DCHECK(pos < cfg.num_chains);
+        a.active_idx[(size_t)cfg.parity * ldc + pos] = c;
+      }
+    }
+  }
+  __syncthreads();  // decisions published
+  const int act = uni_i(sh_act);
+  Act D2{};
+  D2.take_leaf = act & ACT_TAKE_LEAF;
+  D2.done_sub = act & ACT_DONE_SUB;
+  D2.take_biased = act & ACT_TAKE_BIASED;
+  D2.hmc_accept = act & ACT_HMC_ACCEPT;
+  D2.iter_done = act & ACT_ITER_DONE;
+  D2.wf_update = act & ACT_WF_UPDATE;
+  D2.finalize = act & ACT_FINALIZE;
+  D2.start_iter = act & ACT_START;
+  D2.prep_leaf = act & ACT_PREP;
+  D2.dirR = (act & ACT_DIRR) ? 1 : 0;
+  D2.new_dir = (act & ACT_NEWDIR) ? 1 : 0;
+  D2.slot = uni_i(sh_slot);
+  D2.wfn = uni_i(sh_wfn);
+  constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_START |
+                      ACT_PREP;
+  float ke0 = 0.0f;
+  if (act & VEC) {
+    float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc : nullptr;
+    ke0 = persist_apply_rows<NT, B>(v, D2, rows, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp, P.transform,
+                                    cfg);
+  }
+  if (D2.start_iter) {
+    const float t = wave_sum(ke0);
+    if (lane == 0) lds_ke[wv] = t;
+    __syncthreads();
+    if (tid == 0) {
+      float tot = 0.0f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tot += lds_ke[w];
+      const float e0 = sh_pe + 0.5f * tot;  // build_tree :1130
+      AF(NMX_F_E0)[c] = e0;
+      AF(NMX_F_ENERGY)[c] = e0;  // proposal energy of the initial tree (:1137)
+    }
+  }
+}
 // ---------------------------------------------------------------------------------------
 // Reset / init kernels (either arena layout: vidx)
 // ---------------------------------------------------------------------------------------
@@ -2380,12 +2624,43 @@ extern "C" int nmx_nuts_run_small(const nmx_nuts_config* cfg, void* arena, float
   return nmx_check_launch("k_nuts_persistent");
 }
 
+namespace {
+int persist_nt(int dim);
+// nmx_nuts_step on a chain-row arena: the per-chain step kernel (D-split dims only)
+int step_chain_rows(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields, const int8_t* transform,
+                    void* stream) {
+  if (num_slices(cfg->dim) == 0)
+    return nmx_fail(NMX_ERR_INVALID, "step: the chain-row layout is for dim >= %d", WIDE_MIN_D);
+  if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "step: chain-row layout, one chain group only");
+  if (cfg->parity != 0 && cfg->parity != 1) return nmx_fail(NMX_ERR_INVALID, "parity must be 0 or 1");
+  if (cfg->collection_size > 0 && (!fields || !transform))
+    return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");
+  if ((size_t)cfg->ldc * cfg->dim * 4 > 0xFFFFFFF0ull)
+    return nmx_fail(NMX_ERR_INVALID, "step: a vector field exceeds 4 GiB");
+  StepArgs args;
+  args.a = arena_of(cfg, arena);
+  args.cfg = *cfg;
+  args.samples = samples;
+  args.fields = fields;
+  args.transform = transform;
+  const dim3 grid(cfg->num_chains);
+  hipStream_t s = (hipStream_t)stream;
+  switch (persist_nt(cfg->dim)) {
+    case 128: hipLaunchKernelGGL((k_chain_step<128, NMX_PX_B>), grid, dim3(128), 0, s, args); break;
+    case 256: hipLaunchKernelGGL((k_chain_step<256, NMX_PX_B>), grid, dim3(256), 0, s, args); break;
+    case 512: hipLaunchKernelGGL((k_chain_step<512, NMX_PX_B>), grid, dim3(512), 0, s, args); break;
+    default: hipLaunchKernelGGL((k_chain_step<1024, NMX_PX_B>), grid, dim3(1024), 0, s, args);
+  }
+  return nmx_check_launch("k_chain_step");
+}
+}  // namespace
+
 extern "C" int nmx_nuts_step(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
                              const int8_t* transform, void* stream) {
   int st = validate(cfg);
   if (st) return st;
-  if ((st = need_chain_minor(cfg, "nmx_nuts_step"))) return st;
   if (!arena) return nmx_fail(NMX_ERR_INVALID, "arena is NULL");
+  if (cfg->layout == NMX_LAYOUT_CHAIN_ROWS) return step_chain_rows(cfg, arena, samples, fields, transform, stream);
   // samples may be NULL: the per-transition fields alone are collected
   if (cfg->collection_size > 0 && (!fields || !transform))
     return nmx_fail(NMX_ERR_INVALID, "collection buffers are NULL");

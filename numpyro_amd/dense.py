@@ -155,6 +155,9 @@ class WhitenedPotential(Potential):
         self.dim = base.dim
         self.sites = [(n, s, REAL) for n, s, _ in base.sites]
         self.whitening = None
+        # the engine's arena is in chain rows ([ldc][D], k_chain_step): listed chains are
+        # gathered from / scattered to rows (nmx_pack_rows / nmx_unpack_rows)
+        self.rows = False
 
     def _bind(self, C, ldc, device):
         self.base.bind(C, ldc, device)
@@ -189,14 +192,24 @@ class WhitenedPotential(Potential):
         C, ldc, D = ev.num_chains, ev.ldc, self.dim
         if ev.active_idx:
             # compacted list: the products run on packed columns of the listed chains only
-            check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
-                  "nmx_pack_columns")
+            if self.rows:
+                check(L.nmx_pack_rows(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
+                      "nmx_pack_rows")
+            else:
+                check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
+                      "nmx_pack_columns")
             wt.product(True, ptr(self.wp), ptr(self.zb), ptr(wt.mu), None, ev.active_count, C, ldc, stream)
             self.base.evaluate(self._base_batch(ev), stream)
             wt.product(False, ptr(self.gb), ptr(self.wp), None, None, ev.active_count, C, ldc, stream)
-            check(L.nmx_unpack_columns(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
-                                       ptr(self.pe_p), ev.pe, stream), "nmx_unpack_columns")
+            if self.rows:
+                check(L.nmx_unpack_rows(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
+                                        ptr(self.pe_p), ev.pe, stream), "nmx_unpack_rows")
+            else:
+                check(L.nmx_unpack_columns(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,
+                                           ptr(self.pe_p), ev.pe, stream), "nmx_unpack_columns")
             return
+        # (a batch without a list is [D][ldc] in either layout: a chain-row engine passes
+        # transposed copies, Engine._evaluate_all)
         wt.product(True, ev.z, ptr(self.zb), ptr(wt.mu), ev.phase, None, C, ldc, stream)
         self.base.evaluate(self._base_batch(ev), stream)
         wt.product(False, ptr(self.gb), ev.grad, None, ev.phase, None, C, ldc, stream)

@@ -92,6 +92,9 @@ class Engine:
     # D-split models with diagonal mass: the persistent per-chain schedule (nmx_nuts_run_wide,
     # chain-row arena layout); False: the launched wide schedules above
     wide_persistent = True
+    # D-split models behind a batched (dense-mass) potential: the launched loop with the
+    # per-chain step kernel on a chain-row arena (k_chain_step); False: the D-slice kernels
+    chain_rows_step = True
     # launched fused step (dim <= 256): chain groups stepped on their own streams so that one
     # group's latency-bound step and potential tail overlap another group's potential
     # (nmx_nuts_config.num_groups; 1: one stream).  Measured slower for covtype (each group's
@@ -160,10 +163,13 @@ class Engine:
         # chain-row arena layout for the persistent wide schedule (decided once: the arena's
         # layout is part of a resumable state).  The step-size search runs on the launched
         # kernels, which index [D][ldc]: with it, the launched schedule.
-        self.crow = (self.wide_persistent and not self.dense and not opts.find_heuristic_step_size
-                     and lib().nmx_nuts_num_slices(self.D) > 0
-                     and getattr(self.potential, "wide_model", None) is not None
-                     and self.potential.wide_model() is not None)
+        wide = lib().nmx_nuts_num_slices(self.D) > 0 and not opts.find_heuristic_step_size
+        self.persist_wide = (self.wide_persistent and wide and not self.dense
+                             and getattr(self.potential, "wide_model", None) is not None
+                             and self.potential.wide_model() is not None)
+        self.crow = self.persist_wide or (self.chain_rows_step and wide and self.dense and not self.chain_dense)
+        if self.dense and not self.chain_dense:
+            self.potential.rows = self.crow  # the whitening packs the listed chains' rows
 
     # ------------------------------------------------------------------ arena
     def _alloc(self, iter_capacity: int):
@@ -341,12 +347,12 @@ class Engine:
         w = T_new^-1 (z - mu_new), and U, grad_w are re-evaluated at the new w."""
         wt = self.potential.whitening
         z = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
-        wt.to_model(self.view("z"), z, stream=s)
+        wt.to_model(self.view("z").contiguous(), z, stream=s)
         wt.set(inverse_mass_matrix, mu)
         w = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device)
         w[:, :self.C] = wt.to_whitened(z[:, :self.C])
         check(lib().nmx_nuts_init_from(ctypes.byref(self.cfg), ptr(self.arena), ptr(w), s))
-        self.potential.evaluate(self.eval_batch, s)
+        self._evaluate_all(s)
         check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))
         bad = int(self.view("counters")[1].item())
         if bad:
@@ -534,7 +540,7 @@ class Engine:
         cfgp = ctypes.byref(self.cfg)
         arena = ptr(self.arena)
         tr = self._collect_codes()
-        if self.crow:
+        if self.persist_wide:
             return self._run_wide_persistent(a, b, seed, cstart, thinning, S, samples, fields, s, max_launches)
         check(lib().nmx_nuts_resume(cfgp, arena, s), "nmx_nuts_resume")
         small = self._persistent_model()
@@ -728,7 +734,7 @@ class Engine:
             return z.clone(), g.clone()
         wt = self.potential.whitening
         zb = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
-        wt.to_model(self.view("z"), zb, stream=stream_ptr())
+        wt.to_model(self.view("z").contiguous(), zb, stream=stream_ptr())
         # g_w = T^T g_z  ->  g_z = T^-T g_w
         return zb[:, :self.C].t().clone(), wt.grad_to_model(g.t()).t().contiguous()
 

@@ -153,6 +153,8 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_chain_matvec": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_chain_welford": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "nmx_unpack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "nmx_pack_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "nmx_unpack_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "nmx_pe_mvn": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, _evp, c_vp]),
 }
 

@@ -168,10 +168,14 @@ def main():
     p.add_argument("--dense", type=int, default=1)
     p.add_argument("--launched", action="store_true", help="wide models: potential + step loop (A/B)")
     p.add_argument("--fused", action="store_true", help="wide models: the launched fused step, not the persistent one")
+    p.add_argument("--slices", action="store_true", help="dense wide models: the D-slice step kernels (A/B)")
     p.add_argument("--lib", default=None, help="A/B: load this build of libnumpyro_amd.so")
     a = p.parse_args()
     if a.lib:
         native.LIB_PATH = os.path.abspath(a.lib)
+    if a.slices:
+        from numpyro_amd.engine import Engine
+        Engine.chain_rows_step = False
     if a.launched or a.fused:
         from numpyro_amd.engine import Engine
         Engine.wide_persistent = False

@@ -628,3 +628,48 @@ def test_structured_dense_mass_matches_oracle(device):
     print(f"[structured dense eight schools] {match}/{C} chains reproduce the oracle's block-mass transitions")
     _explain_mismatches(mism, "structured dense eight schools")
     assert match >= int(0.9 * C)
+
+
+def _dense_wide_run(monkeypatch, rows_step, C=96, sync=False, chain_offset=None, W=20, S=4, seed=5, fixed=False):
+    from numpyro_amd.engine import Engine
+
+    monkeypatch.setattr(Engine, "chain_rows_step", rows_step)
+    if fixed:  # one given dense matrix for every chain (no pooled adaptation: shards independent)
+        rs = np.random.RandomState(1)
+        a = rs.randn(600, 600) / 60.0
+        kern = NUTS(P.funnel, dense_mass=True, adapt_mass_matrix=False, inverse_mass_matrix=a @ a.T + np.eye(600),
+                    max_tree_depth=7)
+    else:
+        kern = _kernel(NUTS, P.funnel, dense_mass="pooled", max_tree_depth=7)
+    mcmc = MCMC(kern, num_warmup=W, num_samples=S, num_chains=C, sync_chains=sync, chain_offset=chain_offset)
+    mcmc.run(seed, 600, extra_fields=("num_steps",))
+    assert mcmc._engine.crow == rows_step
+    return (mcmc.get_samples(True)["x"].cpu().numpy(), mcmc.get_extra_fields(True)["num_steps"].cpu().numpy())
+
+
+def test_dense_wide_chain_row_step_matches_slices(device, monkeypatch):
+    """Dense mass at D >= 257: the launched loop with the per-chain step on a chain-row arena
+    (k_chain_step; the whitening packs the listed chains' rows) against the D-slice kernels
+    (V1 / R / S / V2) on the chain-minor arena.  Same per-coordinate arithmetic, dot products
+    summed in another fixed order: tree sizes and draws agree to rounding for >= 90% of chains
+    (funnel D = 600, pooled dense adaptation over W = 20)."""
+    x0, n0 = _dense_wide_run(monkeypatch, False)
+    x1, n1 = _dense_wide_run(monkeypatch, True)
+    same = np.all(n0 == n1, axis=1) & np.all(np.isclose(x0, x1, rtol=1e-3, atol=1e-3).reshape(96, -1), axis=1)
+    print(f"[dense wide chain rows] {int(same.sum())}/96 chains: same tree sizes and draws as the D-slice step")
+    assert same.sum() >= 86
+
+
+def test_dense_wide_chain_row_step_invariances(device, monkeypatch):
+    """The chain-row step keeps the engine's invariances bitwise: lockstep == async (pooled
+    adaptation), and two chain shards reproduce the unsharded run (a given dense matrix: the
+    pooled one would be adapted per shard here, all_reduced across ranks in a real run)."""
+    a = _dense_wide_run(monkeypatch, True)
+    b = _dense_wide_run(monkeypatch, True, sync=True)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
+    f = _dense_wide_run(monkeypatch, True, fixed=True)
+    lo = _dense_wide_run(monkeypatch, True, C=40, chain_offset=0, fixed=True)
+    hi = _dense_wide_run(monkeypatch, True, C=56, chain_offset=40, fixed=True)
+    np.testing.assert_array_equal(f[0][:40], lo[0])
+    np.testing.assert_array_equal(f[0][40:], hi[0])
