@@ -430,9 +430,27 @@ __global__ __launch_bounds__(256) void k_x3_split_b(const float* __restrict__ In
   Bp[base + 128] = b3;
 }
 
-constexpr int X3_PIECES = 2 * (4 * 3 + 2 * 3);  // per 32-deep stage: A 2 x 12, B 2 x 6 pieces of 1 KB
+// chain tiles of 32 per workgroup (2: 128 x 64 outputs per workgroup, two per CU; 4: 128 x 128,
+// one per CU, 1.5x the MFMA work per staged byte)
+#ifndef NMX_GEMM_CT
+#define NMX_GEMM_CT 2
+#endif
+// LDS ring depth in stages (3 with CT = 4: 144 KB, one stage more in flight for the lone
+// workgroup of a CU)
+#ifndef NMX_GEMM_NBUF
+#define NMX_GEMM_NBUF 2
+#endif
+template <int N>
+__device__ __forceinline__ void gemm_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+template <int CT>
+constexpr int x3_pieces() { return 2 * (4 * 3 + CT * 3); }  // per 32-deep stage: A 2 x 12, B 2 x 3 CT pieces of 1 KB
+constexpr int X3_PIECES = x3_pieces<2>();
 
-__global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
+template <int CT, int NBUF>
+__global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
                                                     const char* __restrict__ Bp, float* __restrict__ Out,
                                                     const float* __restrict__ bias, int triangle, int ldc,
                                                     const int32_t* __restrict__ phase,
@@ -456,13 +474,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
     ct_i = q % n_ct;
     if (rt_i >= n_rt) return;
   }
+  constexpr int TNC = 32 * CT;  // chains per workgroup
+  constexpr int NPC = x3_pieces<CT>();
   const int i0 = rt_i * TM;
-  const int c0 = ct_i * TN;
+  const int c0 = ct_i * TNC;
   if (count) {
     if (c0 >= *count) return;
   } else {
-    const int c = c0 + lane;
-    const bool act = c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+    bool act = false;
+#pragma unroll
+    for (int q = 0; q < TNC / 64; ++q) {
+      const int c = c0 + 64 * q + lane;
+      act |= c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+    }
     if (!__any(act)) return;
   }
   const int kt_lo = triangle == 1 ? i0 / BK : 0;
@@ -476,9 +500,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
       (void*)Ap, 0, (int)min((int64_t)lda * lda * 6, (int64_t)0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)Bp, 0, (int)min((int64_t)(lda / 16) * ldc * 16 * 6, (int64_t)0x7fffffff), 0x00020000);
-  // stage kt (k-steps 2 kt, 2 kt + 1): pieces [s][12 A: row tile x plane] then [s][6 B: chain
-  // tile x plane]; wave wu DMAs pieces 9 wu .. 9 wu + 8, each at base + kt * stride (bytes)
-  constexpr int PW = X3_PIECES / 4;
+  // stage kt (k-steps 2 kt, 2 kt + 1): pieces [s][12 A: row tile x plane] then [s][3 CT B:
+  // chain tile x plane]; wave wu DMAs pieces PW wu .. PW wu + PW - 1, each at base + kt * stride
+  constexpr int PW = NPC / 4;
   unsigned pbase[PW], pstride[PW];
 #pragma unroll
   for (int jj = 0; jj < PW; ++jj) {
@@ -488,13 +512,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
       pbase[jj] = (unsigned)(((sb * n_it + 4 * rt_i) * 3 + e) * 1024);
       pstride[jj] = (unsigned)(2 * n_it * 3 * 1024);
     } else {
-      const int sb = (pc - 24) / 6, e = (pc - 24) % 6;
-      pbase[jj] = (unsigned)(((sb * n_ct32 + 2 * ct_i) * 3 + e) * 1024);
+      const int sb = (pc - 24) / (3 * CT), e = (pc - 24) % (3 * CT);
+      pbase[jj] = (unsigned)(((sb * n_ct32 + CT * ct_i) * 3 + e) * 1024);
       pstride[jj] = (unsigned)(2 * n_ct32 * 3 * 1024);
     }
   }
   auto issue = [&](int kt, int buf) {
-    char* st = lds + buf * X3_PIECES * 1024;
+    char* st = lds + buf * NPC * 1024;
 #pragma unroll
     for (int jj = 0; jj < PW; ++jj) {
       const int pc = wu * PW + jj;  // wave-uniform
@@ -508,26 +532,34 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
     }
   };
 
-  f32x16 acc[2];
+  f32x16 acc[CT];
 #pragma unroll
-  for (int cl = 0; cl < 2; ++cl)
+  for (int cl = 0; cl < CT; ++cl)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[cl][r] = 0.0f;
   if (kt_begin < nk) issue(kt_begin, 0);
+  if (NBUF == 3 && kt_begin + 1 < nk) issue(kt_begin + 1, 1);
+  int buf = 0;
   for (int kt = kt_begin; kt < nk; ++kt) {
-    const int buf = (kt - kt_begin) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NBUF == 3 && kt + 1 < nk)
+      gemm_wait_vm<PW>();  // stage kt landed, stage kt + 1 may still be in flight
+    else
+      gemm_wait_vm<0>();
     asm volatile("s_barrier" ::: "memory");  // stage kt landed in every wave; stage kt-1 consumed
-    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-    const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + buf * X3_PIECES * 1024) + lane;
+    if (NBUF == 2) {
+      if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    } else {
+      if (kt + 2 < nk) issue(kt + 2, buf == 0 ? 2 : buf - 1);
+    }
+    const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + buf * NPC * 1024) + lane;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 a1 = fr[(s * 12 + w * 3 + 0) * 64], a2 = fr[(s * 12 + w * 3 + 1) * 64],
                    a3 = fr[(s * 12 + w * 3 + 2) * 64];
 #pragma unroll
-      for (int cl = 0; cl < 2; ++cl) {
-        const bf16x8 b1 = fr[(24 + s * 6 + cl * 3 + 0) * 64], b2 = fr[(24 + s * 6 + cl * 3 + 1) * 64],
-                     b3 = fr[(24 + s * 6 + cl * 3 + 2) * 64];
+      for (int cl = 0; cl < CT; ++cl) {
+        const bf16x8 b1 = fr[(24 + s * 3 * CT + cl * 3 + 0) * 64], b2 = fr[(24 + s * 3 * CT + cl * 3 + 1) * 64],
+                     b3 = fr[(24 + s * 3 * CT + cl * 3 + 2) * 64];
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[cl], 0, 0, 0);
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[cl], 0, 0, 0);
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[cl], 0, 0, 0);
@@ -536,6 +568,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[cl], 0, 0, 0);
       }
     }
+    buf = buf + 1 == NBUF ? 0 : buf + 1;
   }
   float* const dst = ksplit > 1 ? part + (size_t)z * D * ldc : Out;
 #pragma unroll
@@ -543,9 +576,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(const char* __restrict__ Ap,
     const int i = i0 + w * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (i < D) {
       const float bi = (bias && ksplit == 1) ? bias[i] : 0.0f;
-      const int ca = c0 + l31, cb = c0 + 32 + l31;
-      if (ca < ldc) dst[(size_t)i * ldc + ca] = acc[0][r] + bi;
-      if (cb < ldc) dst[(size_t)i * ldc + cb] = acc[1][r] + bi;
+#pragma unroll
+      for (int cl = 0; cl < CT; ++cl) {
+        const int cc = c0 + 32 * cl + l31;
+        if (cc < ldc) dst[(size_t)i * ldc + cc] = acc[cl][r] + bi;
+      }
     }
   }
 }
@@ -671,9 +706,16 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
   const int ks = workspace ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
   // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
   // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
-  const int n_rt = lda / TM, n_ct = ldc / TN;
+  constexpr int CT = NMX_GEMM_CT, NBUF = NMX_GEMM_NBUF;
+  const int n_rt = lda / TM, n_ct = (ldc + 32 * CT - 1) / (32 * CT);
   dim3 grid = dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
-  hipLaunchKernelGGL(k_gemm_x3, grid, dim3(256), (size_t)2 * X3_PIECES * 1024, s, (const char*)Ap, lda, D,
+  constexpr size_t lds = (size_t)NBUF * x3_pieces<CT>() * 1024;
+  if (lds > 64 * 1024) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "gemm_x3: hipFuncSetAttribute: %s", hipGetErrorString(attr));
+  }
+  hipLaunchKernelGGL((k_gemm_x3<CT, NBUF>), grid, dim3(256), lds, s, (const char*)Ap, lda, D,
                      (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
                      ks, 1, n_rt, n_ct);
   if (ks > 1)

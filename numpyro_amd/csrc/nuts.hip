@@ -30,7 +30,10 @@ namespace {
 constexpr int MAXD = NMX_MAX_TREE_DEPTH;
 constexpr int NPART = 2 * MAXD + 3;  // KE, checkpoint dots (2 per level), whole-tree dots
 constexpr int WIDE_MIN_D = 257;      // D from which the step runs D-split (wide schedule)
-constexpr int STEP_CPW = 16;        // chains per wave of the fused step (TPC = 8, D >= 16)
+#ifndef NMX_STEP_CPW
+#define NMX_STEP_CPW 16
+#endif
+constexpr int STEP_CPW = NMX_STEP_CPW;  // chains per wave of the fused step (TPC = 8, D >= 16)
 constexpr int SMALL_CPW = 16;        // chains per wave of the one-wave step (D < 16) and persistent kernel
 
 // slice width of the wide schedule: 32 (D < 4096) and 64 measured best over 16-256
