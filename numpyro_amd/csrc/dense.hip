@@ -478,17 +478,20 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
   constexpr int NPC = x3_pieces<CT>();
   const int i0 = rt_i * TM;
   const int c0 = ct_i * TNC;
-  if (count) {
-    if (c0 >= *count) return;
-  } else {
-    bool act = false;
+  // 64-chain tiles with work (an inactive tile's outputs stay untouched)
+  bool act64[TNC / 64];
+  bool any_act = false;
 #pragma unroll
-    for (int q = 0; q < TNC / 64; ++q) {
+  for (int q = 0; q < TNC / 64; ++q) {
+    if (count) {
+      act64[q] = c0 + 64 * q < *count;
+    } else {
       const int c = c0 + 64 * q + lane;
-      act |= c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF);
+      act64[q] = __any(c < C && (phase == nullptr || phase[c] >= NMX_PH_LEAF));
     }
-    if (!__any(act)) return;
+    any_act |= act64[q];
   }
+  if (!any_act) return;
   const int kt_lo = triangle == 1 ? i0 / BK : 0;
   const int kt_hi = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
   const int z = blockIdx.z;
@@ -579,7 +582,7 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
 #pragma unroll
       for (int cl = 0; cl < CT; ++cl) {
         const int cc = c0 + 32 * cl + l31;
-        if (cc < ldc) dst[(size_t)i * ldc + cc] = acc[cl][r] + bi;
+        if (act64[cl / 2] && cc < ldc) dst[(size_t)i * ldc + cc] = acc[cl][r] + bi;
       }
     }
   }
