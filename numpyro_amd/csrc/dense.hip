@@ -435,6 +435,10 @@ __global__ __launch_bounds__(256) void k_x3_split_b(const float* __restrict__ In
 #ifndef NMX_GEMM_CT
 #define NMX_GEMM_CT 2
 #endif
+// row tiles of 32 per workgroup = its waves (4: 128 rows; 8: 256 rows, 512 threads)
+#ifndef NMX_GEMM_RW
+#define NMX_GEMM_RW 4
+#endif
 // LDS ring depth in stages (3 with CT = 4: 144 KB, one stage more in flight for the lone
 // workgroup of a CU)
 #ifndef NMX_GEMM_NBUF
@@ -445,12 +449,12 @@ __device__ __forceinline__ void gemm_wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
-template <int CT>
-constexpr int x3_pieces() { return 2 * (4 * 3 + CT * 3); }  // per 32-deep stage: A 2 x 12, B 2 x 3 CT pieces of 1 KB
+template <int CT, int RW = 4>
+constexpr int x3_pieces() { return 2 * (RW * 3 + CT * 3); }  // per 32-deep stage: A 2 x 3 RW, B 2 x 3 CT pieces of 1 KB
 constexpr int X3_PIECES = x3_pieces<2>();
 
-template <int CT, int NBUF>
-__global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
+template <int CT, int NBUF, int RW>
+__global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
                                                     const char* __restrict__ Bp, float* __restrict__ Out,
                                                     const float* __restrict__ bias, int triangle, int ldc,
                                                     const int32_t* __restrict__ phase,
@@ -475,8 +479,10 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
     if (rt_i >= n_rt) return;
   }
   constexpr int TNC = 32 * CT;  // chains per workgroup
-  constexpr int NPC = x3_pieces<CT>();
-  const int i0 = rt_i * TM;
+  constexpr int TMW = 32 * RW;  // rows per workgroup
+  constexpr int NPC = x3_pieces<CT, RW>();
+  constexpr int NPA = 6 * RW;   // A pieces per stage
+  const int i0 = rt_i * TMW;
   const int c0 = ct_i * TNC;
   // 64-chain tiles with work (an inactive tile's outputs stay untouched)
   bool act64[TNC / 64];
@@ -493,7 +499,7 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
   }
   if (!any_act) return;
   const int kt_lo = triangle == 1 ? i0 / BK : 0;
-  const int kt_hi = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TM + BK - 1) / BK) : (D + BK - 1) / BK;
+  const int kt_hi = triangle == 2 ? min((D + BK - 1) / BK, (i0 + TMW + BK - 1) / BK) : (D + BK - 1) / BK;
   const int z = blockIdx.z;
   const int kt_begin = kt_lo + (int)((int64_t)(kt_hi - kt_lo) * z / ksplit);
   const int nk = kt_lo + (int)((int64_t)(kt_hi - kt_lo) * (z + 1) / ksplit);
@@ -503,19 +509,20 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
       (void*)Ap, 0, (int)min((int64_t)lda * lda * 6, (int64_t)0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)Bp, 0, (int)min((int64_t)(lda / 16) * ldc * 16 * 6, (int64_t)0x7fffffff), 0x00020000);
-  // stage kt (k-steps 2 kt, 2 kt + 1): pieces [s][12 A: row tile x plane] then [s][3 CT B:
+  // stage kt (k-steps 2 kt, 2 kt + 1): pieces [s][3 RW A: row tile x plane] then [s][3 CT B:
   // chain tile x plane]; wave wu DMAs pieces PW wu .. PW wu + PW - 1, each at base + kt * stride
-  constexpr int PW = NPC / 4;
+  static_assert(NPC % RW == 0, "pieces per wave");
+  constexpr int PW = NPC / RW;
   unsigned pbase[PW], pstride[PW];
 #pragma unroll
   for (int jj = 0; jj < PW; ++jj) {
     const int pc = wu * PW + jj;
-    if (pc < 24) {
-      const int sb = pc / 12, e = pc % 12;
-      pbase[jj] = (unsigned)(((sb * n_it + 4 * rt_i) * 3 + e) * 1024);
+    if (pc < NPA) {
+      const int sb = pc / (3 * RW), e = pc % (3 * RW);
+      pbase[jj] = (unsigned)(((sb * n_it + RW * rt_i) * 3 + e) * 1024);
       pstride[jj] = (unsigned)(2 * n_it * 3 * 1024);
     } else {
-      const int sb = (pc - 24) / (3 * CT), e = (pc - 24) % (3 * CT);
+      const int sb = (pc - NPA) / (3 * CT), e = (pc - NPA) % (3 * CT);
       pbase[jj] = (unsigned)(((sb * n_ct32 + CT * ct_i) * 3 + e) * 1024);
       pstride[jj] = (unsigned)(2 * n_ct32 * 3 * 1024);
     }
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
     for (int jj = 0; jj < PW; ++jj) {
       const int pc = wu * PW + jj;  // wave-uniform
       const unsigned so = pbase[jj] + (unsigned)kt * pstride[jj];
-      if (pc < 24)
+      if (pc < NPA)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(st + pc * 1024), 16,
                                                  lane * 16, so, 0, 0);
       else
@@ -557,12 +564,12 @@ __global__ __launch_bounds__(256, CT == 2 ? 2 : 1) void k_gemm_x3(const char* __
     const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + buf * NPC * 1024) + lane;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 a1 = fr[(s * 12 + w * 3 + 0) * 64], a2 = fr[(s * 12 + w * 3 + 1) * 64],
-                   a3 = fr[(s * 12 + w * 3 + 2) * 64];
+      const bf16x8 a1 = fr[(s * 3 * RW + w * 3 + 0) * 64], a2 = fr[(s * 3 * RW + w * 3 + 1) * 64],
+                   a3 = fr[(s * 3 * RW + w * 3 + 2) * 64];
 #pragma unroll
       for (int cl = 0; cl < CT; ++cl) {
-        const bf16x8 b1 = fr[(24 + s * 3 * CT + cl * 3 + 0) * 64], b2 = fr[(24 + s * 3 * CT + cl * 3 + 1) * 64],
-                     b3 = fr[(24 + s * 3 * CT + cl * 3 + 2) * 64];
+        const bf16x8 b1 = fr[(NPA + s * 3 * CT + cl * 3 + 0) * 64], b2 = fr[(NPA + s * 3 * CT + cl * 3 + 1) * 64],
+                     b3 = fr[(NPA + s * 3 * CT + cl * 3 + 2) * 64];
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[cl], 0, 0, 0);
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[cl], 0, 0, 0);
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[cl], 0, 0, 0);
@@ -709,16 +716,16 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
   const int ks = workspace ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
   // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
   // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
-  constexpr int CT = NMX_GEMM_CT, NBUF = NMX_GEMM_NBUF;
-  const int n_rt = lda / TM, n_ct = (ldc + 32 * CT - 1) / (32 * CT);
+  constexpr int CT = NMX_GEMM_CT, NBUF = NMX_GEMM_NBUF, RW = NMX_GEMM_RW;
+  const int n_rt = (lda + 32 * RW - 1) / (32 * RW), n_ct = (ldc + 32 * CT - 1) / (32 * CT);
   dim3 grid = dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
-  constexpr size_t lds = (size_t)NBUF * x3_pieces<CT>() * 1024;
+  constexpr size_t lds = (size_t)NBUF * x3_pieces<CT, RW>() * 1024;
   if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF>,
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF, RW>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "gemm_x3: hipFuncSetAttribute: %s", hipGetErrorString(attr));
   }
-  hipLaunchKernelGGL((k_gemm_x3<CT, NBUF>), grid, dim3(256), lds, s, (const char*)Ap, lda, D,
+  hipLaunchKernelGGL((k_gemm_x3<CT, NBUF, RW>), grid, dim3(64 * RW), lds, s, (const char*)Ap, lda, D,
                      (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
                      ks, 1, n_rt, n_ct);
   if (ks > 1)
