@@ -439,6 +439,10 @@ __global__ __launch_bounds__(256) void k_x3_split_b(const float* __restrict__ In
 #ifndef NMX_GEMM_RW
 #define NMX_GEMM_RW 4
 #endif
+// 1: the 256 x 128 tile for launches it fills (nmx_gemm_chains_x3); 0: always RW x CT (A/B)
+#ifndef NMX_GEMM_BIG
+#define NMX_GEMM_BIG 1
+#endif
 // LDS ring depth in stages (3 with CT = 4: 144 KB, one stage more in flight for the lone
 // workgroup of a CU)
 #ifndef NMX_GEMM_NBUF
@@ -692,6 +696,26 @@ extern "C" size_t nmx_gemm_x3_split_bytes(int lda, int ldc) {
   return lda > 0 && ldc > 0 ? (size_t)(lda / 16) * 16 * ldc * 6 : 0;
 }
 
+namespace {
+template <int CT, int NBUF, int RW>
+int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out, const float* bias, int triangle,
+                   int ldc, const int32_t* phase, const int32_t* active_count, int num_chains, void* workspace,
+                   int ks, hipStream_t s) {
+  const int n_rt = (lda + 32 * RW - 1) / (32 * RW), n_ct = (ldc + 32 * CT - 1) / (32 * CT);
+  const dim3 grid((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
+  constexpr size_t lds = (size_t)NBUF * x3_pieces<CT, RW>() * 1024;
+  if (lds > 64 * 1024) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF, RW>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "gemm_x3: hipFuncSetAttribute: %s", hipGetErrorString(attr));
+  }
+  hipLaunchKernelGGL((k_gemm_x3<CT, NBUF, RW>), grid, dim3(64 * RW), lds, s, (const char*)Ap, lda, D,
+                     (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
+                     ks, 1, n_rt, n_ct);
+  return NMX_OK;
+}
+}  // namespace
+
 extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* In, float* Out, const float* bias,
                                   int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
                                   int num_chains, void* split, void* workspace, void* stream) {
@@ -716,18 +740,23 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
   const int ks = workspace ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
   // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
   // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
-  constexpr int CT = NMX_GEMM_CT, NBUF = NMX_GEMM_NBUF, RW = NMX_GEMM_RW;
-  const int n_rt = (lda + 32 * RW - 1) / (32 * RW), n_ct = (ldc + 32 * CT - 1) / (32 * CT);
-  dim3 grid = dim3((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
-  constexpr size_t lds = (size_t)NBUF * x3_pieces<CT, RW>() * 1024;
-  if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF, RW>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "gemm_x3: hipFuncSetAttribute: %s", hipGetErrorString(attr));
+  // Two workgroup tiles, the same products bitwise (an output's k sequence and its MFMAs do
+  // not depend on the tile; the tile only decides which workgroup computes it): 256 rows x 128
+  // chains (8 waves, one workgroup per CU, half the staged bytes per MFMA: 214 vs 186 TF/s at
+  // D = 10000, C = 4096) when that grid still gives two workgroups per CU, else 128 x 64 (two
+  // workgroups per CU: better for few chains or small D)
+  // (K-split launches keep the 128 x 64 tile: their split points depend on the tile's K range)
+  const bool big = NMX_GEMM_BIG && ks == 1 && (int64_t)((lda + 255) / 256) * ((num_chains + 127) / 128) >= 512;
+  if (big) {
+    if (int st = launch_gemm_x3<4, 2, 8>(Ap, lda, D, split, Out, bias, triangle, ldc, phase, active_count,
+                                         num_chains, workspace, ks, s))
+      return st;
+  } else {
+    if (int st = launch_gemm_x3<NMX_GEMM_CT, NMX_GEMM_NBUF, NMX_GEMM_RW>(Ap, lda, D, split, Out, bias, triangle, ldc,
+                                                                       phase, active_count, num_chains, workspace,
+                                                                       ks, s))
+      return st;
   }
-  hipLaunchKernelGGL((k_gemm_x3<CT, NBUF, RW>), grid, dim3(64 * RW), lds, s, (const char*)Ap, lda, D,
-                     (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
-                     ks, 1, n_rt, n_ct);
   if (ks > 1)
     hipLaunchKernelGGL(k_gemm_reduce, dim3((D + 15) / 16, ldc / TN), dim3(256), 0, s, (const float*)workspace, ks,
                        D, ldc, Out, bias, phase, active_count, num_chains);

@@ -93,7 +93,8 @@ def test_gemm_chains_matches_fp64(device, D, C, tri, split):
 
 @pytest.mark.parametrize("tri", [0, 1, 2])
 @pytest.mark.parametrize("D,C,split", [(3, 64, False), (55, 200, False), (300, 256, False), (1000, 70, False),
-                                       (3000, 130, True), (5038, 64, True), (10000, 256, False)])
+                                       (3000, 130, True), (5038, 64, True), (10000, 256, False),
+                                       (10000, 2048, False)])
 def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
     """Split-bf16 products (nmx_gemm_chains_x3): f32-level error against float64 -- the same
     bound as the f32-MFMA kernel -- and inactive 64-chain tiles untouched.  D = 10000 is
@@ -141,6 +142,41 @@ def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
             assert np.all(np.isnan(o[:, cols]))
     assert lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(dIn), native.ptr(out), None, 0, ldc, None,
                                   None, C, None, None, None) != 0  # no split buffer
+
+
+@pytest.mark.parametrize("tri", [0, 1, 2])
+def test_gemm_chains_x3_tiles_agree(device, tri):
+    """nmx_gemm_chains_x3 picks its workgroup tile from the grid size (256 x 128 when the launch
+    still fills the chip twice over, else 128 x 64); the products must not depend on it: the
+    same active columns computed under a chain bound that selects each tile are equal."""
+    D, ldc = 10000, 2048
+    rs = np.random.RandomState(tri)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    A = rs.randn(D, D)
+    A = {0: A, 1: np.triu(A), 2: np.tril(A)}[tri]
+    At = np.zeros((lda, lda), np.float32)
+    At[:D, :D] = A.T
+    In = rs.randn(D, ldc).astype(np.float32)
+    bias = rs.randn(D).astype(np.float32)
+    phase = np.full(ldc, native.PH_DONE, np.int32)
+    phase[:1024][rs.rand(1024) < 0.7] = native.PH_LEAF
+    dAt, dIn, db, dph = (torch.from_numpy(x).to(device) for x in (At, In, bias, phase))
+    Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=device)
+    sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, ldc), dtype=torch.uint8, device=device)
+    s = native.stream_ptr()
+    native.check(lib.nmx_gemm_x3_pack_a(native.ptr(dAt), lda, native.ptr(Ap), s))
+    outs = []
+    for bound in (2048, 1024):  # 40 x 16 = 640 big-tile workgroups, then 40 x 8 = 320: small tiles
+        out = torch.full((D, ldc), float("nan"), device=device)
+        native.check(lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(dIn), native.ptr(out), native.ptr(db),
+                                            tri, ldc, native.ptr(dph), None, bound, native.ptr(sp), None, s))
+        outs.append(out[:, :1024].cpu().numpy())
+    torch.cuda.synchronize()
+    act = phase[:1024] >= native.PH_LEAF
+    tiles = act.reshape(16, 64).any(axis=1).repeat(64)
+    assert np.array_equal(outs[0][:, tiles], outs[1][:, tiles])
+    assert np.all(np.isnan(outs[0][:, ~tiles])) and np.all(np.isnan(outs[1][:, ~tiles]))
 
 
 def _corr_cov(D, seed=0):
