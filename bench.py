@@ -370,10 +370,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # NMX_BENCH_BACKEND=gloo (rehearsal only): run N ranks on fewer GPUs than ranks (rank r on
+    # GPU r mod count) with gloo collectives, to exercise the multi-rank bench path on a
+    # one-GPU box; the driver's multi-GPU runs use the default, one rank per GPU over RCCL
+    backend = os.environ.get("NMX_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from numpyro_amd import datasets
     from numpyro_amd import potentials as P

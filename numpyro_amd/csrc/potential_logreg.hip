@@ -119,18 +119,36 @@ int x3_num_splits(int64_t n_rows) {
   return (int)s;
 }
 
-// three-term bf16 split of 8 floats (round to nearest even at every step)
+// three-term bf16 split of 8 floats (round to nearest even at every step), one pair of values
+// per conversion: v_cvt_pk_bf16_f32 rounds both, and the f32 values of the two terms come
+// back from the packed word by a shift (low half) and a mask (high half).  Per-value
+// conversions made the compiler convert each value a second time for its f32 image (7 instead
+// of 3 conversions per pair, 56 instead of 24 per tile in the GEMM2 residual split).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ float pk_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float pk_hi(unsigned u) { return __uint_as_float(u & 0xFFFF0000u); }
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+  u32x4 w1, w2, w3;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h1 = (__bf16)v[j];
-    const float e1 = v[j] - (float)h1;
-    const __bf16 h2 = (__bf16)e1;
-    const float e2 = e1 - (float)h2;
-    b1[j] = h1;
-    b2[j] = h2;
-    b3[j] = (__bf16)e2;
+  for (int p = 0; p < 4; ++p) {
+    const float x0 = v[2 * p], x1 = v[2 * p + 1];
+    const unsigned u1 = pk_bf16(x0, x1);
+    const float e0 = x0 - pk_lo(u1), e1 = x1 - pk_hi(u1);
+    const unsigned u2 = pk_bf16(e0, e1);
+    const float f0 = e0 - pk_lo(u2), f1 = e1 - pk_hi(u2);
+    w1[p] = u1;
+    w2[p] = u2;
+    w3[p] = pk_bf16(f0, f1);
   }
+  b1 = __builtin_bit_cast(bf16x8, w1);
+  b2 = __builtin_bit_cast(bf16x8, w2);
+  b3 = __builtin_bit_cast(bf16x8, w3);
 }
 
 // one thread per (tile, piece, lane): 16 bytes of one operand fragment
