@@ -314,7 +314,7 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
             gathered = shard.gather_chains(sm["s"][:, :, :8])
             torch.cuda.synchronize()
             r["end_of_run"] = {"ms": (time.perf_counter() - te) * 1e3, "gathered_chains": int(gathered.shape[0]),
-                               "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"}
+                               "collective": _collective(world)}
             r["parallelism"] = f"chains sharded {world}-way (no data-path collective)"
             r["scaling"] = "strong"
         if world == 1 and rank == 0 and cpu_seconds > 0:
@@ -335,6 +335,15 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
 
 def _identity(z):
     return z
+
+
+def _collective(world):
+    if world == 1:
+        return "none (1 rank)"
+    import torch.distributed as dist
+
+    b = dist.get_backend()
+    return "all_reduce + all_gather (" + ("RCCL" if b == "nccl" else b) + ")"
 
 
 _STREAMS = {}
@@ -520,7 +529,7 @@ def main():
             "end_of_run": {"ms": end_of_run_ms, "gathered_chains": int(gathered.shape[0]),
                            "max_split_rhat": float(rhat.max()) if rhat is not None else None,
                            "min_ess": float(ess.min()),
-                           "collective": "all_reduce + all_gather (RCCL)" if world > 1 else "none (1 rank)"},
+                           "collective": _collective(world)},
         }
         if not args.no_cpu_baseline and world == 1:
             k = min(args.cpu_chains, hi - lo)

@@ -861,17 +861,22 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
   }
 }
 
-// Sum of slots sp0 .. sp1-1 at stride st (in slot order; 32 loads issued ahead of their adds)
+// Sum of slots sp0 .. sp1-1 at stride st (in slot order; FIN_BATCH loads issued ahead of their
+// adds; 64 measured equal at 332 VGPRs, profiles/r03/ab_finalize.txt)
+#ifndef NMX_FIN_BATCH
+#define NMX_FIN_BATCH 32
+#endif
 template <class T>
 __device__ __forceinline__ T sum_slots(const T* __restrict__ p, size_t st, int sp0, int sp1) {
+  constexpr int B = NMX_FIN_BATCH;
   T s = 0;
   int sp = sp0;
-  for (; sp + 32 <= sp1; sp += 32) {
-    T v[32];
+  for (; sp + B <= sp1; sp += B) {
+    T v[B];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = __builtin_nontemporal_load(p + (size_t)(sp + j) * st);
+    for (int j = 0; j < B; ++j) v[j] = __builtin_nontemporal_load(p + (size_t)(sp + j) * st);
 #pragma unroll
-    for (int j = 0; j < 32; ++j) s += v[j];
+    for (int j = 0; j < B; ++j) s += v[j];
   }
   for (; sp < sp1; ++sp) s += p[(size_t)sp * st];
   return s;
@@ -896,6 +901,12 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
   const int c = nmx_eval_chain(ev, pos);
   const int ldc = ev.ldc;
   const int sp0 = w * S / FIN_WAVES, sp1 = (w + 1) * S / FIN_WAVES;
+  // the U row's z loads (wave 0) go out before the slot sums: one dependent round less
+  float zf[64];
+  if (d == D && w == 0 && c >= 0) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) zf[k] = k < D ? ev.z[(size_t)k * ldc + c] : 0.0f;
+  }
   if (c >= 0) {
     if (d < D) part[w][lane] = sum_slots(gpart + (size_t)d * ldc + pos, (size_t)D * ldc, sp0, sp1);
     else part[w][lane] = sum_slots(pepart + pos, (size_t)ldc, sp0, sp1);
@@ -912,10 +923,6 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < FIN_WAVES; ++i) s += part[i][lane];
-    // every z load in flight at once (D <= 64), then the sums in coordinate order
-    float zf[64];
-#pragma unroll
-    for (int k = 0; k < 64; ++k) zf[k] = k < D ? ev.z[(size_t)k * ldc + c] : 0.0f;
     double zz = 0.0, wz = 0.0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
