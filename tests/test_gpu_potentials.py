@@ -303,3 +303,62 @@ def test_logreg_split_bf16_matches_f32_accuracy(device):
     assert e_pe.max() <= max(3 * r_pe.max(), 2e-7)
     assert e_g.max() <= 3e-6
     assert np.median(e_g) <= 3 * max(np.median(r_g), 1e-7)
+
+
+def _bf16_rne(v):
+    """float32 -> its round-to-nearest-even bf16 value as float32 (finite inputs)."""
+    u = np.ascontiguousarray(v, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def test_logreg_packed_split_is_bitwise_the_numpy_split(device):
+    """nmx_logreg_pack's tiles hold each X value as three bf16 terms v1 = bf16(v),
+    v2 = bf16(v - v1), v3 = bf16(v - v1 - v2), round to nearest even (potential_logreg.hip
+    split3, converted in value pairs): bit-exact against a NumPy restatement of that split,
+    in both operand layouts (GEMM1 A pieces: X[32 t + r][16 kb + 8 h + j]; GEMM2 B pieces:
+    X[16 s + 8 (j >> 2) + 4 h + (j & 3)][32 dt + r]), padded rows and columns zero."""
+    import torch
+
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(11)
+    N, D = 77, 55
+    X = (rs.randn(N, D) * np.exp(rs.randn(N, D) * 3)).astype(np.float32)  # wide exponent range
+    X[3, :7] = [0.0, -0.0, 1e-30, -3e-30, 65504.0, 1.0 + 2 ** -23, -(1.0 + 2 ** -9)]
+    y = (rs.rand(N) < 0.5).astype(np.float32)
+    pot = LogisticRegression(X, y)
+    pot.bind(64, 64, device)
+    raw = pot.packed.view(torch.uint8).cpu().numpy()
+    KB, DT = (D + 15) // 16, (D + 31) // 32
+    NP = 3 * KB + 6 * DT + 1
+    nt = (N + 31) // 32
+    tiles = raw[512:512 + nt * NP * 1024].view(np.uint16).reshape(nt, NP, 64, 8)
+    got = (tiles.astype(np.uint32) << 16).view(np.float32)  # bf16 bits -> float32 values
+
+    Xp = np.zeros((nt * 32, 64), np.float32)
+    Xp[:N, :D] = X
+    t1 = _bf16_rne(Xp)
+    e1 = Xp - t1
+    t2 = _bf16_rne(e1)
+    t3 = _bf16_rne(e1 - t2)
+    planes = [t1, t2, t3]
+    lane = np.arange(64)
+    r, h = lane & 31, lane >> 5
+    j = np.arange(8)
+    for t in range(nt):
+        for p in range(3):
+            for kb in range(KB):
+                rows = 32 * t + r[:, None]
+                cols = 16 * kb + 8 * h[:, None] + j[None, :]
+                want = planes[p][rows, cols]
+                np.testing.assert_array_equal(got[t, p * KB + kb].view(np.uint32), want.view(np.uint32))
+            for dt in range(DT):
+                for s in range(2):
+                    rows = 32 * t + 16 * s + 8 * (j[None, :] >> 2) + 4 * h[:, None] + (j[None, :] & 3)
+                    cols = 32 * dt + r[:, None] + 0 * j[None, :]
+                    want = planes[p][rows, cols]
+                    piece = 3 * KB + p * 2 * DT + 2 * dt + s
+                    np.testing.assert_array_equal(got[t, piece].view(np.uint32), want.view(np.uint32))
+    # the three terms represent every value to within 2^-24 relative (f32 rounding unit)
+    assert np.all(np.abs((t1.astype(np.float64) + t2 + t3) - Xp) <= 2.0 ** -24 * np.abs(Xp) + 1e-45)
