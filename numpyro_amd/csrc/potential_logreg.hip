@@ -108,7 +108,15 @@ constexpr int X3_MAX_S = 256;
 
 inline int x3_kb(int D) { return (D + 15) / 16; }
 inline int x3_dt(int D) { return (D + 31) / 32; }
-inline int x3_np(int D) { return 3 * x3_kb(D) + 6 * x3_dt(D) + 1; }
+// Combined last k-block (H = 1: KB = 4 and D % 16 in 1..8, the covtype D = 55): the last
+// k-block has at most 8 real columns, so two products fit one 16-deep MFMA (columns in the
+// k-slots 0..7 of one term, 8..15 of the other) and its six split products run as three MFMAs
+// on two extra pieces behind the A pieces (x3_gemm1): 45 instead of 48 MFMAs per tile.
+inline int x3_h(int D) {
+  const int r = D % 16;
+  return (x3_kb(D) == 4 && r != 0 && r <= 8) ? 1 : 0;
+}
+inline int x3_np(int D) { return 3 * x3_kb(D) + 2 * x3_h(D) + 6 * x3_dt(D) + 1; }
 inline int64_t x3_ntiles(int64_t n) { return (n + X3_ROWS - 1) / X3_ROWS; }
 
 int x3_num_splits(int64_t n_rows) {
@@ -153,8 +161,8 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& b1, bf16x8& 
 
 // one thread per (tile, piece, lane): 16 bytes of one operand fragment
 __global__ void k_logreg_pack_x3(const float* __restrict__ X, const float* __restrict__ y, int64_t n, int D,
-                                 int KB, int DT, int64_t ntiles, bf16x8* __restrict__ out) {
-  const int NP = 3 * KB + 6 * DT + 1;
+                                 int KB, int DT, int H, int64_t ntiles, bf16x8* __restrict__ out) {
+  const int NP = 3 * KB + 2 * H + 6 * DT + 1;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ntiles * NP * 64) return;
   const int lane = (int)(i & 63);
@@ -174,8 +182,19 @@ __global__ void k_logreg_pack_x3(const float* __restrict__ X, const float* __res
       const int d = 16 * kb + 8 * h + j;
       v[j] = (row < n && d < D) ? X[row * D + d] : 0.0f;
     }
+  } else if (piece < 3 * KB + 2 * H) {
+    // combined pieces of the last k-block: every lane holds its columns 16 (KB - 1) + j; piece
+    // 3 KB: terms 1 (h = 0) and 2 (h = 1), piece 3 KB + 1: terms 3 (h = 0) and 1 (h = 1)
+    const int cp = piece - 3 * KB;
+    plane = cp == 0 ? h : (h == 0 ? 2 : 0);
+    const int64_t row = r0 + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * (KB - 1) + j;
+      v[j] = (row < n && d < D) ? X[row * D + d] : 0.0f;
+    }
   } else if (piece < NP - 1) {
-    const int qq = piece - 3 * KB;
+    const int qq = piece - 3 * KB - 2 * H;
     plane = qq / (2 * DT);
     const int rem = qq % (2 * DT);
     const int dt = rem >> 1, s = rem & 1;
@@ -215,16 +234,29 @@ __device__ __forceinline__ void x3_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-// GEMM1 of one tile: L = X . Z (32 rows x 32 chains), six split products per k-block
-template <int KB>
+// A-piece (plane p, k-block kb) and combined-piece (c) positions in an LDS ring slot: the tile
+// image in HBM order, or (COMPACT, the main kernel with H = 1) the slot without the last
+// k-block's plane pieces, which only the transposed GEMM2 reads of the TR / tail forms need
+template <int KB, bool COMPACT>
+__device__ constexpr int x3_ai(int p, int kb) { return COMPACT ? p * (KB - 1) + kb : p * KB + kb; }
+template <int KB, bool COMPACT>
+__device__ constexpr int x3_ci(int c) { return COMPACT ? 3 * (KB - 1) + c : 3 * KB + c; }
+
+// GEMM1 of one tile: L = X . Z (32 rows x 32 chains), six split products per k-block; with H
+// the last k-block's six as three MFMAs on the combined pieces (columns in k-slots 0..7 of
+// one term and 8..15 of the other; x3_load_z builds the matching Z fragments):
+//   (a3 | a1) . (z1 | z3) = a3 z1 + a1 z3,  (a1 | a2) . (z2 | z1) = a1 z2 + a2 z1,
+//   (a1 | a2) . (z1 | z2) = a1 z1 + a2 z2
+template <int KB, int H, bool COMPACT = false>
 __device__ __forceinline__ f32x16 x3_gemm1(const bf16x8* fr, const bf16x8 (&z1)[KB], const bf16x8 (&z2)[KB],
                                            const bf16x8 (&z3)[KB]) {
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const bf16x8 a1 = fr[(0 * KB + kb) * 64], a2 = fr[(1 * KB + kb) * 64], a3 = fr[(2 * KB + kb) * 64];
+  for (int kb = 0; kb < KB - H; ++kb) {
+    const bf16x8 a1 = fr[x3_ai<KB, COMPACT>(0, kb) * 64], a2 = fr[x3_ai<KB, COMPACT>(1, kb) * 64],
+                 a3 = fr[x3_ai<KB, COMPACT>(2, kb) * 64];
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], acc, 0, 0, 0);
@@ -232,7 +264,46 @@ __device__ __forceinline__ f32x16 x3_gemm1(const bf16x8* fr, const bf16x8 (&z1)[
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], acc, 0, 0, 0);
   }
+  if constexpr (H) {
+    const bf16x8 c0 = fr[x3_ci<KB, COMPACT>(0) * 64], c1 = fr[x3_ci<KB, COMPACT>(1) * 64];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, z3[KB - 1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, z2[KB - 1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, z1[KB - 1], acc, 0, 0, 0);
+  }
   return acc;
+}
+
+// Z fragments of a chain tile (B operand: lane (n, h) holds Z[16 kb + 8 h + j][chain n]),
+// pre-scaled by -log2(e) and split.  Through a buffer descriptor: coordinates >= D and inactive
+// lanes (c = -1) fall outside its range and read 0.  With H the last k-block's lanes all hold
+// columns 16 (KB - 1) + j, as (z1 | z2), (z2 | z1), (z1 | z3) for x3_gemm1's combined products.
+template <int KB, int H>
+__device__ __forceinline__ void x3_load_z(const __amdgpu_buffer_rsrc_t zrs, int c, int h, int ldc, bf16x8 (&z1)[KB],
+                                          bf16x8 (&z2)[KB], bf16x8 (&z3)[KB]) {
+  const unsigned zoff = c >= 0 ? (unsigned)((8 * h * ldc + c) * 4) : 0xFFFFFFF0u;
+  const unsigned zoff0 = c >= 0 ? (unsigned)(c * 4) : 0xFFFFFFF0u;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const bool comb = H && kb == KB - 1;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(zrs, comb ? zoff0 : zoff, (16 * kb + j) * ldc * 4, 0));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= -LOG2E;
+    bf16x8 t1, t2, t3;
+    split3(v, t1, t2, t3);
+    if (comb) {
+      z1[kb] = h ? t2 : t1;
+      z2[kb] = h ? t1 : t2;
+      z3[kb] = h ? t3 : t1;
+    } else {
+      z1[kb] = t1;
+      z2[kb] = t2;
+      z3[kb] = t3;
+    }
+  }
 }
 
 // Labels of a tile (16 per lane, rows of the accumulator layout), read by inline asm: a
@@ -296,10 +367,10 @@ __device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&yh4
   x3_epi_finish(lin, prod, pe);
 }
 
-// GEMM2 of one tile: G += X^T . R, R split into three bf16 terms (k-step s = registers 8s..8s+7)
-template <int KB, int DT>
+// GEMM2 of one tile: G += X^T . R, R split into three bf16 terms (k-step s = registers 8s..8s+7);
+// G2 = the first GEMM2 piece (3 KB + 2 H)
+template <int G2, int DT>
 __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16], f32x16 (&g)[DT]) {
-  constexpr int G2 = 3 * KB;  // first GEMM2 piece
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     float v[8];
@@ -442,17 +513,21 @@ __device__ __forceinline__ void x3_gemm2_regs(const bf16x8 (&fb)[3][DT][2], cons
 // the main kernel's GEMM2 operand from transposed reads of the GEMM1 image (needs KB >= 2 DT)
 template <int KB, int DT>
 constexpr bool x3_tr() { return NMX_X3_TR && KB >= 2 * DT; }
-template <int KB, int DT>
+// A pieces of a main-kernel LDS A slot: without the last k-block's plane pieces when the
+// combined pieces replace them (H) and GEMM2 does not read the slot (not TR)
+template <int KB, int DT, int H>
+constexpr int x3_nal() { return (H && !x3_tr<KB, DT>()) ? 3 * (KB - 1) + 2 : 3 * KB + 2 * H; }
+template <int KB, int DT, int H>
 inline size_t x3_lds_bytes() {
-  constexpr int NA = 3 * KB, NP = 3 * KB + 6 * DT + 1;
-  return x3_tr<KB, DT>() ? (size_t)(3 * NA + 2) * 1024 : (size_t)2 * NP * 1024;
+  constexpr int NA = 3 * KB + 2 * H, NP = NA + 6 * DT + 1;
+  return x3_tr<KB, DT>() ? (size_t)(3 * NA + 2) * 1024 : (size_t)2 * (x3_nal<KB, DT, H>() + NP - NA) * 1024;
 }
 
-template <int KB, int DT, int SCHED>
+template <int KB, int DT, int H, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
                                         nmx_eval_batch ev, float* __restrict__ gpart,
                                         double* __restrict__ pepart) {
-  constexpr int NP = 3 * KB + 6 * DT + 1;
+  constexpr int NP = 3 * KB + 2 * H + 6 * DT + 1;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -472,23 +547,12 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
 
-  // Z through a buffer descriptor: coordinates >= D and inactive lanes (c = -1) fall outside
-  // its range and read 0, so the loads need no per-element conditions (conditions and 64-bit
-  // addresses hoisted out of the item loop spilled)
+  // Z through a buffer descriptor (no per-element conditions: conditions and 64-bit addresses
+  // hoisted out of the item loop spilled)
   const __amdgpu_buffer_rsrc_t zrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)ev.z, 0, D * ldc * 4, 0x00020000);
-  const unsigned zoff = c >= 0 ? (unsigned)((8 * h * ldc + c) * 4) : 0xFFFFFFF0u;
   bf16x8 z1[KB], z2[KB], z3[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zoff, (16 * kb + j) * ldc * 4, 0));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= -LOG2E;
-    split3(v, z1[kb], z2[kb], z3[kb]);
-  }
+  x3_load_z<KB, H>(zrs, c, h, ldc, z1, z2, z3);
   f32x16 g[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -504,18 +568,24 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
     // only the A pieces and the labels are streamed (half the bytes); the A ring then keeps
     // tile k for GEMM2(k) beside tile k+1 (GEMM1) and tile k+2 landing: 3 slots, and B slots
     // hold the label piece only (3 x 12 + 2 x 1 KB)
-    constexpr int NA = 3 * KB, NBP = NP - NA;
+    // With H the A part also holds the two combined pieces; the non-TR slot skips the last
+    // k-block's plane pieces (NAL = 11 of 14 for covtype, x3_ai / x3_ci COMPACT positions).
+    constexpr int NA = 3 * KB + 2 * H, NBP = NP - NA;
     constexpr bool TR = x3_tr<KB, DT>();
+    constexpr int NAL = x3_nal<KB, DT, H>();
+    constexpr bool CMP = NAL != NA;
     constexpr int ASL = TR ? 3 : 2, BSZ = TR ? 1 : NBP;
     char* aring = lds;
-    char* bring = lds + ASL * NA * 1024;
+    char* bring = lds + ASL * NAL * 1024;
     auto issue_a = [&](int k) {
-      char* dst = aring + (k % ASL) * NA * 1024;
+      char* dst = aring + (k % ASL) * NAL * 1024;
 #pragma unroll
-      for (int j = 0; j < (NA + 3) / 4; ++j) {
-        const int i = wu + 4 * j;
-        if (i < NA)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+      for (int j = 0; j < (NAL + 3) / 4; ++j) {
+        const int il = wu + 4 * j;  // slot position; i = the tile's piece
+        const int i = !CMP ? il
+                           : (il < 3 * (KB - 1) ? (il / (KB - 1)) * KB + il % (KB - 1) : 3 * KB + (il - 3 * (KB - 1)));
+        if (il < NAL)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + il * 1024), 16,
                                                    lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
       }
     };
@@ -542,7 +612,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
       if (nt > 1) issue_a(1);
       issue_b(0);
       f32x16 accA, accB;
-      if (active) accA = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      if (active) accA = x3_gemm1<KB, H, CMP>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
       // one tile: epilogue + GEMM2 of tile k on `acc`, GEMM1 of tile k+1 into `nxt`; the loop
       // below alternates the two accumulators (no register copy between tiles)
       auto step = [&](int k, const f32x16& acc, f32x16& nxt) {
@@ -559,12 +629,12 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         x3_labels_wait(y4);
         // GEMM1 of tile k+1 (a stale slot past the last tile: computed, never used) beside
         // the epilogue of tile k
-        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % ASL) * NA * 1024) + lane;
+        const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % ASL) * NAL * 1024) + lane;
         float res[16];
-        nxt = x3_gemm1<KB>(fa, z1, z2, z3);
+        nxt = x3_gemm1<KB, H, CMP>(fa, z1, z2, z3);
         x3_epilogue(acc, y4, res, pe);
-        if constexpr (TR) x3_gemm2_tr<KB, DT>(aring + (k % ASL) * NA * 1024, res, g);
-        else x3_gemm2<KB, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
+        if constexpr (TR) x3_gemm2_tr<KB, DT>(aring + (k % ASL) * NAL * 1024, res, g);
+        else x3_gemm2<NA, DT>(reinterpret_cast<const bf16x8*>(bs) - NA * 64 + lane, res, g);
         if constexpr (SCHED == 0) {
           // scheduling hints (LLVM igrouplp): each GEMM1(k+1) MFMA followed by 5 VALU (tile k's
           // epilogue and the first split half), each GEMM2(k) MFMA by 3 (the second split half),
@@ -572,7 +642,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
           // (scripts/ab_logreg.py, C = 4096 all active): 2.74 vs 2.85 ms without the hints; 4-7
           // and 1-3 VALU per group all within 1.5%.
 #pragma unroll
-          for (int i = 0; i < 6 * KB; ++i) {
+          for (int i = 0; i < 6 * KB - 3 * H; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);            // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, NMX_X3_VALU1, 0);  // VALU
           }
@@ -605,7 +675,7 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
 // (workgroup b = x mod 8), the chain groups of a split on consecutive workgroups of that XCD, so
 // they share X tiles in its L2.  A workgroup whose chain group lies past the compacted list's
 // count leaves after one scalar load: the tail of a NUTS run launches thousands of them.
-template <int KB, int DT, int MINB, int SCHED>
+template <int KB, int DT, int H, int MINB, int SCHED>
 __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict__ Xq, int64_t ntiles, int D, int S,
                                                      int Gt, nmx_eval_batch ev, float* __restrict__ gpart,
                                                      double* __restrict__ pepart) {
@@ -614,7 +684,7 @@ __global__ __launch_bounds__(256, MINB) void k_logreg_x3(const char* __restrict_
   const int ct = qb % Gt;
   const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
   if (ct * 128 >= npos) return;
-  x3_item<KB, DT, SCHED>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
+  x3_item<KB, DT, H, SCHED>(Xq, ntiles, D, S, (qb / Gt) * 8 + (b & 7), ct, ev, gpart, pepart);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -674,19 +744,21 @@ constexpr int X3_ROLE_PA = 2;
 template <int PA>
 constexpr int x3_roles_aslots() { return PA + 2; }
 
-template <int KB, int DT, int PA>
+template <int KB, int DT, int H, int PA>
 inline size_t x3_roles_lds_bytes() {
-  constexpr int NA = 3 * KB;
+  constexpr int NA = 3 * KB + 2 * H;
   // A ring, the label ring (one 1-KB piece per tile, PA + 1 slots), the residual ring
   return (size_t)(x3_roles_aslots<PA>() * NA + (PA + 1)) * 1024 + (size_t)2 * 4 * 4096;
 }
 
-template <int KB, int DT, int PA>
+template <int KB, int DT, int H, int PA>
 __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const char* __restrict__ Xq,
                                                                          int64_t ntiles, int D, int S, int Gt,
                                                                          nmx_eval_batch ev, float* __restrict__ gpart,
                                                                          double* __restrict__ pepart) {
-  constexpr int NP = 3 * KB + 6 * DT + 1, NA = 3 * KB;
+  // the A ring holds the whole A part (the tile's GEMM1 image incl. the combined pieces): the B
+  // waves read GEMM2's X^T operand from its plane pieces
+  constexpr int NP = 3 * KB + 2 * H + 6 * DT + 1, NA = 3 * KB + 2 * H;
   static_assert(KB == 4, "role-split tail form: D in (48, 64]");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x;
@@ -743,18 +815,8 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
   if (roleA) {
     // ---- role A: GEMM1 + epilogue, hands R(k) to its B wave --------------------------------
     const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc((void*)ev.z, 0, D * ldc * 4, 0x00020000);
-    const unsigned zoff = c >= 0 ? (unsigned)((8 * h * ldc + c) * 4) : 0xFFFFFFF0u;
     bf16x8 z1[KB], z2[KB], z3[KB];
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zrs, zoff, (16 * kb + j) * ldc * 4, 0));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= -LOG2E;
-      split3(v, z1[kb], z2[kb], z3[kb]);
-    }
+    x3_load_z<KB, H>(zrs, c, h, ldc, z1, z2, z3);
     double pe = 0.0;
     if (nt > 0) {
       issue_a(0);
@@ -762,7 +824,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
       for (int j = 1; j < PA && j < nt; ++j) issue_a(j);
       for (int j = 0; j < PA - 1 && j < nt; ++j) issue_b(j);
       f32x16 accA, accB;
-      if (active) accA = x3_gemm1<KB>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      if (active) accA = x3_gemm1<KB, H>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
       auto stepA = [&](int k, const f32x16& acc, f32x16& nxt) {
         x3_roles_barrier();  // A(k+1), B(k) landed; R slot k&1 was read by B in iteration k-1
         if (k + PA < nt) issue_a(k + PA);
@@ -782,12 +844,15 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         float prod[2] = {1.0f, 1.0f};
         bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
+        for (int kb = 0; kb < KB - H; ++kb) {
           bf16x8 n1, n2, n3;
-          if (kb + 1 < KB) {
+          if (kb + 1 < KB - H) {
             n1 = fa[(kb + 1) * 64];
             n2 = fa[(KB + kb + 1) * 64];
             n3 = fa[(2 * KB + kb + 1) * 64];
+          } else if (H && kb + 1 == KB - 1) {  // the combined pieces (a1 | a2), (a3 | a1)
+            n1 = fa[(3 * KB) * 64];
+            n2 = fa[(3 * KB + 1) * 64];
           }
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
           x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
@@ -803,11 +868,25 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
-          if (kb + 1 < KB) {
+          if (kb + 1 < KB - H) {
             a1 = n1;
             a2 = n2;
             a3 = n3;
+          } else if (H && kb + 1 == KB - 1) {
+            a1 = n1;
+            a2 = n2;
           }
+        }
+        if constexpr (H) {  // x3_gemm1's combined products (a1 = (a1 | a2), a2 = (a3 | a1) here)
+          constexpr int kb = KB - 1;
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z3[kb], nxt, 0, 0, 0);
+          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
+          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+          __builtin_amdgcn_sched_barrier(0);
+          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
         x3_epi_finish(lin, prod, pe);
         x3_res_store(rmine + (k & 1) * 4 * 4096, res);
@@ -975,7 +1054,7 @@ extern "C" int nmx_logreg_pack(const float* X, const float* y, int64_t n_rows, i
   const int64_t nt = x3_ntiles(n_rows);
   const int64_t nthreads = nt * x3_np(dim) * 64;
   hipLaunchKernelGGL(k_logreg_pack_x3, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, X,
-                     y, n_rows, dim, x3_kb(dim), x3_dt(dim), nt, (bf16x8*)((char*)packed + x3_offset()));
+                     y, n_rows, dim, x3_kb(dim), x3_dt(dim), x3_h(dim), nt, (bf16x8*)((char*)packed + x3_offset()));
   return nmx_check_launch("k_logreg_pack_x3");
 }
 
@@ -999,26 +1078,32 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   double* pepart = (double*)((char*)workspace + ((size_t)S * dim * ev->ldc * sizeof(float) + 255) / 256 * 256);
   const int64_t nt = x3_ntiles(n_rows);
   const int KB = x3_kb(dim);
+  const int H = x3_h(dim);
   const char* Xq = (const char*)packed + x3_offset();
   const int nb = std::min(ev->num_chains, ev->ldc);  // batch positions that can hold a chain
   const int Gt = (nb + 127) / 128;
   const dim3 grid(Gt * S), blk(256);
-  if (KB == 4 && Gt <= X3_TAIL_TILES)
-    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
-                       (x3_roles_lds_bytes<4, 2, X3_ROLE_PA>()), s, Xq,
-                       nt, dim, S, Gt, *ev, gpart, pepart);
+  if (KB == 4 && Gt <= X3_TAIL_TILES && H)
+    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 1, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
+                       (x3_roles_lds_bytes<4, 2, 1, X3_ROLE_PA>()), s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+  else if (KB == 4 && Gt <= X3_TAIL_TILES)
+    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 0, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
+                       (x3_roles_lds_bytes<4, 2, 0, X3_ROLE_PA>()), s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+  else if (KB == 4 && H)
+    hipLaunchKernelGGL((k_logreg_x3<4, 2, 1, 3, 0>), grid, blk, (x3_lds_bytes<4, 2, 1>()), s, Xq, nt, dim, S, Gt,
+                       *ev, gpart, pepart);
   else if (KB == 4)
-    hipLaunchKernelGGL((k_logreg_x3<4, 2, 3, 0>), grid, blk, (x3_lds_bytes<4, 2>()), s, Xq, nt, dim, S, Gt, *ev,
-                       gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<4, 2, 0, 3, 0>), grid, blk, (x3_lds_bytes<4, 2, 0>()), s, Xq, nt, dim, S, Gt,
+                       *ev, gpart, pepart);
   else if (KB == 3)
-    hipLaunchKernelGGL((k_logreg_x3<3, 2, 3, 0>), grid, blk, (x3_lds_bytes<3, 2>()), s, Xq, nt, dim, S, Gt, *ev,
-                       gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<3, 2, 0, 3, 0>), grid, blk, (x3_lds_bytes<3, 2, 0>()), s, Xq, nt, dim, S, Gt,
+                       *ev, gpart, pepart);
   else if (KB == 2)
-    hipLaunchKernelGGL((k_logreg_x3<2, 1, 3, 0>), grid, blk, (x3_lds_bytes<2, 1>()), s, Xq, nt, dim, S, Gt, *ev,
-                       gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<2, 1, 0, 3, 0>), grid, blk, (x3_lds_bytes<2, 1, 0>()), s, Xq, nt, dim, S, Gt,
+                       *ev, gpart, pepart);
   else
-    hipLaunchKernelGGL((k_logreg_x3<1, 1, 3, 0>), grid, blk, (x3_lds_bytes<1, 1>()), s, Xq, nt, dim, S, Gt, *ev,
-                       gpart, pepart);
+    hipLaunchKernelGGL((k_logreg_x3<1, 1, 0, 3, 0>), grid, blk, (x3_lds_bytes<1, 1, 0>()), s, Xq, nt, dim, S, Gt,
+                       *ev, gpart, pepart);
   if (int st = nmx_check_launch("k_logreg_x3")) return st;
   const double* wcol = (const double*)packed;
   const double shift = -(double)(nt * X3_ROWS - n_rows) * 0.6931471805599453;

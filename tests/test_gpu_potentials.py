@@ -317,7 +317,9 @@ def test_logreg_packed_split_is_bitwise_the_numpy_split(device):
     v2 = bf16(v - v1), v3 = bf16(v - v1 - v2), round to nearest even (potential_logreg.hip
     split3, converted in value pairs): bit-exact against a NumPy restatement of that split,
     in both operand layouts (GEMM1 A pieces: X[32 t + r][16 kb + 8 h + j]; GEMM2 B pieces:
-    X[16 s + 8 (j >> 2) + 4 h + (j & 3)][32 dt + r]), padded rows and columns zero."""
+    X[16 s + 8 (j >> 2) + 4 h + (j & 3)][32 dt + r]) and in the combined last-k-block pieces
+    of D % 16 <= 8 (every lane X[32 t + r][48 + j], terms (1 | 2) and (3 | 1) by lane half),
+    padded rows and columns zero."""
     import torch
 
     from numpyro_amd.potentials import LogisticRegression
@@ -331,7 +333,8 @@ def test_logreg_packed_split_is_bitwise_the_numpy_split(device):
     pot.bind(64, 64, device)
     raw = pot.packed.view(torch.uint8).cpu().numpy()
     KB, DT = (D + 15) // 16, (D + 31) // 32
-    NP = 3 * KB + 6 * DT + 1
+    H = 1  # D = 55: combined last k-block (potential_logreg.hip x3_h)
+    NP = 3 * KB + 2 * H + 6 * DT + 1
     nt = (N + 31) // 32
     tiles = raw[512:512 + nt * NP * 1024].view(np.uint16).reshape(nt, NP, 64, 8)
     got = (tiles.astype(np.uint32) << 16).view(np.float32)  # bf16 bits -> float32 values
@@ -358,7 +361,12 @@ def test_logreg_packed_split_is_bitwise_the_numpy_split(device):
                     rows = 32 * t + 16 * s + 8 * (j[None, :] >> 2) + 4 * h[:, None] + (j[None, :] & 3)
                     cols = 32 * dt + r[:, None] + 0 * j[None, :]
                     want = planes[p][rows, cols]
-                    piece = 3 * KB + p * 2 * DT + 2 * dt + s
+                    piece = 3 * KB + 2 * H + p * 2 * DT + 2 * dt + s
                     np.testing.assert_array_equal(got[t, piece].view(np.uint32), want.view(np.uint32))
+    rows = 32 * np.arange(nt)[:, None, None] + r[None, :, None]
+    cols = 16 * (KB - 1) + j[None, None, :] + 0 * rows
+    for cp, (ph0, ph1) in enumerate([(0, 1), (2, 0)]):
+        want = np.where((h == 0)[None, :, None], planes[ph0][rows, cols], planes[ph1][rows, cols])
+        np.testing.assert_array_equal(got[:, 3 * KB + cp].view(np.uint32), want.view(np.uint32))
     # the three terms represent every value to within 2^-24 relative (f32 rounding unit)
     assert np.all(np.abs((t1.astype(np.float64) + t2 + t3) - Xp) <= 2.0 ** -24 * np.abs(Xp) + 1e-45)
