@@ -69,7 +69,7 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None, dev_pe=None):
+def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None, dev_trace=None):
     """Reduced-chain CPU comparator (SURVEY.md §8d CPU side 2): `chains` chains of the oracle's
     NUTS (oracle/hmc_ref.py, float32) started from the GPU's adapted state of the first chains
     (z, U, grad, step size, diagonal mass) and the same Philox stream, so they run the timed
@@ -79,9 +79,9 @@ def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=Non
     waits for the others between transitions); returns leapfrogs/s.
 
     Full-size parity (with dev_ns [chains, T] / dev_z [chains, T, D], the GPU's timed
-    transitions of those chains): the oracle chains' tree sizes and draws are compared with the
-    GPU's transitions from the same state on the same stream, and every chain that leaves the
-    GPU's path is reported with the oracle's decision closest to a tie at that transition."""
+    transitions of those chains, and dev_trace, their per-leaf decision trace): the oracle chains'
+    tree sizes and draws are compared with the GPU's transitions from the same state on the same
+    stream, and every chain that leaves the GPU's path is located at its parting leaf."""
     import numpy as np
 
     from oracle import cpu_batched as CB
@@ -109,19 +109,29 @@ def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=Non
            "potential_gflops": gflops, "potential_share": stats["pot_s"] / dt,
            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
     if dev_ns is not None:
-        par = CB.compare_paths(hist, dev_ns[:chains], dev_z[:chains], atol=1e-4,
-                               dev_pe=None if dev_pe is None else dev_pe[:chains])
-        ties = sum(1 for m in par["mismatches"] if m[4])
-        for c, t, kind, m, tie in par["mismatches"]:
-            print(f"[parity] chain {c}: first difference at timed transition {t}, closest oracle decision {kind} "
-                  f"margin {m:.3g} ({'rounding tie' if tie else 'NOT a tie'})", file=sys.stderr)
-        par["mismatches_at_tie"] = ties
-        par["mismatches"] = [list(m) for m in par["mismatches"]]
+        par = _located_parity(hist, dev_trace, dev_ns[:chains], dev_z[:chains], atol=1e-4, label="parity")
         par["basis"] = ("oracle NUTS (C potential, full data) vs the GPU's timed transitions of the same chains "
                         "from the same state on the same Philox stream: equal tree sizes and draws within 1e-4 "
-                        "per transition")
+                        "per transition; a chain that parts is located at the first leaf where a decision differs "
+                        "(device decision trace vs oracle leaf records, oracle/parity.py) and checked there")
         out["parity"] = par
     return out
+
+
+def _located_parity(hist, dev_trace, dev_ns, dev_z, atol, rtol=0.0, to_model=None, label="parity"):
+    """Leaf-located parity record (oracle/parity.py compare_traced), JSON-ready; each parting is
+    printed to stderr with its leaf, decision, the two values, the shared uniform and the bound."""
+    import numpy as np
+
+    from oracle import parity as PR
+
+    par = PR.compare_traced(hist, dev_trace, dev_ns, dev_z, atol=atol, rtol=rtol, to_model=to_model)
+    for m in par["mismatches"]:
+        print(f"[{label}] " + PR.describe(m), file=sys.stderr)
+    par["mismatches"] = [{k: (float(v) if isinstance(v, (np.floating, float)) else v) for k, v in m.items()}
+                         for m in par["mismatches"]]
+    par["unexplained"] = len(par["mismatches"]) - par["explained"]
+    return par
 
 
 # BASELINE.json configs[2..4]: (model, args, chains (total), adaptation transitions, timed
@@ -159,14 +169,15 @@ def _config_specs():
 CONFIG_WARMUP = {"c2": 100, "c3": 100, "c4": 200}
 
 
-def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_pe=None):
+def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
     """CPU side of a secondary config (SURVEY.md §8d CPU side 2): `cpu_chains` of the oracle's
     NUTS resumed from the GPU's adapted state of the first chains (whitened coordinates and the
     pooled whitening T, mu for dense mass; step size, diagonal mass otherwise) on the same
     Philox stream, their potential calls batched over chains (oracle/batched.py: NumPy float32,
     products on multithreaded BLAS), run continuously for `seconds`.  Returns the baseline and a
     parity record of the oracle's transitions against the GPU's timed ones (tree sizes, draws
-    in model space to 1e-3 relative)."""
+    in model space to 1e-3 relative), each parting located at its leaf with dev_trace (the
+    engine's decision trace of the timed transitions)."""
     import numpy as np
     import threadpoolctl
 
@@ -203,10 +214,8 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_pe=None):
                      ("; dense mass as the whitened identity-mass chain with the GPU's pooled T, mu"
                       if eng.dense else ""),
            "potential_share": stats["pot_s"] / dt, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
-    par = CB.compare_paths(hist, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model,
-                           dev_pe=None if dev_pe is None else dev_pe[:k])
-    par["mismatches_at_tie"] = sum(1 for m in par["mismatches"] if m[4])
-    par["mismatches"] = [list(m) for m in par["mismatches"]]
+    par = _located_parity(hist, dev_trace, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model,
+                          label=f"parity {sp['name'].split(',')[0]}")
     return out, par
 
 
@@ -258,6 +267,9 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
             evs.append((a, b))
 
         pot.evaluate = timed_eval
+        parity_leg = world == 1 and rank == 0 and cpu_seconds > 0
+        if parity_leg:  # decision trace of the CPU comparator's chains (parity located per leaf)
+            eng.set_trace(min(sp["cpu_chains"], eng.C), eng.iteration, sp["steps"])
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -317,15 +329,16 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
                                "collective": _collective(world)}
             r["parallelism"] = f"chains sharded {world}-way (no data-path collective)"
             r["scaling"] = "strong"
-        if world == 1 and rank == 0 and cpu_seconds > 0:
+        if parity_leg:
             k = min(sp["cpu_chains"], eng.C)
             dev_ns = ef["num_steps"][:k].cpu().numpy()
             dev_z = mcmc._samples[:, :, :k].permute(2, 0, 1).to(torch.float64).cpu().numpy()  # model space
+            dev_trace = eng.trace_records()
+            eng.set_trace(0, 0, 0)
             # resume the CPU chains from the post-warmup state (the timed run moved the engine on)
             from numpyro_amd.infer.hmc import restore_state
             restore_state(eng, mcmc.post_warmup_state)
-            dev_pe = ef["potential_energy"][:k].to(torch.float64).cpu().numpy()
-            cb, par = cpu_baseline_config(sp, eng, key_to_seed(8), dev_ns, dev_z, cpu_seconds, dev_pe=dev_pe)
+            cb, par = cpu_baseline_config(sp, eng, key_to_seed(8), dev_ns, dev_z, cpu_seconds, dev_trace)
             r["cpu_baseline"], r["parity"] = cb, par
         out[key] = r
         del mcmc, eng, pot
@@ -436,6 +449,9 @@ def main():
         evs.append((a, b))
 
     pot.evaluate = timed_eval
+    parity_leg = not args.no_cpu_baseline and world == 1
+    if parity_leg:  # decision trace of the CPU comparator's chains (parity located per leaf)
+        eng.set_trace(min(args.cpu_chains, hi - lo), eng.iteration, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -531,14 +547,14 @@ def main():
                            "min_ess": float(ess.min()),
                            "collective": _collective(world)},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if parity_leg:
             k = min(args.cpu_chains, hi - lo)
             cb = cpu_baseline(X, y, start_state, key_to_seed(args.seed + 2), args.adapt + args.warmup, args.adapt, k,
                               args.cpu_seconds, dev_ns=ns[:k].cpu().numpy(),
-                              dev_z=site[:k].to(torch.float64).cpu().numpy(),
-                              dev_pe=ef["potential_energy"][:k].to(torch.float64).cpu().numpy())
+                              dev_z=site[:k].to(torch.float64).cpu().numpy(), dev_trace=eng.trace_records())
             out["parity"] = cb.pop("parity")
             out["cpu_baseline"] = cb
+    eng.set_trace(0, 0, 0)
     if args.configs != "none":
         del mcmc, eng, pot, start_state
         torch.cuda.empty_cache()

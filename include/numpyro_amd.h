@@ -153,7 +153,37 @@ typedef struct nmx_nuts_config {
                                     on two streams that overlap one group's step with the
                                     other's potential.  A chain's results do not depend on it. */
   int32_t group;                 /* the group nmx_nuts_step advances (0 .. num_groups - 1) */
+  /* Per-leaf decision trace (parity tests and bench parity legs; NULL = off).  For arena
+   * chains c < trace_chains and transitions it0 <= t < it0 + trace_iters, leaf n < trace_leaves
+   * of the transition (n counted over the whole tree) writes NMX_TRACE_REC floats at
+   * trace[((t - it0) * trace_chains + c) * trace_leaves + n][.] (enum nmx_trace_field): the
+   * quantities the reference's decisions at that leaf are taken on (hmc_util.py:851-894
+   * leaf energy, :749-764 transition probabilities, :735-746 U-turn dots), so a transition
+   * whose path leaves the oracle's can be located at its first differing leaf.  Writing
+   * does not change any result. */
+  int32_t trace_chains;
+  int32_t trace_it0;
+  int32_t trace_iters;
+  int32_t trace_leaves;
+  float* trace;
 } nmx_nuts_config;
+
+#define NMX_TRACE_REC 8
+enum nmx_trace_field {
+  NMX_T_DE = 0,      /* leaf delta energy (NaN -> +inf), hmc_util.py:868-871 */
+  NMX_T_P_LEAF,      /* uniform (in-subtree) transition probability; -1 for a subtree's first leaf */
+  NMX_T_DOT_SUB,     /* min of the iterative U-turn dots checked at this leaf (+inf: none) */
+  NMX_T_P_BIASED,    /* at a subtree end: min(1, exp(w_sub - w_tree)) before turning/diverging
+                        zero it; -1 elsewhere */
+  NMX_T_DOT_TREE,    /* at a subtree end completed by size: min whole-tree U-turn dot; +inf elsewhere */
+  NMX_T_FLAGS,       /* bits: nmx_trace_flag */
+  NMX_T_PE,          /* potential energy of the leaf */
+  NMX_T_LEAF         /* leaf index in the transition (as float) */
+};
+enum nmx_trace_flag {
+  NMX_TF_TAKE_LEAF = 1, NMX_TF_TURN_SUB = 2, NMX_TF_DIVERGE = 4, NMX_TF_DONE_SUB = 8,
+  NMX_TF_TAKE_BIASED = 16, NMX_TF_TURN_TREE = 32, NMX_TF_ITER_DONE = 64
+};
 
 /* D-slices of the wide step (0 when dim is small enough for the fused one-kernel step).
  * Depends on dim only, so results never depend on how chains are sharded. */

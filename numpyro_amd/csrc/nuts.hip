@@ -284,7 +284,7 @@ struct Act {
   bool tree_chk;  // this leaf completes its subtree by size: the whole-tree U-turn dots are needed
   bool start_iter, prep_leaf, fin_done, fin_wait, div_new;
   int dirR, new_dir, k, j, imin, imax, slot, fin_t, wfn;
-  float pe_eval, E_new, acc_new, w_new;
+  float pe_eval, E_new, acc_new, w_new, p_leaf;
 };
 
 enum : int {
@@ -353,12 +353,14 @@ __device__ __forceinline__ void leaf_phase(const nmx_nuts_config& cfg, ChainScal
   const int k = A.k, j = A.j;
   if (k == 0) {  // new_tree = new_leaf (:1019-1021)
     A.take_leaf = true;
+    A.p_leaf = -1.0f;
     S.sub_w = A.w_new;
     S.sub_acc = A.acc_new;
   } else {  // _combine_tree(..., biased_transition=False) (:767-848, :749-753)
     const float p = nmx_sigmoid(A.w_new - S.sub_w);
     const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_LEAF, j, k).x);
     A.take_leaf = u < p;
+    A.p_leaf = p;
     S.sub_w = nmx_logaddexp(S.sub_w, A.w_new);
     S.sub_acc = S.sub_acc + A.acc_new;
   }
@@ -384,6 +386,9 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
   bool it_div = false;
   bool new_doubling = false;
   if (A.leaf && is_nuts) {
+    const int leaf_n = S.tree_n + A.k;  // leaf index in the transition (trace)
+    const int leaf_it = S.it;
+    float pb_raw = -1.0f;
     bool turning_sub = false;
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
@@ -397,6 +402,7 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
       const bool turning_tree = turning_sub || (A.tree_chk && ((tree(0) <= 0.0f) || (tree(1) <= 0.0f)));
       float pb = expf(S.sub_w - S.tree_w);
       pb = isnan(pb) ? pb : fminf(pb, 1.0f);  // jnp.clip keeps NaN
+      pb_raw = pb;
       if (turning_sub || A.div_new) pb = 0.0f;
       const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_BIASED, A.j, 0).x);
       A.take_biased = u < pb;
@@ -421,6 +427,29 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
       }
     } else {
       A.prep_leaf = true;
+    }
+    // decision trace (cfg.trace, parity tests): the quantities of this leaf's decisions
+    if (cfg.trace != nullptr && writer && c < cfg.trace_chains && leaf_it >= cfg.trace_it0 &&
+        leaf_it < cfg.trace_it0 + cfg.trace_iters && leaf_n < cfg.trace_leaves) {
+      float dmin_sub = INFINITY, dmin_tree = INFINITY;
+#pragma unroll
+      for (int i = 0; i < MAXD; ++i)
+        if (i >= A.imin && i <= A.imax) dmin_sub = fminf(dmin_sub, fminf(turn(i, 0), turn(i, 1)));
+      if (A.done_sub && A.tree_chk && !turning_sub && !A.div_new) dmin_tree = fminf(tree(0), tree(1));
+      const int fl = (A.take_leaf ? NMX_TF_TAKE_LEAF : 0) | (turning_sub ? NMX_TF_TURN_SUB : 0) |
+                     (A.div_new ? NMX_TF_DIVERGE : 0) | (A.done_sub ? NMX_TF_DONE_SUB : 0) |
+                     (A.take_biased ? NMX_TF_TAKE_BIASED : 0) | (S.turning && A.done_sub ? NMX_TF_TURN_TREE : 0) |
+                     (A.iter_done ? NMX_TF_ITER_DONE : 0);
+      float* R = cfg.trace + (((size_t)(leaf_it - cfg.trace_it0) * cfg.trace_chains + c) * cfg.trace_leaves + leaf_n) *
+                                 NMX_TRACE_REC;
+      R[NMX_T_DE] = -A.w_new;
+      R[NMX_T_P_LEAF] = A.p_leaf;
+      R[NMX_T_DOT_SUB] = dmin_sub;
+      R[NMX_T_P_BIASED] = pb_raw;
+      R[NMX_T_DOT_TREE] = dmin_tree;
+      R[NMX_T_FLAGS] = (float)fl;
+      R[NMX_T_PE] = A.pe_eval;
+      R[NMX_T_LEAF] = (float)leaf_n;
     }
   }
   // HMC leaf bookkeeping (_hmc_next, hmc.py:364-414)

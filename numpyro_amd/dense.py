@@ -260,6 +260,65 @@ class PooledCovariance:
         return cov, mean_y + self.shift
 
 
+# ------------------------------------------------------------------ initial matrix as site blocks
+def assemble_inverse_mass_matrix(sites, dense_mass, inverse_mass_matrix):
+    """The initial inverse mass matrix in ravel coordinates from the reference's structural
+    forms (hmc_util.py:439-487 _initialize_mass_matrix, dict branch; hmc.py:759-769 turns a model's
+    dense_mass=True / False into [tuple(sorted(z))] / []): a dict {site group: block} or, with a
+    structured dense_mass, an array (converted to {tuple(sorted(z)): array}).  Dense groups take
+    their block from the dict (in the group's coordinate order) or the identity; the dict's other
+    groups are diagonal blocks (a vector, or the diagonal of a matrix); the remaining sites get
+    ones.  Returns a [D] diagonal when no group is dense, else a [D, D] float64 matrix.  A site in
+    two groups raises the reference's assertion."""
+    import numpy as np
+
+    pos, o = {}, 0
+    for name, shape, _ in sites:
+        n = int(np.prod(shape, dtype=np.int64))
+        pos[name] = (o, n)
+        o += n
+    D = o
+    names = tuple(sorted(pos))
+    if isinstance(dense_mass, bool):
+        dense_mass = [names] if dense_mass else []
+    dense_mass = [tuple(g) for g in dense_mass]
+    imm = inverse_mass_matrix
+    if not isinstance(imm, dict):
+        imm = {names: imm}
+    imm = {tuple(k): v for k, v in imm.items()}
+    groups = list(dense_mass) + [k for k in imm if k not in dense_mass]
+    got = sorted(n for g in groups for n in g)
+    rest = tuple(sorted(set(pos) - set(got)))
+    if sorted(got + list(rest)) != sorted(pos) or len(set(got)) != len(got):
+        raise AssertionError("There seems to be a conflict of sites names specified in the initial "
+                             "`inverse_mass_matrix` and in `dense_mass` argument.")
+    idx = lambda g: np.concatenate([np.arange(pos[n][0], pos[n][0] + pos[n][1]) for n in g])  # noqa: E731
+    full = np.zeros((D, D))
+    for g in groups:
+        ii = idx(g)
+        v = imm.get(g)
+        v = None if v is None else np.asarray(v.cpu() if hasattr(v, "cpu") else v, np.float64)
+        if g in dense_mass:
+            if v is None:
+                v = np.eye(len(ii))
+            elif v.ndim == 1:
+                v = np.diag(v)
+            if v.shape != (len(ii), len(ii)):
+                raise ValueError(f"inverse_mass_matrix block {g} must be [{len(ii)}, {len(ii)}], got {v.shape}")
+            full[np.ix_(ii, ii)] = v
+        else:
+            d = np.ones(len(ii)) if v is None else (np.diag(v) if v.ndim == 2 else v.reshape(-1))
+            if d.shape != (len(ii),):
+                raise ValueError(f"inverse_mass_matrix block {g} must have {len(ii)} diagonal entries")
+            full[ii, ii] = d
+    for n in rest:
+        ii = idx((n,))
+        full[ii, ii] = 1.0
+    if not dense_mass:
+        return torch.from_numpy(np.diag(full).copy())
+    return torch.from_numpy(full)
+
+
 # --------------------------------------------------------------------------------------- per chain
 CHAIN_DENSE_MAX_D = 256
 

@@ -69,7 +69,7 @@ class SamplerOptions:
     num_steps: int | None = None
     regularize_mass_matrix: bool = True
     max_delta_energy: float = 1000.0
-    inverse_mass_matrix: object = None  # diag [D] or None
+    inverse_mass_matrix: object = None  # diag [D], dense [D, D], {site group: block} or None
     # dense pooled adaptation: bytes of window draws buffered per chunk
     dense_adapt_bytes: int = 4 << 30
     # per-chain dense mass: device bytes allowed for the matrices (dense.chain_dense_bytes)
@@ -111,15 +111,27 @@ class Engine:
             raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
                                       "coordinates, the dense engine in whitened ones")
         self.model_potential = potential
+        # the initial inverse mass matrix in ravel coordinates: a dict of site-group blocks, a
+        # structured dense_mass's array, or a matrix for a diagonal mass take the reference's
+        # structural form (hmc_util.py:439-487)
+        imm = opts.inverse_mass_matrix
+        if imm is not None and (isinstance(imm, dict) or opts.dense_blocks or
+                                (not self.dense and torch.as_tensor(imm).dim() == 2)):
+            from .dense import assemble_inverse_mass_matrix
+            structure = opts.dense_blocks if opts.dense_blocks else self.dense
+            imm = assemble_inverse_mass_matrix(potential.sites, structure, imm)
+        self.init_inverse_mass_matrix = imm
         # dense mass: per-chain matrices (the reference's semantics) when they are adapted and
         # fit, one pooled matrix when asked for ("pooled"), one shared whitening when the
-        # matrix is given and not adapted (every chain holds the same one: same semantics)
-        self.chain_dense = self.dense and opts.dense_mass != "pooled" and bool(opts.adapt_mass_matrix)
+        # matrix is given and not adapted (every chain holds the same one: same semantics);
+        # structured blocks are always per chain (each block factored in its own order)
+        self.chain_dense = self.dense and opts.dense_mass != "pooled" and (bool(opts.adapt_mass_matrix)
+                                                                           or bool(opts.dense_blocks))
         self.blocks = None
         if opts.dense_blocks:
             from .dense import MassBlocks
             if not self.chain_dense:
-                raise NotImplementedError("structured dense_mass needs adapt_mass_matrix=True (per-chain blocks)")
+                raise NotImplementedError("structured dense_mass with dense_mass='pooled'")
             self.blocks = MassBlocks(potential.sites, opts.dense_blocks)
         if self.chain_dense:
             from .dense import CHAIN_DENSE_MAX_D, ChainWhitenedPotential, chain_dense_bytes
@@ -158,6 +170,7 @@ class Engine:
         self._mass_cache = None  # dense: (whitening version, HMCAdaptState mass fields)
         # False: collected draws stay unconstrained (MCMC(postprocess_fn=...) maps them itself)
         self.constrain_samples = True
+        self._trace = None  # per-leaf decision trace (set_trace), off by default
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
         # chain-row arena layout for the persistent wide schedule (decided once: the arena's
@@ -241,6 +254,34 @@ class Engine:
         c.collection_size = int(collection_size)
         c.ldc = self.ldc
         c.layout = native.LAYOUT_CHAIN_ROWS if self.crow else native.LAYOUT_CHAIN_MINOR
+        tr = self._trace
+        if tr is None:
+            c.trace, c.trace_chains, c.trace_it0, c.trace_iters, c.trace_leaves = None, 0, 0, 0, 0
+        else:
+            c.trace = ptr(tr["buf"])
+            c.trace_chains, c.trace_it0 = tr["chains"], tr["it0"]
+            c.trace_iters, c.trace_leaves = tr["buf"].shape[0], tr["buf"].shape[2]
+
+    # ------------------------------------------------------------------ decision trace
+    def set_trace(self, chains: int, it0: int, iters: int):
+        """Record the per-leaf decision quantities (nmx_nuts_config.trace, enum nmx_trace_field)
+        of arena chains [0, chains) for transitions [it0, it0 + iters) of later runs; results do
+        not change.  Used by the parity tests and bench.py's parity legs to locate the leaf at
+        which a device transition first parts from the oracle's (oracle/parity.py)."""
+        if chains <= 0 or iters <= 0:
+            self._trace = None
+            return
+        leaves = 1 << self.md
+        buf = torch.full((int(iters), min(int(chains), self.C), leaves, native.TRACE_REC), float("nan"),
+                         dtype=torch.float32, device=self.device)
+        self._trace = {"buf": buf, "chains": buf.shape[1], "it0": int(it0)}
+
+    def trace_records(self):
+        """The decision trace as a float32 numpy array [iters, chains, leaves, TRACE_REC] (NaN:
+        no leaf recorded), or None."""
+        if self._trace is None:
+            return None
+        return self._trace["buf"].cpu().numpy()
 
     # ------------------------------------------------------------------ phases
     def initialize(self, seed: int, num_warmup: int, init_params=None, radius: float = 2.0,
@@ -254,7 +295,7 @@ class Engine:
         self.num_warmup = int(num_warmup)
         self._alloc(self.iter_capacity)
         self._fill_cfg(0, 0, num_warmup, seed, 0, 1, 0)
-        imm = self.opts.inverse_mass_matrix
+        imm = self.init_inverse_mass_matrix
         imm_t = None
         if self.dense:
             # chains are initialised in model coordinates (w = z), then re-expressed

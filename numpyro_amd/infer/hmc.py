@@ -147,6 +147,13 @@ class MCMCKernel:
         return ""
 
 
+def _args_key(model_args, model_kwargs):
+    """Identity of the model arguments an engine's potential is bound to (MCMC._get_engine keys
+    its engine the same way)."""
+    return (tuple(id(a) for a in (model_args or ())),
+            tuple(sorted((k, id(v)) for k, v in (model_kwargs or {}).items())))
+
+
 def init_to_uniform(site=None, radius=2):
     """Marker for the default init strategy (numpyro/infer/initialization.py:95-129)."""
     return ("uniform", float(radius))
@@ -187,9 +194,8 @@ class HMC(MCMCKernel):
             dense_mass = [tuple(g) for g in dense_mass]
             if not all(len(g) > 0 and all(isinstance(n, str) for n in g) for g in dense_mass):
                 raise ValueError("dense_mass as a list holds tuples of site names, e.g. [('x', 'y')]")
-            if isinstance(inverse_mass_matrix, dict):
-                raise NotImplementedError("an inverse_mass_matrix dict of blocks: the blocks are adapted from "
-                                          "identity here; pass adapt_mass_matrix=True without inverse_mass_matrix")
+        # an inverse_mass_matrix dict {site group: block} (hmc_util.py:439-487) is assembled in
+        # ravel coordinates by the engine (dense.assemble_inverse_mass_matrix)
         if model is not None and not (isinstance(model, FusedModel) or callable(model)):
             raise TypeError("`model` must be a model function (numpyro_amd.sample / plate / distributions, "
                             "mapped onto a fused kernel by numpyro_amd.frontend) or a fused model")
@@ -302,6 +308,7 @@ class HMC(MCMCKernel):
         with torch.cuda.device(eng.device):
             eng.initialize(seed, int(num_warmup), init_params=ip, radius=self.init_radius())
         self._engine, self._seed = eng, seed
+        self._engine_args = _args_key(model_args, model_kwargs)
         self._sample_fn = self.sample
         return snapshot_state(eng, seed, keep_arena=False)
 
@@ -317,11 +324,14 @@ class HMC(MCMCKernel):
             if getattr(state, "_layout", None) is None:
                 raise ValueError("state must come from init() or sample() of this kernel")
             # an unpickled state: resumed by an engine of this kernel for these model args
+            # (the engine's bound data must be these model args: same layout is not enough)
             eng = getattr(self, "_engine", None)
-            if eng is None or eng.layout() != state._layout:
+            if (eng is None or eng.layout() != state._layout
+                    or getattr(self, "_engine_args", None) != _args_key(model_args, model_kwargs)):
                 C, chain_offset = state._layout[1], state._layout[4]
                 eng = self.make_engine(C, model_args, model_kwargs, chain_offset=chain_offset)
                 self._engine = eng
+                self._engine_args = _args_key(model_args, model_kwargs)
         with torch.cuda.device(eng.device):
             restore_state(eng, state)
             eng.run(1, state.adapt_state.rng_key, collection_size=0)
@@ -351,6 +361,7 @@ class HMC(MCMCKernel):
         state = self.__dict__.copy()
         state["_sample_fn"] = None
         state["_engine"] = None
+        state["_engine_args"] = None
         if self._model is not None:  # rebuilt from the model and its args by potential()
             state["_potential"] = None
         return state

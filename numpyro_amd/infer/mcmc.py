@@ -25,6 +25,23 @@ _FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
 from ..shard import shard_chains  # noqa: E402  (re-exported: contiguous chain shard per rank)
 
 
+def _postprocess_per_draw(fn, sites):
+    """postprocess_fn applied to each draw's site dict ({site: [*shape]}), as the reference's
+    fori_collect does per iteration (util.py:277-407 _collect_and_postprocess, vmapped over
+    chains when vectorized, mcmc.py:422-442): vectorized over the C x S draws by torch.func.vmap,
+    or one call per draw when fn cannot be vmapped (e.g. it converts to Python numbers).
+    sites: {site: [C, S, *shape]} -> {name: [C, S, *out_shape]}."""
+    v0 = next(iter(sites.values()))
+    C, S = int(v0.shape[0]), int(v0.shape[1])
+    flat = {k: v.reshape(C * S, *v.shape[2:]) for k, v in sites.items()}
+    try:
+        res = dict(torch.func.vmap(fn)(flat))
+    except Exception:  # noqa: BLE001  (not vmappable: per draw)
+        rows = [dict(fn({k: v[i] for k, v in flat.items()})) for i in range(C * S)]
+        res = {k: torch.stack([torch.as_tensor(r[k], device=v0.device) for r in rows]) for k in rows[0]} if rows else {}
+    return {k: torch.as_tensor(v).reshape(C, S, *torch.as_tensor(v).shape[1:]) for k, v in res.items()}
+
+
 class MCMC:
     def __init__(self, sampler, *, num_warmup, num_samples, num_chains=1, thinning=1,
                  postprocess_fn=None, chain_method="parallel", progress_bar=True,
@@ -41,8 +58,8 @@ class MCMC:
         self.thinning = thinning
         # postprocess_fn (mcmc.py:331,345,422-442): maps a dict of unconstrained site values to
         # the collected values; None = the sampler's (constrain + deterministic sites, done on
-        # the device and by the potential).  Applied to the batch of draws [chains, draws, ...]
-        # (the reference vmaps it over chains, mcmc.py:425-433)
+        # the device and by the potential).  Applied per draw on site-shaped values, as the
+        # reference's fori_collect does (_postprocess_per_draw)
         self.postprocess_fn = postprocess_fn
         if not callable(chain_method) and chain_method not in ("parallel", "vectorized", "sequential"):
             raise ValueError('Only supporting the following methods to draw chains: "sequential", '
@@ -184,7 +201,7 @@ class MCMC:
         if self.postprocess_fn is not None:
             # draws are unconstrained here (Engine.constrain_samples = False)
             names = set(out)
-            out = dict(self.postprocess_fn(out))
+            out = _postprocess_per_draw(self.postprocess_fn, out)
             if not include_deterministic:  # print_summary keeps the sample sites (mcmc.py:748-758)
                 out = {k: v for k, v in out.items() if k in names}
         elif include_deterministic:

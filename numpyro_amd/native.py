@@ -79,7 +79,16 @@ class NutsConfig(ctypes.Structure):
         ("collect_start", ctypes.c_int32), ("collect_thinning", ctypes.c_int32),
         ("collection_size", ctypes.c_int32), ("ldc", ctypes.c_int32), ("parity", ctypes.c_int32),
         ("layout", ctypes.c_int32), ("num_groups", ctypes.c_int32), ("group", ctypes.c_int32),
+        ("trace_chains", ctypes.c_int32), ("trace_it0", ctypes.c_int32), ("trace_iters", ctypes.c_int32),
+        ("trace_leaves", ctypes.c_int32), ("trace", c_vp),
     ]
+
+
+# per-leaf decision trace (nmx_nuts_config.trace): record layout and flag bits
+TRACE_REC = 8  # NMX_TRACE_REC
+TRACE_FIELDS = ["dE", "p_leaf", "dot_sub", "p_biased", "dot_tree", "flags", "pe", "leaf"]  # enum nmx_trace_field
+TF_TAKE_LEAF, TF_TURN_SUB, TF_DIVERGE, TF_DONE_SUB, TF_TAKE_BIASED, TF_TURN_TREE, TF_ITER_DONE = (
+    1, 2, 4, 8, 16, 32, 64)  # enum nmx_trace_flag
 
 
 LAYOUT_CHAIN_MINOR, LAYOUT_CHAIN_ROWS = 0, 1  # enum nmx_layout

@@ -32,17 +32,27 @@ class Potential:
     dim: int = 0
 
     def bind(self, num_chains: int, ldc: int, device) -> None:
-        before = set(self.__dict__)
+        before = dict(self.__dict__)
         self.num_chains, self.ldc, self.device = num_chains, ldc, torch.device(device)
         self._codes = None
         self._bind(num_chains, ldc, self.device)
-        # attributes made by binding (device copies of the data, workspaces) are not pickled:
-        # an unpickled potential is unbound and binds again on its engine
-        self._bound_keys = getattr(self, "_bound_keys", set()) | (set(self.__dict__) - before)
+        # what binding made or replaced (device copies of the data, workspaces, whitening) is not
+        # pickled: attributes binding created are dropped, attributes it replaced (e.g. a
+        # `packed = None` set in __init__) go back to their unbound value, so an unpickled
+        # potential is unbound and binds again on its engine
+        made = set(self.__dict__) - set(before)
+        replaced = {k: v for k, v in before.items() if k in self.__dict__ and self.__dict__[k] is not v
+                    and k not in ("num_chains", "ldc", "device", "_codes")}
+        self._bound_keys = getattr(self, "_bound_keys", set()) | made
+        unbound = getattr(self, "_unbound_values", {})
+        for k, v in replaced.items():
+            unbound.setdefault(k, v)
+        self._unbound_values = unbound
 
     def __getstate__(self):
-        drop = getattr(self, "_bound_keys", set()) | {"_bound_keys"}
-        return {k: v for k, v in self.__dict__.items() if k not in drop}
+        drop = getattr(self, "_bound_keys", set()) | {"_bound_keys", "_unbound_values"}
+        unbound = getattr(self, "_unbound_values", {})
+        return {k: unbound.get(k, v) for k, v in self.__dict__.items() if k not in drop}
 
     def _bind(self, num_chains, ldc, device):
         pass

@@ -113,7 +113,8 @@ def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, r
     here.  With `deadline` (a time.perf_counter() value) a chain starts no further transition
     once it has passed (chains run on continuously until then, so the batch stays full: the
     CPU comparator's fixed-batch mode).  With `record`, every history entry is (state,
-    decisions of that transition: (kind, margin) list, see hmc_ref.record_decisions).  `stats`
+    decisions of that transition: (kind, margin) list, see hmc_ref.record_decisions, per-leaf
+    records, see hmc_ref.record_leaves and oracle/parity.py).  `stats`
     (a dict) receives the seconds spent inside the batched potential ("pot_s").
     Returns (final states, per-chain list of states, potential evaluations, batched calls)."""
     n = len(states)
@@ -133,10 +134,13 @@ def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, r
                 if deadline is not None and time.perf_counter() >= deadline:
                     break
                 log = [] if record else None
+                leaves = [] if record else None
                 H.record_decisions(log)
+                H.record_leaves(leaves)
                 st = o.sample(st)
-                hist[k].append((st, log) if record else st)
+                hist[k].append((st, log, leaves) if record else st)
             H.record_decisions(None)
+            H.record_leaves(None)
             out[k] = st
         except Exception as e:  # noqa: BLE001
             errs.append(e)
@@ -195,7 +199,7 @@ def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, dev
         transitions += T
         bad = None
         for t in range(T):
-            st, log = h[t]
+            st, log = h[t][:2]
             z = np.asarray(st.z, np.float64) if to_model is None else np.asarray(to_model(st.z), np.float64)
             ref = np.asarray(dev_z[c, t], np.float64)
             dz = float(np.max(np.abs(z - ref) - rtol * np.abs(ref)))

@@ -45,6 +45,42 @@ def record_decisions(log):
     _TLS.decisions = log
 
 
+def record_leaves(log):
+    """Append one record per NUTS leaf of this thread's trajectories to `log` (a list of dicts,
+    the oracle side of the device's decision trace, nmx_nuts_config.trace), or stop (None).
+    A record holds the leaf's delta energy, the in-subtree transition probability and its
+    uniform, the smallest iterative U-turn dot checked at the leaf with the magnitude of its
+    terms, and, at a subtree end, the biased transition probability, its uniform and the
+    whole-tree dot; plus the decisions taken (oracle/parity.py compares them leaf by leaf)."""
+    _TLS.leaves = log
+
+
+def _leaf_log():
+    return getattr(_TLS, "leaves", None)
+
+
+def _angles_scale(inverse_mass_matrix, r_left, r_right, r_sum):
+    """(left dot, right dot, scale of each): _momentum_angle's dots and the sums of the
+    magnitudes of their terms (the size of their f32 rounding)."""
+    v_l = kinetic_grad(inverse_mass_matrix, r_left)
+    v_r = kinetic_grad(inverse_mass_matrix, r_right)
+    rs = r_sum - (r_left + r_right) / r_sum.dtype.type(2)
+    return (float(np.dot(v_l, rs)), float(np.dot(v_r, rs)),
+            float(np.dot(np.abs(v_l).astype(np.float64), np.abs(rs))),
+            float(np.dot(np.abs(v_r).astype(np.float64), np.abs(rs))))
+
+
+def _min_dot(pairs):
+    """(min dot, its scale) over (dot_l, dot_r, scale_l, scale_r) tuples; (inf, 0) if none."""
+    best, sc = math.inf, 0.0
+    for dl, dr, sl, sr in pairs:
+        if dl < best:
+            best, sc = dl, sl
+        if dr < best:
+            best, sc = dr, sr
+    return best, sc
+
+
 # A decision is a rounding-level tie when device and oracle can order it differently: the
 # two compute in f32 with different summation orders (potential, kinetic energy, U-turn
 # dots), so energies differ by ~1e-6 relative (dE by ~1e-4 absolute for |E| ~ 1e2-1e3) and
@@ -436,13 +472,19 @@ def _combine_tree(current_tree, new_tree, inverse_mass_matrix, going_right, u, b
     if biased_transition:  # :756-764, :795-799
         with np.errstate(over="ignore"):
             transition_prob = np.exp(new_tree.weight - current_tree.weight)
+        p_raw = transition_prob if np.isnan(transition_prob) else min(transition_prob, dt(1.0))
         transition_prob = dt(0.0) if (new_tree.turning or new_tree.diverging) else min(
             transition_prob, dt(1.0))
         turning = new_tree.turning or _is_turning(inverse_mass_matrix, r_left, r_right, r_sum)
+        if _leaf_log() is not None:
+            _TLS.last_combine = (float(p_raw), float(u),
+                                 _angles_scale(inverse_mass_matrix, r_left, r_right, r_sum))
     else:  # :749-753
         with np.errstate(over="ignore"):
             transition_prob = dt(1.0) / (dt(1.0) + np.exp(-(new_tree.weight - current_tree.weight)))
         turning = current_tree.turning
+        if _leaf_log() is not None:
+            _TLS.last_combine = (float(transition_prob), float(u), None)
     transition = bool(u < transition_prob)
     if 0.0 < transition_prob < 1.0:
         _log("transition", abs(u - transition_prob))
@@ -476,15 +518,34 @@ def _iterative_build_subtree(prototype_tree, vv_update, kinetic_fn, inverse_mass
         leaf_idx = tree.num_proposals
         if tree.num_proposals == 0:
             new_tree = new_leaf
+            p_leaf, u_leaf, take = -1.0, math.nan, True
         else:
             new_tree = _combine_tree(tree, new_leaf, inverse_mass_matrix, going_right,
                                      rng.leaf(j, leaf_idx), False)
+            if _leaf_log() is not None:
+                p_leaf, u_leaf, _ = _TLS.last_combine
+                take = bool(u_leaf < p_leaf)
         ckpt_idx_min, ckpt_idx_max = _leaf_idx_to_ckpt_idxs(leaf_idx)
         if leaf_idx % 2 == 0:
             r_ckpts[ckpt_idx_max] = new_leaf.r_right
             r_sum_ckpts[ckpt_idx_max] = new_tree.r_sum
         turning = _is_iterative_turning(inverse_mass_matrix, new_leaf.r_right, new_tree.r_sum,
                                         r_ckpts, r_sum_ckpts, ckpt_idx_min, ckpt_idx_max)
+        log = _leaf_log()
+        if log is not None:
+            # every checkpoint dot of the leaf (the loop above stops at the first turning one)
+            pairs = [_angles_scale(inverse_mass_matrix, np.atleast_1d(r_ckpts[i]), np.atleast_1d(new_leaf.r_right),
+                                   np.atleast_1d(new_tree.r_sum) - np.atleast_1d(r_sum_ckpts[i])
+                                   + np.atleast_1d(r_ckpts[i]))
+                     for i in range(ckpt_idx_min, ckpt_idx_max + 1)]
+            dmin, dscale = _min_dot(pairs)
+            n = new_tree.num_proposals
+            log.append({"dE": -float(new_leaf.weight), "p_leaf": float(p_leaf), "u_leaf": float(u_leaf),
+                        "take_leaf": take, "dot_sub": dmin, "scale_sub": dscale, "turn_sub": bool(turning),
+                        "diverge": bool(new_leaf.diverging), "pe": float(new_leaf.z_proposal_pe),
+                        "done_sub": bool(n >= max_num_proposals or turning or new_tree.diverging),
+                        "p_biased": -1.0, "u_biased": math.nan, "dot_tree": math.inf, "scale_tree": 0.0,
+                        "take_biased": False, "turn_tree": False, "iter_done": False, "depth": prototype_tree.depth})
         tree = new_tree
     return tree._replace(depth=prototype_tree.depth, turning=turning)
 
@@ -511,6 +572,16 @@ def build_tree(verlet_update, kinetic_fn, verlet_state, inverse_mass_matrix, ste
                                             step_size, going_right, rng, j, energy_current,
                                             max_delta_energy, r_ckpts, r_sum_ckpts)
         tree = _combine_tree(tree, new_tree, inverse_mass_matrix, going_right, rng.biased(j), True)
+        log = _leaf_log()
+        if log:  # the subtree's last leaf carries the subtree-end decisions
+            p_raw, u_b, ang = _TLS.last_combine
+            rec = log[-1]
+            rec["p_biased"], rec["u_biased"] = p_raw, u_b
+            rec["take_biased"] = bool(u_b < (0.0 if (new_tree.turning or new_tree.diverging) else p_raw))
+            rec["turn_tree"] = bool(tree.turning)
+            if new_tree.num_proposals == 2 ** j and not new_tree.turning and not new_tree.diverging:
+                rec["dot_tree"], rec["scale_tree"] = _min_dot([ang])
+            rec["iter_done"] = bool(tree.depth >= max_tree_depth_current or tree.turning or tree.diverging)
     return tree
 
 

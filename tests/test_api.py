@@ -209,3 +209,30 @@ def test_mass_blocks_structure():
     assert NUTS(P.eight_schools, dense_mass=[]).options().dense_mass is False
     o = NUTS(P.eight_schools, dense_mass=[("theta", "mu")]).options()
     assert o.dense_mass is True and o.dense_blocks == [("theta", "mu")]
+
+
+def test_postprocess_fn_is_applied_per_draw():
+    """MCMC(postprocess_fn=fn): fn sees one draw's site values (site-shaped, as the reference's
+    fori_collect passes them), so reducing / indexing / reshaping functions give per-draw
+    results; a function that cannot be vmapped runs once per draw."""
+    import torch
+
+    from numpyro_amd.infer.mcmc import _postprocess_per_draw
+
+    C, S = 3, 4
+    g = torch.Generator().manual_seed(0)
+    sites = {"theta": torch.randn(C, S, 8, generator=g), "mu": torch.randn(C, S, generator=g)}
+
+    def fn(z):
+        return {"s": z["theta"].sum(), "first": z["theta"][0], "m": z["theta"].reshape(2, 4) * z["mu"]}
+
+    out = _postprocess_per_draw(fn, sites)
+    assert out["s"].shape == (C, S) and out["first"].shape == (C, S) and out["m"].shape == (C, S, 2, 4)
+    torch.testing.assert_close(out["s"], sites["theta"].sum(-1))
+    torch.testing.assert_close(out["first"], sites["theta"][..., 0])
+    torch.testing.assert_close(out["m"], sites["theta"].reshape(C, S, 2, 4) * sites["mu"][..., None, None])
+
+    def py(z):  # .item(): not vmappable
+        return {"s": torch.tensor(float(z["theta"].sum().item()))}
+
+    torch.testing.assert_close(_postprocess_per_draw(py, sites)["s"], sites["theta"].sum(-1))

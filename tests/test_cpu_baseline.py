@@ -80,8 +80,9 @@ def test_fixed_batch_mode_and_path_comparison():
     t0 = time.perf_counter()
     _, hist, evals, _ = CB.run_chains(rowwise, states, oracles, 1 << 30, deadline=t0 + 0.5, record=True)
     assert all(len(h) >= 2 for h in hist) and evals > 0
-    st, log = hist[0][0]
+    st, log, leaves = hist[0][0]
     assert isinstance(log, list) and all(k in H.TIE for k, _ in log)
+    assert len(leaves) == st.num_steps and leaves[-1]["iter_done"]
     T = min(len(h) for h in hist)
     ns = np.array([[h[t][0].num_steps for t in range(T)] for h in hist])
     zs = np.array([[h[t][0].z for t in range(T)] for h in hist], np.float64)

@@ -1,0 +1,115 @@
+"""The first-parting-leaf parity machinery (oracle/parity.py) on oracle-vs-oracle runs: two
+oracle runs whose potentials differ by a rounding-sized perturbation part only at decisions
+the leaf energies explain, and a decision flipped far from its tie is reported as not
+explained (the check has teeth).  The device side of these records is nmx_nuts_config.trace
+(tests/test_gpu_parity_trace.py)."""
+import numpy as np
+
+from oracle import cpu_batched as CB
+from oracle import hmc_ref as H
+from oracle import parity as PR
+from oracle import philox
+from oracle import potentials as OP
+
+
+def _case(N=400, D=6, seed=11):
+    rs = np.random.RandomState(seed)
+    X = rs.randn(N, D).astype(np.float32)
+    beta = rs.randn(D) * 0.4
+    y = (rs.rand(N) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
+    return OP.LogisticRegression(X, y, dtype=np.float32), D
+
+
+def _run(pe_grad, D, n, seed, T, step):
+    states, oracles = [], []
+    for c in range(n):
+        o = H.NUTSOracle(pe_grad, D, 0, step_size=step, adapt_step_size=False, adapt_mass_matrix=False)
+        states.append(o.init(philox.init_uniform(seed, c, 0, D) * np.float32(0.1), seed, c))
+        oracles.append(H.NUTSOracle(None, D, 0, step_size=step, adapt_step_size=False, adapt_mass_matrix=False))
+
+    def batch(Z):
+        out = [pe_grad(z) for z in Z]
+        return np.array([o[0] for o in out], np.float32), np.stack([o[1] for o in out])
+
+    _, hist, _, _ = CB.run_chains(batch, states, oracles, T, record=True)
+    return hist
+
+
+def _as_device(hist, T, L=1024):
+    n = len(hist)
+    tr = np.full((T, n, L, 8), np.nan, np.float32)
+    ns = np.zeros((n, T), np.int64)
+    z = np.zeros((n, T, hist[0][0][0].z.shape[0]))
+    for c, h in enumerate(hist):
+        for t in range(T):
+            st, _, leaves = h[t]
+            tr[t, c] = PR.oracle_to_trace(leaves, L)
+            ns[c, t] = st.num_steps
+            z[c, t] = st.z
+    return tr, ns, z
+
+
+def test_leaf_records_follow_the_tree():
+    ref, D = _case()
+    hist = _run(ref.pe_grad, D, 4, 3, 3, 0.05)
+    for h in hist:
+        for st, _, leaves in h:
+            assert len(leaves) == st.num_steps
+            assert leaves[-1]["iter_done"] and not any(r["iter_done"] for r in leaves[:-1])
+            # subtree ends: sizes 1, 2, 4, ... (or cut short by a U-turn / divergence)
+            ends = [i for i, r in enumerate(leaves) if r["done_sub"]]
+            assert ends[0] == 0 and all(r["p_leaf"] == -1.0 for r in leaves[:1])
+
+
+def test_identical_runs_match_leaf_for_leaf():
+    ref, D = _case()
+    T = 3
+    hist = _run(ref.pe_grad, D, 6, 5, T, 0.05)
+    tr, ns, z = _as_device(hist, T)
+    par = PR.compare_traced(hist, tr, ns, z, atol=0.0)
+    assert par["matched"] == 6 and not par["mismatches"] and par["max_dE_err"] == 0.0
+    for c, h in enumerate(hist):
+        for t in range(T):
+            assert PR.locate(tr[t, c], h[t][2]) is None
+
+
+def test_energy_perturbation_parts_only_at_explained_leaves():
+    """Every leaf energy perturbed by a deterministic function of the position of size <= 5e-3
+    (gradients untouched, so the trajectories stay the same): transition probabilities move by
+    up to ~1e-3, some chains part, and each must do so at a leaf where the shared uniform falls
+    between the two probabilities, within the bound the measured leaf-energy discrepancy
+    allows."""
+    ref, D = _case(N=600)
+
+    def perturbed(z):
+        u, g = ref.pe_grad(z)
+        return np.float32(u + np.float32(5e-3) * np.float32(np.sin(1e4 * float(z[0]) + 3e3 * float(z[1])))), g
+
+    T, n = 8, 32
+    a = _run(ref.pe_grad, D, n, 9, T, 0.08)
+    b = _run(perturbed, D, n, 9, T, 0.08)
+    tr, ns, z = _as_device(b, T)
+    par = PR.compare_traced(a, tr, ns, z, atol=0.0)
+    for m in par["mismatches"]:
+        print(PR.describe(m))
+    assert 0 < par["max_dE_err"] <= 1.1e-2  # two perturbed energies per dE
+    assert par["mismatches"], "the perturbation flipped no decision: the test would be vacuous"
+    assert all(m["explained"] for m in par["mismatches"]), par["mismatches"]
+
+
+def test_flip_far_from_a_tie_is_not_explained():
+    ref, D = _case()
+    hist = _run(ref.pe_grad, D, 4, 7, 2, 0.05)
+    for c, h in enumerate(hist):
+        leaves = h[0][2]
+        # a leaf with an in-subtree transition whose uniform is far from its probability
+        cand = [i for i, r in enumerate(leaves) if r["p_leaf"] >= 0 and abs(r["u_leaf"] - r["p_leaf"]) > 0.05]
+        if not cand:
+            continue
+        i = cand[0]
+        dev = PR.oracle_to_trace(leaves, 1024)
+        dev[i, PR.T_FLAGS] = float(int(dev[i, PR.T_FLAGS]) ^ PR.TF_TAKE_LEAF)
+        loc = PR.locate(dev, leaves)
+        assert loc["leaf"] == i and loc["kind"] == "take_leaf" and not loc["explained"]
+        return
+    raise AssertionError("no leaf with a clear transition decision")
