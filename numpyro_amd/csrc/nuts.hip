@@ -2787,12 +2787,16 @@ extern "C" int nmx_nuts_step_wide_model(const nmx_nuts_config* cfg, void* arena,
 
 namespace {
 // threads per chain of the persistent wide kernel, from dim only (the sums' order depends on
-// it; NMX_PERSIST_NT overrides for kernel experiments)
+// it).  The NMX_PERSIST_NT environment override for kernel experiments exists only in the debug
+// build and in experiment builds (-DNMX_EXPERIMENT, scripts/ab_build.py): the release library's
+// results never depend on the environment.
 int persist_nt(int dim) {
+#if defined(NMX_DEBUG) || defined(NMX_EXPERIMENT)
   if (const char* e = getenv("NMX_PERSIST_NT")) {
     const int v = atoi(e);
     if (v == 128 || v == 256 || v == 512 || v == 1024) return v;
   }
+#endif
   // SV (D = 2519): 256 -> 13.1M leapfrog/s at 8192 chains, 512 -> 9.6M; funnel-10k: 512 -> 5.1M,
   // 256 -> 4.7M (profiles/r03/ab_persistent_nt.txt)
   return dim <= 4096 ? 256 : 512;

@@ -238,7 +238,15 @@ class PooledCovariance:
         self.s1 += y.sum(1)
         self.s2 += y @ y.t()
 
-    def all_reduce(self):
+    def all_reduce(self, group=None):
+        """Sum the moments over ranks: torch.distributed ranks, or the devices of one process
+        (group = (shard.DeviceGroup, rank))."""
+        if group is not None:
+            g, rank = group
+            n = torch.tensor([float(self.n)], dtype=torch.float64, device=self.s1.device)
+            n, self.s1, self.s2 = g.all_reduce_sum(rank, [n, self.s1, self.s2])
+            self.n = int(round(float(n.item())))
+            return
         dist = torch.distributed
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             n = torch.tensor([float(self.n)], dtype=torch.float64, device=self.s1.device)

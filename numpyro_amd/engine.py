@@ -171,6 +171,9 @@ class Engine:
         # False: collected draws stay unconstrained (MCMC(postprocess_fn=...) maps them itself)
         self.constrain_samples = True
         self._trace = None  # per-leaf decision trace (set_trace), off by default
+        # (shard.DeviceGroup, rank) when this engine is one device of a process's multi-device
+        # run (MCMC chain_method="parallel"): pooled dense moments are summed over the group
+        self.device_group = None
         self.cfg = NutsConfig()
         self.potential.bind(self.C, self.ldc, self.device)
         # chain-row arena layout for the persistent wide schedule (decided once: the arena's
@@ -553,7 +556,7 @@ class Engine:
                 if self.chain_dense:
                     cov, mean = pool.finalize(self.opts.regularize_mass_matrix, self.blocks), None
                 else:
-                    pool.all_reduce()
+                    pool.all_reduce(self.device_group)
                     cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
                 self._pool = None
                 self._reexpress(cov, mean, s)

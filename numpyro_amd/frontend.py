@@ -350,6 +350,17 @@ def eval_sym(x, values):
     raise NotImplementedError(f"deterministic expression with operation {x.op!r}")
 
 
+def _check_sym(x, name):
+    """Raise NotImplementedError at model-mapping time for an expression eval_sym cannot evaluate."""
+    if not isinstance(x, Sym) or x.op == "latent":
+        return
+    if x.op not in _SYM_UNARY and x.op not in _SYM_BINARY and x.op != "matmul":
+        raise NotImplementedError(f"deterministic site {name!r}: operation {x.op!r} is not supported "
+                                  f"(supported: {sorted(_SYM_UNARY) + sorted(_SYM_BINARY) + ['matmul']})")
+    for a in x.args:
+        _check_sym(a, name)
+
+
 def _with_traced_deterministics(pot, trace):
     """The model's own numpyro.deterministic sites (primitives.py:293-314) come back with the
     samples (MCMC.get_samples, postprocess_fn), evaluated from the traced expressions after
@@ -357,14 +368,26 @@ def _with_traced_deterministics(pot, trace):
     dets = dict(trace.deterministics)
     if not dets:
         return pot
+    for name, expr in dets.items():  # unsupported operations fail here, not after sampling
+        _check_sym(expr, name)
     base = pot.deterministic
+    site_shape = {n: tuple(s) for n, s, _ in pot.sites}
 
     def deterministic(sites):
+        import torch
+
         out = base(sites)
         vals = dict(sites)
         vals.update(out)
+        n0 = next(n for n in sites if n in site_shape)
+        v0 = sites[n0]
+        batch = tuple(v0.shape[:v0.dim() - len(site_shape[n0])])
         for name, expr in dets.items():
             v = eval_sym(expr, vals)
+            # a constant (or batch-free) expression still has one value per draw
+            ev = tuple(shape_of(expr)) if isinstance(expr, Sym) else tuple(torch.as_tensor(v).shape)
+            if tuple(v.shape) != batch + ev:
+                v = v.expand(*batch, *ev).clone()
             out[name] = v
             vals[name] = v
         return out

@@ -46,7 +46,7 @@ class MCMC:
     def __init__(self, sampler, *, num_warmup, num_samples, num_chains=1, thinning=1,
                  postprocess_fn=None, chain_method="parallel", progress_bar=True,
                  jit_model_args=False, device=None, sync_chains=False, chain_offset=None,
-                 poll_every=16):
+                 poll_every=16, devices=None):
         self.sampler = sampler
         self._sample_field = sampler.sample_field
         self._default_fields = sampler.default_fields
@@ -67,6 +67,11 @@ class MCMC:
         self.chain_method = chain_method
         self.progress_bar = progress_bar
         self.device = device
+        # chain_method="parallel" (the reference's default: pmap over local devices,
+        # mcmc.py:700-715) or a callable (pmap-of-vectorized, mcmc.py:296-320) shards the chains
+        # of this process over `devices` (default: every visible GPU when there are several and
+        # torch.distributed is not running), one engine and one host thread per device
+        self.devices = None if devices is None else [torch.device(d) for d in devices]
         self.sync_chains = sync_chains
         self.poll_every = int(poll_every)
         # chain shard of this process
@@ -81,6 +86,7 @@ class MCMC:
             self.chain_lo, self.chain_hi, self.local_chains = 0, self.num_chains, self.num_chains
         self._engine = None
         self._engine_key = None
+        self._engines = None  # multi-device run: one engine per device (chain shards)
         self._warmup_state = None
         self._last_state = None
         self._samples = None
@@ -94,10 +100,54 @@ class MCMC:
     def _get_engine(self, args, kwargs):
         key = (id(self.sampler), tuple(id(a) for a in args), tuple(sorted((k, id(v)) for k, v in kwargs.items())))
         if self._engine is None or self._engine_key != key:
-            self._engine = self.sampler.make_engine(self.local_chains, args, kwargs, device=self.device,
+            dev = self.device if self.device is not None or not self.devices else self.devices[0]
+            self._engine = self.sampler.make_engine(self.local_chains, args, kwargs, device=dev,
                                                     chain_offset=self.chain_lo, sync_chains=self.sync_chains)
             self._engine_key = key
         return self._engine
+
+    def _run_devices(self):
+        """Devices of a multi-device run of this process's chains, or None (one engine)."""
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            return None  # one process per GPU: this rank's shard lives on its device
+        if self.devices is not None:
+            devs = self.devices
+        elif (self.chain_method == "parallel" or callable(self.chain_method)) and self.device is None:
+            n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+            devs = [torch.device("cuda", i) for i in range(n)]
+        else:
+            return None
+        devs = devs[:max(1, self.local_chains)]
+        return devs if len(devs) > 1 else None
+
+    def _get_engines(self, args, kwargs, devs):
+        import pickle
+
+        from .hmc import _args_key
+
+        key = (id(self.sampler), _args_key(args, kwargs), tuple(str(d) for d in devs))
+        if self._engines is None or self._engine_key != key:
+            engines = []
+            pot_fn = getattr(self.sampler, "_potential_fn", None)
+            for g, dev in enumerate(devs):
+                lo, hi = shard_chains(self.local_chains, g, len(devs))
+                if pot_fn is not None and g > 0:
+                    # a user potential object binds to one device: the other shards get copies
+                    # (a pickled potential is unbound)
+                    from ..engine import Engine
+
+                    eng = Engine(pickle.loads(pickle.dumps(pot_fn)), hi - lo, self.sampler.options(), device=dev,
+                                 chain_offset=self.chain_lo + lo, sync_chains=self.sync_chains)
+                else:
+                    eng = self.sampler.make_engine(hi - lo, args, kwargs, device=dev, chain_offset=self.chain_lo + lo,
+                                                   sync_chains=self.sync_chains)
+                engines.append(eng)
+            group = shard.DeviceGroup(len(engines))
+            for g, eng in enumerate(engines):
+                eng.device_group = (group, g)
+            self._engines, self._engine_key = engines, key
+            self._engine = engines[0]
+        return self._engines
 
     # ------------------------------------------------------------------ state
     @property
@@ -148,6 +198,9 @@ class MCMC:
                                  f"available: {native.COLLECT}")
         self._collected = tuple(collect)
         seed = key_to_seed(rng_key)
+        devs = self._run_devices()
+        if devs is not None:
+            return self._run_multi(devs, seed, args, kwargs, init_params, n_iter, lower, resume)
         eng = self._get_engine(args, kwargs)
         self._args, self._kwargs = tuple(args), dict(kwargs)
         eng.constrain_samples = self.postprocess_fn is None
@@ -181,6 +234,76 @@ class MCMC:
                                    "iterations": n_iter}
         self._samples, self._fields = samples, fields
         self._last_state = self._snapshot(eng, seed)
+
+    def _run_multi(self, devs, seed, args, kwargs, init_params, n_iter, lower, resume):
+        """The chains sharded over `devs` (contiguous global chain ids, like the torchrun ranks),
+        each shard's engine driven by its own host thread (the library calls release the GIL),
+        draws and fields gathered to the first device in global chain order."""
+        import threading
+        import time
+
+        engines = self._get_engines(args, kwargs, devs)
+        self._args, self._kwargs = tuple(args), dict(kwargs)
+        G = len(engines)
+        ip_all = None
+        if resume is None and init_params is not None:
+            ip_all = init_params
+            if isinstance(ip_all, dict):
+                ip_all = engines[0].potential.flatten(ip_all)
+            ip_all = torch.as_tensor(ip_all, dtype=torch.float32)
+            if ip_all.dim() == 1:
+                ip_all = ip_all[None, :].expand(self.local_chains, -1)
+            if ip_all.shape[0] != self.local_chains:
+                raise ValueError("`init_params` must have the same leading dimension as `num_chains`.")
+        parts = None
+        if resume is not None:
+            parts = getattr(resume, "_parts", None)
+            if parts is None or len(parts) != G:
+                raise ValueError(f"the state to resume holds no per-device snapshots for these {G} devices "
+                                 "(it comes from a run on another device layout)")
+        out, errs = [None] * G, []
+        group = engines[0].device_group[0]
+
+        def work(g):
+            eng = engines[g]
+            try:
+                eng.constrain_samples = self.postprocess_fn is None
+                with torch.cuda.device(eng.device):
+                    if parts is not None:
+                        self._restore(eng, parts[g])
+                    else:
+                        ip = None
+                        if ip_all is not None:
+                            lo, hi = shard_chains(self.local_chains, g, G)
+                            ip = ip_all[lo:hi]
+                        eng.initialize(seed, self.num_warmup, init_params=ip, radius=self.sampler.init_radius())
+                    t0 = time.perf_counter()
+                    samples, fields, launches = eng.run(n_iter, seed, collect_begin=lower, thinning=self.thinning,
+                                                        poll_every=self.poll_every,
+                                                        collect_samples=not getattr(self, "_fields_only", False))
+                    torch.cuda.synchronize(eng.device)
+                    out[g] = (samples[:, :, :eng.C], fields[:, :, :eng.C], launches,
+                              (time.perf_counter() - t0) * 1e3, self._snapshot(eng, seed))
+            except BaseException as e:  # noqa: BLE001  (re-raised below; the others must not wait)
+                errs.append(e)
+                group.abort()
+
+        threads = [threading.Thread(target=work, args=(g,)) for g in range(G)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errs:
+            for eng in engines:  # a broken barrier cannot be reused
+                eng.device_group = None
+            self._engines = None
+            raise errs[0]
+        d0 = engines[0].device
+        self._samples = torch.cat([o[0].to(d0) for o in out], dim=2)
+        self._fields = torch.cat([o[1].to(d0) for o in out], dim=2)
+        self.last_run_stats = {"launches": max(o[2] for o in out), "device_ms": max(o[3] for o in out),
+                               "iterations": n_iter, "devices": [str(e.device) for e in engines]}
+        self._last_state = _combine_states([o[4] for o in out], engines, d0)
 
     # ------------------------------------------------------------------ results
     def _model_potential(self):
@@ -266,5 +389,41 @@ class MCMC:
         state = self.__dict__.copy()
         state["_engine"] = None
         state["_engine_key"] = None
+        state["_engines"] = None
         state["_host_potential"] = None
         return state
+
+
+def _combine_states(parts, engines, device):
+    """One HMCState over the chains of every device (global chain order: per-chain fields
+    concatenated, a pooled / shared dense matrix taken once); the per-device snapshots ride
+    along as `_parts` for resuming (MCMC.post_warmup_state = last_state)."""
+    from .hmc import HMCAdaptState, HMCState
+
+    shared_mass = engines[0].dense and not engines[0].chain_dense
+
+    def cat(vals, shared=False):
+        v0 = vals[0]
+        if isinstance(v0, torch.Tensor):
+            if shared or v0.dim() == 0:
+                return v0.to(device)
+            return torch.cat([v.to(device) for v in vals], dim=0)
+        if isinstance(v0, dict):
+            return {k: cat([v[k] for v in vals], shared) for k in v0}
+        if isinstance(v0, tuple) and not hasattr(v0, "_fields"):
+            return tuple(cat([v[i] for v in vals], shared) for i in range(len(v0)))
+        return v0
+
+    a = [p.adapt_state for p in parts]
+    adapt = HMCAdaptState(
+        cat([x.step_size for x in a]),
+        cat([x.inverse_mass_matrix for x in a], shared_mass),
+        cat([x.mass_matrix_sqrt for x in a], shared_mass),
+        cat([x.mass_matrix_sqrt_inv for x in a], shared_mass),
+        cat([x.ss_state for x in a]), cat([x.mm_state for x in a]), cat([x.window_idx for x in a]), a[0].rng_key)
+    st = HMCState(*[cat([getattr(p, f) for p in parts]) if f not in ("adapt_state", "trajectory_length", "rng_key")
+                    else (adapt if f == "adapt_state" else getattr(parts[0], f)) for f in HMCState._fields])
+    st._parts = list(parts)
+    st._engine = None
+    st._layout = ("devices", tuple(p._layout for p in parts))
+    return st

@@ -29,6 +29,40 @@ def shard_chains(num_chains, rank, world_size):
     return lo, hi
 
 
+class DeviceGroup:
+    """Chains of ONE process sharded over several devices, one host thread per device (MCMC
+    chain_method="parallel" without torch.distributed; the reference pmaps over local devices,
+    mcmc.py:700-715): the in-process counterpart of the torch.distributed ranks.  Shards are
+    contiguous in global chain id (shard_chains), so every chain's draws equal the one-device
+    and the torchrun runs bitwise; the only exchange while sampling is the pooled dense-mass
+    moment sum at window ends (all_reduce_sum, ranks summed in rank order: for two devices
+    the same single addition an all_reduce makes)."""
+
+    def __init__(self, size):
+        import threading
+
+        self.size = int(size)
+        self.barrier = threading.Barrier(self.size)
+        self.slots = [None] * self.size
+
+    def all_reduce_sum(self, rank, tensors):
+        """Every rank passes the same list of tensors; each gets back their sums over ranks (in
+        rank order), on its own tensors' devices."""
+        self.slots[rank] = list(tensors)
+        self.barrier.wait()
+        out = []
+        for i, t in enumerate(tensors):
+            acc = self.slots[0][i].to(t.device).clone()
+            for r in range(1, self.size):
+                acc += self.slots[r][i].to(t.device)
+            out.append(acc)
+        self.barrier.wait()  # every rank has read the slots before they are reused
+        return out
+
+    def abort(self):
+        self.barrier.abort()
+
+
 def dist_info():
     d = torch.distributed
     if d.is_available() and d.is_initialized():

@@ -5,6 +5,10 @@ whitening around any of them.  They restate oracle/potentials.py (float64, one c
 against scipy.stats and finite differences in tests/test_oracle_potentials.py) for a batch
 Z [B, D] -> (U [B], grad [B, D]), so that oracle/cpu_batched.run_chains can drive many of the
 oracle's NUTS chains with one potential call per round: the CPU side of SURVEY.md §8d.
+
+`dtype=np.float64` computes the same expressions in float64 (outputs rounded to float32): the
+rounding reference of the parity calibration (oracle/parity.py), against which the float32
+batch is "another float32 implementation" like the device.
 """
 from __future__ import annotations
 
@@ -21,10 +25,12 @@ class FunnelBatch:
     """examples/funnel.py:44-46 (centred), z = (x[K], y): U = y^2/18 + log(3 sqrt(2 pi))
     + sum_i [x_i^2 e^-y / 2 + y/2 + log(2 pi)/2] (Normal.log_prob, continuous.py:2200-2204)."""
 
-    def __init__(self, dim):
+    def __init__(self, dim, dtype=np.float32):
         self.dim, self.K = dim, dim - 1
+        self.F = dtype
 
     def __call__(self, Z):
+        F = self.F
         Z = np.asarray(Z, F)
         x, y = Z[:, :-1], Z[:, -1]
         e = np.exp(-y)
@@ -34,7 +40,7 @@ class FunnelBatch:
         G = np.empty_like(Z)
         G[:, :-1] = x * e[:, None]
         G[:, -1] = y / F(9) + F(0.5 * self.K) - F(0.5) * e * xx
-        return pe.astype(F), G
+        return pe.astype(np.float32), G.astype(np.float32)
 
 
 class SVBatch:
@@ -42,12 +48,14 @@ class SVBatch:
     (continuous.py:473-475) + GaussianRandomWalk (:684-690) + StudentT (:2373-2384) with the
     ExpTransform log-Jacobians; gradient as oracle/potentials.py StochasticVolatility."""
 
-    def __init__(self, returns):
-        self.r2 = np.asarray(returns, np.float64).astype(F) ** 2
+    def __init__(self, returns, dtype=np.float32):
+        self.F = dtype
+        self.r2 = np.asarray(returns, np.float64).astype(dtype) ** 2
         self.T = self.r2.shape[0]
         self.dim = self.T + 2
 
     def __call__(self, Z):
+        F = self.F
         Z = np.asarray(Z, F)
         a, s, b = Z[:, 0], Z[:, 1:-1], Z[:, -1]
         nu, sigma = np.exp(a), np.exp(b)
@@ -71,7 +79,7 @@ class SVBatch:
                    + F(T) * (-F(0.5) / nu + F(0.5) * dg)) + F(1)
         G = np.empty_like(Z)
         G[:, 0], G[:, 1:-1], G[:, -1] = -ga, -gs, -gb
-        return (-lp).astype(F), G
+        return (-lp).astype(np.float32), G.astype(np.float32)
 
 
 class BNNBatch:
@@ -80,14 +88,16 @@ class BNNBatch:
     1 / sqrt(prec)); the backward pass of oracle/potentials.py BNN over a batch of networks
     (batched matmuls)."""
 
-    def __init__(self, X, Y, H):
-        self.X = np.asarray(X, F)
-        self.Y = np.asarray(Y, F).reshape(-1)
+    def __init__(self, X, Y, H, dtype=np.float32):
+        self.F = dtype
+        self.X = np.asarray(X, dtype)
+        self.Y = np.asarray(Y, dtype).reshape(-1)
         self.N, self.Dx = self.X.shape
         self.H = int(H)
         self.dim = 1 + self.Dx * self.H + self.H * self.H + self.H
 
     def __call__(self, Z):
+        F = self.F
         Z = np.asarray(Z, F)
         B, H, Dx, N = Z.shape[0], self.H, self.Dx, self.N
         u = Z[:, 0]
@@ -113,7 +123,7 @@ class BNNBatch:
         gw1 = w1 + np.matmul(self.X.T[None], ga1)
         gu = -(F(3) - p + F(0.5 * N) - F(0.5) * p * ee)
         G = np.concatenate([gu[:, None], gw1.reshape(B, -1), gw2.reshape(B, -1), gw3.reshape(B, -1)], axis=1)
-        return (-lp).astype(F), G.astype(F)
+        return (-lp).astype(np.float32), G.astype(np.float32)
 
 
 class Whitened:
@@ -122,16 +132,19 @@ class Whitened:
     (hmc.py:92-110, hmc_util.py:1183-1220).  The two products per call are [B, D] x [D, D]
     float32 GEMMs."""
 
-    def __init__(self, base, T, mu):
+    def __init__(self, base, T, mu, dtype=np.float32):
         self.base = base
-        self.Tt = np.ascontiguousarray(np.asarray(T, np.float64).T.astype(F))  # z = mu + w @ T^T
-        self.T = np.ascontiguousarray(np.asarray(T, np.float64).astype(F))
-        self.mu = np.asarray(mu, F)
+        self.F = dtype
+        self.Tt = np.ascontiguousarray(np.asarray(T, np.float64).T.astype(dtype))  # z = mu + w @ T^T
+        self.T = np.ascontiguousarray(np.asarray(T, np.float64).astype(dtype))
+        self.mu = np.asarray(mu, dtype)
         self.dim = base.dim
 
     def to_model(self, W):
-        return self.mu[None, :] + np.asarray(W, F) @ self.Tt
+        return self.mu[None, :] + np.asarray(W, self.F) @ self.Tt
 
     def __call__(self, W):
+        # dtype float64 with a float64 base: the rounding reference of the parity calibration
+        # (oracle/parity.py) -- positions, model and gradient product in float64, results rounded
         pe, G = self.base(self.to_model(W))
-        return pe, (G @ self.T).astype(F)
+        return pe, (np.asarray(G, self.F) @ self.T).astype(np.float32)

@@ -26,8 +26,16 @@ rounding flip -- `explained` -- when:
   more than max(4 x the largest relative dot discrepancy seen at the earlier leaves, 1e-5) x the
   magnitude of the dot's terms.
 
-A transition whose decisions all agree but whose draw differs is reported as `draw` (never
-seen so far: equal decisions select the same leaf)."""
+A transition whose decisions all agree but whose draw differs is reported as `draw`: the same
+leaf was selected, but the positions drifted apart along the trajectory (leapfrog dynamics of a
+tanh network or a stiff posterior amplify rounding over hundreds of leaves).
+
+Calibration.  How far rounding alone carries two float32 implementations of the same
+algorithm apart is measured, not assumed: `compare_traced` run between the oracle and a second
+oracle whose potential is another float32 implementation (oracle/batched.py's NumPy batch vs
+oracle/potentials.py's rounded float64, or float32 vs rounded float64 sums) gives the reference
+spread of matched chains, located partings and drift; `like_calibration` requires the device's
+to be of the same order (tests/test_gpu_parity_trace.py)."""
 from __future__ import annotations
 
 import math
@@ -170,3 +178,27 @@ def describe(m):
     return (f"chain {m['chain']}: transition {m['transition']} (tree {m['tree_dev']} dev / {m['tree_oracle']} "
             f"oracle) parts at leaf {m['leaf']} on {m['kind']}:{val}{u}{b}, leaf-energy discrepancy up to it "
             f"{m['dE_err']:.3g} -> {'rounding flip' if m['explained'] else 'NOT explained by rounding'}")
+
+
+def counts(par):
+    """{matched, chains, <kind>: n, unexplained} of a compare_traced record."""
+    out = {"chains": par["chains"], "matched": par["matched"], "unexplained": 0}
+    for m in par["mismatches"]:
+        out[m["kind"]] = out.get(m["kind"], 0) + 1
+        out["unexplained"] += 0 if (m["explained"] or m["kind"] == "draw") else 1
+    return out
+
+
+def like_calibration(dev, cal, slack=None):
+    """(ok, message): the device-vs-oracle record `dev` is of the same order as the rounding
+    calibration `cal` (oracle vs another float32 oracle on the same chains): every located
+    parting explained at its leaf, matched chains within `slack` (default max(4, chains / 10))
+    of the calibration's, and the largest leaf-energy discrepancy on matched paths within 10x
+    of the calibration's (floor 1e-3)."""
+    a, b = counts(dev), counts(cal)
+    slack = max(4, dev["chains"] // 10) if slack is None else slack
+    msg = (f"device {a} (max dE err {dev['max_dE_err']:.3g}) vs rounding calibration {b} "
+           f"(max dE err {cal['max_dE_err']:.3g})")
+    ok = (a["unexplained"] == 0 and a["matched"] >= b["matched"] - slack
+          and dev["max_dE_err"] <= 10.0 * max(cal["max_dE_err"], 1e-3))
+    return ok, msg

@@ -24,7 +24,8 @@ for spec in sys.argv[2:]:
     out = os.path.join(ROOT, "build", "ab", name)
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, os.path.basename(src) + ".o")
-    cmd = [B.HIPCC, *B.COMMON_FLAGS, *B.FILE_FLAGS.get(os.path.basename(src), ()), *shlex.split(flags), "-x", "hip",
+    cmd = [B.HIPCC, *B.COMMON_FLAGS, *B.FILE_FLAGS.get(os.path.basename(src), ()), "-DNMX_EXPERIMENT",
+           *shlex.split(flags), "-x", "hip",
            "-c", src_v, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:

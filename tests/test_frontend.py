@@ -133,3 +133,33 @@ def test_model_deterministic_sites_are_evaluated():
     c = rs.randn(7, 55).astype(np.float32)
     out = pot.deterministic({"coefs": torch.from_numpy(c)})
     np.testing.assert_allclose(out["logits"].numpy(), c @ Xc.T, rtol=1e-4, atol=1e-4)
+
+
+def test_constant_deterministic_broadcasts_and_bad_ops_fail_at_mapping():
+    """A constant deterministic site (numpyro.deterministic('c', 3.0)) has one value per draw;
+    an expression the evaluator does not support raises when the model is mapped, not after
+    sampling."""
+    import torch
+
+    Xc, yc = datasets.covtype_synthetic(n_rows=50, seed=3)
+
+    def cov_const(data, labels):
+        coefs = numpyro.sample("coefs", dist.Normal(np.zeros(55), np.ones(55)))
+        numpyro.deterministic("c", 3.0)
+        numpyro.deterministic("v", np.arange(3.0))
+        numpyro.sample("obs", dist.Bernoulli(logits=Z.jnp.dot(data, coefs)), obs=labels)
+
+    pot = potential_from_model(cov_const, (Xc, yc))
+    out = pot.deterministic({"coefs": torch.zeros(4, 2, 55)})
+    assert out["c"].shape == (4, 2) and float(out["c"][3, 1]) == 3.0
+    assert out["v"].shape == (4, 2, 3) and torch.equal(out["v"][1, 0], torch.arange(3.0))
+
+    from numpyro_amd.jnp import Sym
+
+    def cov_bad(data, labels):
+        coefs = numpyro.sample("coefs", dist.Normal(np.zeros(55), np.ones(55)))
+        numpyro.deterministic("odd", Sym("erf", (coefs,), (55,)))
+        numpyro.sample("obs", dist.Bernoulli(logits=Z.jnp.dot(data, coefs)), obs=labels)
+
+    with pytest.raises(NotImplementedError, match="'erf' is not supported"):
+        potential_from_model(cov_bad, (Xc, yc))

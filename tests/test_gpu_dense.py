@@ -710,3 +710,65 @@ def test_dense_wide_chain_row_step_invariances(device, monkeypatch):
     hi = _dense_wide_run(monkeypatch, True, C=56, chain_offset=40, fixed=True)
     np.testing.assert_array_equal(f[0][:40], lo[0])
     np.testing.assert_array_equal(f[0][40:], hi[0])
+
+
+def test_inverse_mass_matrix_dict_of_blocks_matches_oracle(device):
+    """inverse_mass_matrix as a dict {site group: block} (hmc_util.py:439-487, hmc.py:223-234)
+    with a structured dense_mass and no adaptation: the dense block over (theta, mu) in the group's
+    order and the diagonal block of tau come from the dict; the state holds them back keyed by
+    group; the oracle's dense-mass NUTS with the blocks scattered into full matrices (momentum from
+    each block's own factor) takes the device's trees and draws at a fixed step size."""
+    from numpyro_amd import datasets
+    from oracle import philox
+    from test_gpu_nuts import _explain_mismatches, _first_split
+
+    seed, C, T, D = 29, 32, 3, 10
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    rs = np.random.RandomState(3)
+    a = rs.randn(9, 9) * 0.3
+    blk = (a @ a.T + np.eye(9)).astype(np.float32)
+    imm = {("theta", "mu"): blk, ("tau",): np.array([0.5], np.float32)}
+    mcmc = MCMC(NUTS(P.eight_schools, dense_mass=[("theta", "mu")], inverse_mass_matrix=imm, adapt_mass_matrix=False,
+                     step_size=0.1, adapt_step_size=False), num_warmup=0, num_samples=T, num_chains=C,
+                postprocess_fn=lambda z: z)
+    mcmc.run(seed, *args, extra_fields=("num_steps",))
+    st = mcmc.last_state.adapt_state.inverse_mass_matrix
+    np.testing.assert_allclose(st[("theta", "mu")][0].cpu().numpy(), blk, rtol=1e-6)
+    np.testing.assert_allclose(st[("tau",)][0].cpu().numpy(), [0.5], rtol=1e-6)
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
+    sm = mcmc.get_samples(True)
+    zs = np.concatenate([sm["mu"].cpu().numpy()[..., None], sm["tau"].cpu().numpy()[..., None],
+                         sm["theta"].cpu().numpy()], axis=-1)
+    order = list(range(2, 10)) + [0]
+    imm_f = np.zeros((D, D), np.float32)
+    msq_f = np.zeros((D, D), np.float32)
+    i_b, sq_b, _ = H._initialize_mass_matrix(9, blk, True)
+    imm_f[np.ix_(order, order)], msq_f[np.ix_(order, order)] = i_b, sq_b
+    i_t, sq_t, _ = H._initialize_mass_matrix(1, np.array([0.5], np.float32), False)
+    imm_f[1, 1], msq_f[1, 1] = i_t[0], sq_t[0]
+    ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    match, mism = 0, []
+    for c in range(C):
+        o = H.NUTSOracle(pe_grad, D, 0, step_size=0.1, adapt_step_size=False, adapt_mass_matrix=False,
+                         dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32))
+        s = o.init(philox.init_uniform(seed, c, 0, D), seed, c)
+        s = s._replace(adapt_state=s.adapt_state._replace(inverse_mass_matrix=imm_f, mass_matrix_sqrt=msq_f))
+        ok, margins = [], []
+        for t in range(T):
+            H.DECISIONS = []
+            try:
+                s = o.sample(s)
+            finally:
+                d, H.DECISIONS = H.DECISIONS, None
+            margins.append(H.closest_decision(d))
+            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
+        t = _first_split(ok)
+        if t < 0:
+            match += 1
+        else:
+            mism.append((c, t, margins[t]))
+    print(f"[inverse_mass_matrix dict] {match}/{C} chains reproduce the oracle's block-mass transitions")
+    _explain_mismatches(mism, "inverse_mass_matrix dict")
+    assert match >= int(0.9 * C)

@@ -132,3 +132,38 @@ def test_postprocess_fn(device):
     torch.testing.assert_close(b["tau"], a["tau"], rtol=2e-6, atol=0)  # host exp vs device exp
     assert m.get_samples(group_by_chain=True)["log_tau"].shape == (16, 20)
     assert set(m._site_arrays(True, include_deterministic=False)) == {"mu", "tau", "theta"}
+
+
+def test_bound_potentials_pickle_unbound(device):
+    """A bound potential pickles without its device data: the packed split-bf16 covtype image
+    (`packed`, set to None in __init__) and a whitened potential's whitening go back to their
+    unbound values, workspaces are dropped; the copy binds again and evaluates identically."""
+    from numpyro_amd import native
+    from numpyro_amd.dense import WhitenedPotential
+
+    X, y = datasets.covtype_synthetic(n_rows=2000, seed=2)
+    pot = P.LogisticRegression(X, y)
+    pot.bind(64, 64, "cuda:0")
+    assert pot.packed is not None and pot.packed.is_cuda
+    blob = pickle.dumps(pot)
+    cp = pickle.loads(blob)
+    assert cp.packed is None and not hasattr(cp, "workspace")
+
+    def cuda_tensors(obj):
+        return [k for k, v in obj.__dict__.items() if isinstance(v, torch.Tensor) and v.is_cuda]
+
+    assert not cuda_tensors(cp)
+    cp.bind(64, 64, "cuda:0")
+    z = (0.1 * torch.randn(55, 64, generator=torch.Generator().manual_seed(0))).cuda()
+    outs = []
+    for p_ in (pot, cp):
+        g, pe = torch.empty_like(z), torch.empty(64, device="cuda")
+        ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), num_chains=64, ldc=64)
+        p_.evaluate(ev, native.stream_ptr())
+        outs.append((g, pe))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    wp = WhitenedPotential(P.funnel.potential(20))
+    wp.bind(64, 64, "cuda:0")
+    assert wp.whitening is not None
+    wc = pickle.loads(pickle.dumps(wp))
+    assert wc.whitening is None and not cuda_tensors(wc) and not cuda_tensors(wc.base)

@@ -113,3 +113,26 @@ def test_flip_far_from_a_tie_is_not_explained():
         assert loc["leaf"] == i and loc["kind"] == "take_leaf" and not loc["explained"]
         return
     raise AssertionError("no leaf with a clear transition decision")
+
+
+def test_calibration_between_two_float32_implementations():
+    """like_calibration: two float32 implementations of one potential (float32 sums vs rounded
+    float64) compared with a third are of the same order; a record with an unexplained parting
+    or far fewer matched chains is not."""
+    from oracle import potentials as OP
+
+    rs = np.random.RandomState(4)
+    X = rs.randn(500, 5).astype(np.float32)
+    y = (rs.rand(500) < 0.5).astype(np.float32)
+    r32 = OP.LogisticRegression(X, y, dtype=np.float32)
+    r64 = OP.LogisticRegression(X, y, dtype=np.float64)
+    f64 = lambda z: tuple(np.asarray(v, np.float32) for v in r64.pe_grad(z))  # noqa: E731
+    T, n = 4, 12
+    ref = _run(f64, 5, n, 2, T, 0.1)
+    a = _run(r32.pe_grad, 5, n, 2, T, 0.1)
+    tr, ns, z = _as_device(a, T)
+    par = PR.compare_traced(ref, tr, ns, z, atol=1e-4, rtol=1e-4)
+    ok, msg = PR.like_calibration(par, par)
+    assert ok, msg
+    bad = dict(par, matched=0, mismatches=par["mismatches"] + [{"kind": "take_leaf", "explained": False}])
+    assert not PR.like_calibration(bad, par)[0]

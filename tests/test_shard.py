@@ -95,3 +95,27 @@ def test_gloo_two_ranks_reproduce_single_process():
         n = 301
         ref_cov = np.cov(zs) * n / (n + 5.0) + 1e-3 * 5.0 / (n + 5.0) * np.eye(5)
         np.testing.assert_allclose(r["cov"], ref_cov, rtol=1e-9)
+
+
+def test_device_group_all_reduce_sum_in_rank_order():
+    """shard.DeviceGroup (MCMC chain_method='parallel' in one process): every thread gets the
+    rank-ordered sum; two ranks give exactly a + b, as an all_reduce does."""
+    import threading
+
+    from numpyro_amd.shard import DeviceGroup
+
+    g = DeviceGroup(3)
+    vals = [torch.tensor([0.1, 1e16], dtype=torch.float64) * (r + 1) for r in range(3)]
+    out = [None] * 3
+
+    def work(r):
+        out[r] = g.all_reduce_sum(r, [vals[r], torch.tensor([float(r)])])
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ref = (vals[0] + vals[1]) + vals[2]
+    for r in range(3):
+        assert torch.equal(out[r][0], ref) and float(out[r][1]) == 3.0
