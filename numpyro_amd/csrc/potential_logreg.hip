@@ -733,11 +733,43 @@ __device__ __forceinline__ void x3_roles_barrier() {
   __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8) | (0 << 14));  // vmcnt(0) lgkmcnt(0)
   asm volatile("s_barrier" ::: "memory");
 }
+// the same with up to N of this wave's youngest LDS-DMA loads still in flight (the prefetch of
+// later tiles), its LDS writes complete
+template <int N>
+__device__ __forceinline__ void x3_roles_barrier_n() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
+  asm volatile("s_barrier" ::: "memory");
+}
+__device__ __forceinline__ void x3_roles_barrier_rt(int n) {  // n wave-uniform
+  switch (n) {
+    case 0: x3_roles_barrier_n<0>(); break;
+    case 1: x3_roles_barrier_n<1>(); break;
+    case 2: x3_roles_barrier_n<2>(); break;
+    case 3: x3_roles_barrier_n<3>(); break;
+    case 4: x3_roles_barrier_n<4>(); break;
+    case 5: x3_roles_barrier_n<5>(); break;
+    case 6: x3_roles_barrier_n<6>(); break;
+    case 7: x3_roles_barrier_n<7>(); break;
+    case 8: x3_roles_barrier_n<8>(); break;
+    case 9: x3_roles_barrier_n<9>(); break;
+    case 10: x3_roles_barrier_n<10>(); break;
+    case 11: x3_roles_barrier_n<11>(); break;
+    default: x3_roles_barrier_n<12>(); break;  // (n > 12: waits for more than needed)
+  }
+}
 
 constexpr int X3_ROLE_WAVES = 8;
-// A-ring slots: X tiles are prefetched PA - 1 tiles ahead (the B ring has PA + 1 slots); 2, 3
-// and 4 measured equal (the tail launch streams the 465 MB of split tiles at ~7 TB/s)
-constexpr int X3_ROLE_PA = 2;
+// Prefetch depth: tile k + PA is issued in iteration k, and the barrier of iteration k waits
+// only for the DMAs of the tile pair it needs (A(k+1), labels(k)), leaving the later PA - 2
+// pairs in flight (counted vmcnt: with a plain vmcnt(0) every barrier waited for the DMAs
+// issued one iteration earlier, so the HBM latency was exposed once per tile whatever the
+// depth -- round 3 measured 2, 3 and 4 slots equal).  LDS at PA = 4: 6 A slots x 14 KB + 5
+// label slots + 32 KB of residual slots = 121 KB, one workgroup per CU as before.
+#ifndef NMX_X3_ROLE_PA
+#define NMX_X3_ROLE_PA 4
+#endif
+constexpr int X3_ROLE_PA = NMX_X3_ROLE_PA;
 
 // A-ring slots of the tail form: tiles k - 1 (GEMM2 of the B waves, transposed reads of the
 // GEMM1 image), k + 1 (GEMM1 of the A waves) and k + PA landing
@@ -811,6 +843,18 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
                                                16, lane * 16, (unsigned)((k * NP + NP - 1) * 1024), 0, 0);
   };
   char* const rmine = rring + t * 4096 + lane * 16;  // + slot * 4 * 4096
+  // LDS-DMA pair p = (A(p + 1), labels(p)): pair p is issued in the prologue (p < PA - 1) or in
+  // iteration p - PA + 1; iteration k needs pair k, so this wave's DMAs of pairs k + 1 ..
+  // k + PA - 2 may stay in flight at its barrier
+  const int na_w = (w < NA - X3_ROLE_WAVES ? 2 : 1) + (NA > 2 * X3_ROLE_WAVES ? 1 : 0);
+  static_assert(NA <= 2 * X3_ROLE_WAVES, "issue_a: at most two pieces per wave");
+  auto pair_ops = [&](int p) { return (p + 1 < nt ? na_w : 0) + (w == X3_ROLE_WAVES - 1 && p < nt ? 1 : 0); };
+  auto in_flight = [&](int k) {
+    int n = 0;
+#pragma unroll
+    for (int p = 1; p <= X3_ROLE_PA - 2; ++p) n += pair_ops(k + p);
+    return n;
+  };
 
   if (roleA) {
     // ---- role A: GEMM1 + epilogue, hands R(k) to its B wave --------------------------------
@@ -821,12 +865,14 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
     if (nt > 0) {
       issue_a(0);
       x3_roles_barrier();  // A(0) is in
-      for (int j = 1; j < PA && j < nt; ++j) issue_a(j);
-      for (int j = 0; j < PA - 1 && j < nt; ++j) issue_b(j);
+      for (int p = 0; p < PA - 1; ++p) {  // pairs (A(p + 1), labels(p)), in the loop's order
+        if (p + 1 < nt) issue_a(p + 1);
+        if (p < nt) issue_b(p);
+      }
       f32x16 accA, accB;
       if (active) accA = x3_gemm1<KB, H>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
       auto stepA = [&](int k, const f32x16& acc, f32x16& nxt) {
-        x3_roles_barrier();  // A(k+1), B(k) landed; R slot k&1 was read by B in iteration k-1
+        x3_roles_barrier_rt(in_flight(k));  // A(k+1), B(k) landed; R slot k&1 was read by B in iteration k-1
         if (k + PA < nt) issue_a(k + PA);
         if (k + PA - 1 < nt) issue_b(k + PA - 1);
         if (!active) return;
@@ -918,10 +964,12 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
     if (nt > 0) {
       issue_a(0);
       x3_roles_barrier();
-      for (int j = 1; j < PA && j < nt; ++j) issue_a(j);
-      for (int j = 0; j < PA - 1 && j < nt; ++j) issue_b(j);
+      for (int p = 0; p < PA - 1; ++p) {
+        if (p + 1 < nt) issue_a(p + 1);
+        if (p < nt) issue_b(p);
+      }
       for (int k = 0; k < nt; ++k) {
-        x3_roles_barrier();
+        x3_roles_barrier_rt(in_flight(k));
         if (k + PA < nt) issue_a(k + PA);
         if (k + PA - 1 < nt) issue_b(k + PA - 1);
         if (active && k > 0) gemm2(k - 1);

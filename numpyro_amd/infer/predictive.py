@@ -9,10 +9,15 @@ reference re-runs the traced model once per sample under ``substitute`` (:803-88
 model's observed-site sampler is one HIP kernel over all samples (csrc/predictive.hip).
 
 An observed site whose data is passed (not ``None``) keeps that data, as ``numpyro.sample``
-with ``obs=`` does under the reference's Predictive.  Models: covtype logistic regression
-(``obs``), eight schools (``obs``), BNN (``Y``).  Out of scope (raise): guides / params (SVI),
-``infer_discrete``, prior predictive (no posterior samples), models without a free observed
-site (funnel; stochastic volatility, whose observed ``returns`` also fix its length).
+with ``obs=`` does under the reference's Predictive.  Deterministic sites (the model's
+``numpyro.deterministic`` and reparameterised sites such as the non-centred funnel's ``x``,
+reparam.py:140-142) are returned by default, as the reference's ``_predictive`` does
+(util.py:870-877), computed from the posterior samples.  Models: covtype logistic regression
+(``obs``), eight schools (``obs``), BNN (``Y``), stochastic volatility (``r``: its returns are
+both the observation and the series length, examples/stochastic_volatility.py:57-65, so -- as in
+the reference -- the observed data come back), funnel and its LocScaleReparam form (no observed
+site: deterministic ``x`` and any ``return_sites``, as examples/funnel.py:84-87 uses it).  Out of
+scope (raise): guides / params (SVI), ``infer_discrete``, prior predictive (no posterior samples).
 """
 from __future__ import annotations
 
@@ -78,12 +83,31 @@ def _predict_bnn(samples, seed, device, X, Y, D_H, D_Y=1):
     return {"Y": out}
 
 
+def _predict_sv(samples, seed, device, returns):
+    if returns is None:
+        raise ValueError("stochastic volatility: `returns` set the series length (examples/stochastic_volatility.py:"
+                         "57-65); the observed site r keeps them")
+    S = samples["s"].reshape(samples["s"].shape[0], -1).shape[0]
+    return {"r": _observed(returns, S, device)}
+
+
+def _predict_none(samples, seed, device, *args, **kwargs):
+    return {}
+
+
 # FusedModel -> (observed sites, sampler(samples, seed, device, *args, **kwargs))
 _PREDICTORS = {
     "logistic_regression": (("obs",), _predict_logreg),
     "eight_schools": (("obs",), _predict_eight_schools),
     "bnn": (("Y",), _predict_bnn),
+    "stochastic_volatility": (("r",), _predict_sv),
+    "funnel": ((), _predict_none),
+    "funnel_reparam": ((), _predict_none),
 }
+
+
+# models whose Predictive draws nothing on the device (no free observed site)
+_HOST_ONLY = {"stochastic_volatility", "funnel", "funnel_reparam"}
 
 
 class Predictive:
@@ -138,17 +162,28 @@ class Predictive:
         S = self.num_samples
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
         if device is None:
-            raise RuntimeError("Predictive needs a GPU (the samplers are HIP kernels)")
+            if self.model.__name__ not in _HOST_ONLY:
+                raise RuntimeError("Predictive needs a GPU (the samplers are HIP kernels)")
+            device = torch.device("cpu")  # nothing is drawn: observed data / deterministic sites
         flat = {k: torch.as_tensor(v).reshape(S, *v.shape[nb:]) for k, v in self.posterior_samples.items()}
         draws = sampler(flat, key_to_seed(rng_key), device, *args, **kwargs)
+        # deterministic sites from the (constrained) latent values: recomputed from the samples
+        # (exclude_deterministic=True, the default) or taken as given
+        pot = self.model.potential(*args, **kwargs)
+        latent = {n: flat[n] for n, _, _ in pot.sites if n in flat}
+        dets = pot.deterministic(latent) if len(latent) == len(pot.sites) else {}
+        if not self.exclude_deterministic:
+            dets.update({k: v for k, v in flat.items() if k in dets})
         if self.return_sites is None:
-            names = [n for n in observed if n not in self.posterior_samples]
+            names = [n for n in observed if n not in self.posterior_samples] + list(dets)
         else:
             names = list(self.return_sites)
         out = {}
         for n in names:
             if n in draws and n not in self.posterior_samples:
                 v = draws[n]
+            elif n in dets:
+                v = dets[n]
             elif n in flat:  # a substituted latent site, returned as given
                 v = flat[n]
             else:

@@ -803,3 +803,22 @@ def test_chain_groups_are_bitwise_the_one_stream_loop(device, groups, C, sync, m
                   ef["potential_energy"].cpu().numpy())
     for a, b in zip(out[1], out[groups]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_covtype_full_size_recovers_ref_params(device):
+    """BASELINE config 1's data at full size: the synthetic covtype labels are drawn from
+    Bernoulli(sigmoid(X . ref_params)) with the reference's coefficient vector
+    (examples/covtype.py:79-139, datasets.COVTYPE_REF_COEFS), so at N = 581012 the posterior
+    concentrates around ref_params (sd ~ 3e-3): each posterior mean lies within 5 posterior sd of
+    its generating value, and the standardized errors are of unit size (mean square <= 3)."""
+    X, y = datasets.covtype_synthetic(seed=0)
+    Xd, yd = torch.from_numpy(X).to(device), torch.from_numpy(y).to(device)
+    mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=150, num_samples=40, num_chains=32, progress_bar=False)
+    mcmc.run(11, Xd, yd)
+    c = mcmc.get_samples()["coefs"].to(torch.float64).cpu().numpy()  # [C * S, 55]
+    m, sd = c.mean(0), c.std(0)
+    zerr = (m - datasets.COVTYPE_REF_COEFS) / sd
+    print(f"[covtype ref_params] posterior sd {sd.min():.2e}..{sd.max():.2e}, max |z| {np.abs(zerr).max():.2f}, "
+          f"mean z^2 {np.mean(zerr ** 2):.2f}")
+    assert np.all(np.abs(zerr) <= 5.0), np.argsort(-np.abs(zerr))[:5]
+    assert np.mean(zerr ** 2) <= 3.0
