@@ -323,9 +323,14 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
         rh = max(float(shard.split_gelman_rubin(v.reshape(v.shape[0], v.shape[1], -1)).max()) for v in sm.values())
         r["max_split_rhat"] = rh
         if not sp["one_gpu"]:
-            gathered = shard.gather_chains(sm["s"][:, :, :8])
+            # the whole draw set of every site, all_gathered to every rank (SURVEY.md §8e sample gather)
+            gathered = {k: shard.gather_chains(v) for k, v in sm.items()}
             torch.cuda.synchronize()
-            r["end_of_run"] = {"ms": (time.perf_counter() - te) * 1e3, "gathered_chains": int(gathered.shape[0]),
+            nbytes = sum(v.numel() * v.element_size() for v in gathered.values())
+            r["end_of_run"] = {"ms": (time.perf_counter() - te) * 1e3,
+                               "gathered_chains": int(next(iter(gathered.values())).shape[0]),
+                               "gathered": f"every site's draws [chains, {sp['steps']}, ...]: {nbytes / 1e6:.0f} MB "
+                                           f"on every rank, plus the cross-chain split R-hat",
                                "collective": _collective(world)}
             r["parallelism"] = f"chains sharded {world}-way (no data-path collective)"
             r["scaling"] = "strong"

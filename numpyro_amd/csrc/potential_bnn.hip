@@ -52,20 +52,18 @@ struct BnnDims {
   int o_w1, o_w2, o_w3;  // offsets of the sites in z
 };
 
+// Sum over the workgroup in a fixed order: the 8 waves' values per lane in wave order, then the
+// 64 lanes by a butterfly (the serial 64-step loop of thread 0 it replaces was ~1.5 us per sum)
 __device__ __forceinline__ float block_sum256(float v, float* red) {
   red[threadIdx.x] = v;
   __syncthreads();
-  if (threadIdx.x < 64) {
-    float s = 0.0f;
-#pragma unroll
-    for (int w = 0; w < THREADS / 64; ++w) s += red[w * 64 + threadIdx.x];
-    red[threadIdx.x] = s;
-  }
-  __syncthreads();
   float t = 0.0f;
-  if (threadIdx.x == 0) {
-    for (int i = 0; i < 64; ++i) t += red[i];
-    red[0] = t;
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int w = 0; w < THREADS / 64; ++w) t += red[w * 64 + threadIdx.x];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) red[0] = t;
   }
   __syncthreads();
   t = red[0];
@@ -197,6 +195,8 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   float esq = 0.0f;
   for (int n = t; n < N; n += THREADS) {
     float yh = 0.0f;
+    // sequential in j (the sum's order), unrolled so the LDS reads are issued ahead of the FMA chain
+#pragma unroll 16
     for (int j = 0; j < H; ++j) yh += h2[n * H + j] * w3[j];
     const float e = Ys[n] - yh;
     esq += e * e;
@@ -207,6 +207,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   // grad w3 = w3 + h2^T gy
   for (int j = t; j < H; j += THREADS) {
     float s = 0.0f;
+#pragma unroll 16
     for (int n = 0; n < N; ++n) s += h2[n * H + j] * gy[n];
     g[dm.o_w3 + j] = w3[j] + s;
   }
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int e = t; e < Dx * H; e += THREADS) {
     const int k = e / H, j = e % H;
     float s = 0.0f;
+#pragma unroll 16
     for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[n * H + j];
     g[dm.o_w1 + e] = W1[e] + s;
   }

@@ -523,6 +523,28 @@ inline size_t x3_lds_bytes() {
   return x3_tr<KB, DT>() ? (size_t)(3 * NA + 2) * 1024 : (size_t)2 * (x3_nal<KB, DT, H>() + NP - NA) * 1024;
 }
 
+#ifdef NMX_X3_CLOCK
+// diagnostic build only (scripts/x3_clock.py, cdna_hip_programming.md rule 28 / DVFS give-back
+// item 6): per workgroup of the last all-active launch, the shader-clock and 100 MHz real-time
+// ticks spent in the tile loop; the in-kernel clock is their ratio x 100 MHz.  Written only here
+// and read only by nmx_debug_x3_clock: no output depends on it.
+__device__ unsigned long long g_x3_clock[16384 * 2];
+__device__ __forceinline__ unsigned long long x3_memtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ unsigned long long x3_memrealtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+
 template <int KB, int DT, int H, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
                                         nmx_eval_batch ev, float* __restrict__ gpart,
@@ -605,6 +627,9 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         }
       }
     };
+#ifdef NMX_X3_CLOCK
+    const unsigned long long ck_t0 = x3_memtime(), ck_r0 = x3_memrealtime();
+#endif
     if (nt > 0) {
       issue_a(0);
       x3_wait_vm<0>();
@@ -658,6 +683,13 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         if (k + 1 < nt) step(k + 1, accB, accA);
       }
     }
+#ifdef NMX_X3_CLOCK
+    const unsigned long long ck_t1 = x3_memtime(), ck_r1 = x3_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+      g_x3_clock[2 * blockIdx.x + (threadIdx.x & 1)] = ck_t1 - ck_t0;
+      g_x3_clock[2 * blockIdx.x + 1 + (threadIdx.x & 1)] = ck_r1 - ck_r0;
+    }
+#endif
   }
   if (!active || pos >= ldc) return;
 #pragma unroll
@@ -1081,6 +1113,14 @@ int check_ev(const nmx_eval_batch* ev) {
 }  // namespace
 
 extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return x3_num_splits(n_rows); }
+
+#ifdef NMX_X3_CLOCK
+extern "C" int nmx_debug_x3_clock(unsigned long long* host) {  // [16384][2] (shader ticks, 100 MHz ticks)
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_clock), sizeof(unsigned long long) * 16384 * 2) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
+  return NMX_OK;
+}
+#endif
 
 // packed buffer: w[64] (k_logreg_colsums) | split-bf16 tiles (k_logreg_pack_x3)
 inline size_t x3_offset() { return (COLTERM_BYTES + 255) / 256 * 256; }
