@@ -14,7 +14,8 @@
 // equals its f32 vector peak (157 TF/s), so the gain over register-blocked FMA loops is the
 // freed VALU (measured 0.30 vs 0.34 ms at 2048 chains, scripts/ab_bnn.py); the rest of a
 // chain's evaluation is latency-bound serial phases (tanh layers, reductions, 20 KB of
-// parameters in and gradient out).  The chain-major columns of the
+// parameters in and gradient out).  Round 4: 16 x 16 tiles (v_mfma_f32_16x16x4_f32, less padding,
+// even over the waves) and the serial sums unrolled (their loads issued ahead, same order).  The chain-major columns of the
 // evaluated chains are first transposed to rows (k_cols_to_rows, 64x64 LDS tiles, both
 // sides coalesced) so each workgroup reads its chain's 20 KB parameter vector and writes
 // its gradient contiguously; k_rows_to_cols scatters the gradients back.
@@ -46,6 +47,28 @@ __device__ __forceinline__ f32x16 mfma_tile(int K, FA fa, FB fb) {
   return acc;
 }
 __device__ __forceinline__ int tile_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
+
+// One 16 x 16 output tile of v_mfma_f32_16x16x4_f32: lane l supplies A(l & 15, 4s + (l >> 4)) and
+// B(4s + (l >> 4), l & 15); register r of lane l holds row 4 (l >> 4) + r, column l & 15.  The
+// same f32 products accumulated in k order as the 32 x 32 form, on tiles that fit N = 100 and
+// H = 69 with less padding (7 x 5 tiles of 16 vs 4 x 3 of 32: 0.77 of the MACs useful vs 0.56)
+// and spread evenly over the 8 waves (35 / 25 tiles instead of 12 / 9).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <class FA, class FB>
+__device__ __forceinline__ f32x4 mfma_tile16(int K, FA fa, FB fb) {
+  const int lane = threadIdx.x & 63, l15 = lane & 15, kq = lane >> 4;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 6
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const int k = k0 + kq;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa(l15, k), fb(k, l15), acc, 0, 0, 0);
+  }
+  return acc;
+}
+__device__ __forceinline__ int tile_row16(int r) { return 4 * ((threadIdx.x & 63) >> 4) + r; }
+#ifndef NMX_BNN_TILE
+#define NMX_BNN_TILE 16  // 16: v_mfma_f32_16x16x4_f32 tiles; 32: the 32 x 32 x 2 form (A/B)
+#endif
 
 struct BnnDims {
   int N, Dx, H;
@@ -174,8 +197,24 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
   __syncthreads();
 
-  // h2 = tanh(h1 W2): 32 x 32 tiles over (n, j), K = i
+  // h2 = tanh(h1 W2): tiles over (n, j), K = i
   const int wv = t >> 6, l31 = t & 31;
+#if NMX_BNN_TILE == 16
+  const int l15 = t & 15;
+  const int mtn = (N + 15) / 16, mth = (H + 15) / 16;
+  for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
+    const int n0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
+    const f32x4 acc = mfma_tile16(
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[k * H + j0 + c] : 0.0f; });
+    const int j = j0 + l15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + tile_row16(r);
+      if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
+    }
+  }
+#else
   const int ntn = (N + 31) / 32, nth = (H + 31) / 32;
   for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
     const int n0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
@@ -189,6 +228,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
       if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
     }
   }
+#endif
   __syncthreads();
 
   // yhat = h2 w3; residual; dU/dyhat = -p (Y - yhat)
@@ -220,7 +260,21 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
   __syncthreads();
 
-  // grad W2 = W2 + h1^T ga2: 32 x 32 tiles over (i, j), K = n
+  // grad W2 = W2 + h1^T ga2: tiles over (i, j), K = n
+#if NMX_BNN_TILE == 16
+  for (int tile = wv; tile < mth * mth; tile += NWAVES) {
+    const int i0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
+    const f32x4 acc = mfma_tile16(
+        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[k * H + i0 + m] : 0.0f; },
+        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[k * H + j0 + c] : 0.0f; });
+    const int j = j0 + l15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + tile_row16(r);
+      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
+    }
+  }
+#else
   for (int tile = wv; tile < nth * nth; tile += NWAVES) {
     const int i0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
     const f32x16 acc = mfma_tile(
@@ -233,10 +287,29 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
       if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
     }
   }
+#endif
   __syncthreads();
 
-  // ga1 = (ga2 W2^T) * (1 - h1^2): 32 x 32 tiles over (n, i), K = j, in place of h1 (a tile
-  // reads h1 only at its own elements; grad W2 above finished reading h1 at the barrier)
+  // ga1 = (ga2 W2^T) * (1 - h1^2): tiles over (n, i), K = j, in place of h1 (a tile reads h1
+  // only at its own elements; grad W2 above finished reading h1 at the barrier)
+#if NMX_BNN_TILE == 16
+  for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
+    const int n0 = (tile / mth) * 16, i0 = (tile % mth) * 16;
+    const f32x4 acc = mfma_tile16(
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[(i0 + c) * H + k] : 0.0f; });
+    const int i = i0 + l15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + tile_row16(r);
+      if (n < N && i < H) {
+        float* hp = &h1[n * H + i];
+        const float hv = *hp;
+        *hp = acc[r] * (1.0f - hv * hv);
+      }
+    }
+  }
+#else
   for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
     const int n0 = (tile / nth) * 32, i0 = (tile % nth) * 32;
     const f32x16 acc = mfma_tile(
@@ -253,6 +326,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
       }
     }
   }
+#endif
   __syncthreads();
 
   // grad W1 = W1 + X^T ga1

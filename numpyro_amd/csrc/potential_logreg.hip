@@ -95,6 +95,28 @@ constexpr float LN2 = 0.6931471805599453f;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// One 32x32x16 bf16 product.  NMX_X3_SHAPE16_PROBE (timing experiment only, wrong results): each
+// is replaced by two v_mfma_f32_16x16x32_bf16 on the same operand registers into two 4-register
+// slices of the accumulator -- the same matrix-pipe cycles (2 x 16 vs 32), VALU and LDS traffic --
+// to measure what the 16x16 shape's clock gives this kernel before rewriting its layouts
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7, cdna_hip_programming.md rule 28).
+template <int S = 0>
+__device__ __forceinline__ f32x16 x3_mma(const bf16x8& a, const bf16x8& b, f32x16 acc) {
+#ifdef NMX_X3_SHAPE16_PROBE
+  // slices (0-3, 8-11) for S = 0, (4-7, 12-15) for S = 1: calls alternate S, every register lives
+  constexpr int o = 4 * S;
+  f32x4 lo = {acc[o], acc[o + 1], acc[o + 2], acc[o + 3]};
+  f32x4 hi = {acc[8 + o], acc[9 + o], acc[10 + o], acc[11 + o]};
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, hi, 0, 0, 0);
+  acc[o] = lo[0]; acc[o + 1] = lo[1]; acc[o + 2] = lo[2]; acc[o + 3] = lo[3];
+  acc[8 + o] = hi[0]; acc[9 + o] = hi[1]; acc[10 + o] = hi[2]; acc[11 + o] = hi[3];
+  return acc;
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+#endif
+}
+
 // VALU instructions the scheduling hints place after each GEMM1(k+1) / GEMM2(k) MFMA (x3_item)
 #ifndef NMX_X3_VALU1
 #define NMX_X3_VALU1 5
@@ -257,18 +279,18 @@ __device__ __forceinline__ f32x16 x3_gemm1(const bf16x8* fr, const bf16x8 (&z1)[
   for (int kb = 0; kb < KB - H; ++kb) {
     const bf16x8 a1 = fr[x3_ai<KB, COMPACT>(0, kb) * 64], a2 = fr[x3_ai<KB, COMPACT>(1, kb) * 64],
                  a3 = fr[x3_ai<KB, COMPACT>(2, kb) * 64];
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], acc, 0, 0, 0);
+    acc = x3_mma<0>(a3, z1[kb], acc);
+    acc = x3_mma<1>(a2, z2[kb], acc);
+    acc = x3_mma<0>(a1, z3[kb], acc);
+    acc = x3_mma<1>(a2, z1[kb], acc);
+    acc = x3_mma<0>(a1, z2[kb], acc);
+    acc = x3_mma<1>(a1, z1[kb], acc);
   }
   if constexpr (H) {
     const bf16x8 c0 = fr[x3_ci<KB, COMPACT>(0) * 64], c1 = fr[x3_ci<KB, COMPACT>(1) * 64];
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, z3[KB - 1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, z2[KB - 1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, z1[KB - 1], acc, 0, 0, 0);
+    acc = x3_mma<0>(c1, z3[KB - 1], acc);
+    acc = x3_mma<1>(c0, z2[KB - 1], acc);
+    acc = x3_mma<0>(c0, z1[KB - 1], acc);
   }
   return acc;
 }
@@ -383,12 +405,12 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
       const bf16x8 b1 = fr[(G2 + 0 * 2 * DT + 2 * dt + s) * 64];
       const bf16x8 b2 = fr[(G2 + 1 * 2 * DT + 2 * dt + s) * 64];
       const bf16x8 b3 = fr[(G2 + 2 * 2 * DT + 2 * dt + s) * 64];
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
+      g[dt] = x3_mma<1>(b3, r1, g[dt]);
+      g[dt] = x3_mma<0>(b2, r2, g[dt]);
+      g[dt] = x3_mma<1>(b1, r3, g[dt]);
+      g[dt] = x3_mma<0>(b2, r1, g[dt]);
+      g[dt] = x3_mma<1>(b1, r2, g[dt]);
+      g[dt] = x3_mma<0>(b1, r1, g[dt]);
     }
   }
 }

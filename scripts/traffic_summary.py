@@ -1,0 +1,70 @@
+"""Per-kernel HBM bytes from the FETCH_SIZE / WRITE_SIZE passes of scripts/pmc_traffic.sh, per
+MI355X_MICROARCH.md's HBM section: FETCH_SIZE (KB) doubled on gfx950 (it reports 1/2 of wide
+streaming reads), WRITE_SIZE (KB) as is, x 1024 B.  For each workload and kernel: dispatches, the
+median bytes per dispatch, the total, and -- for the NUTS workloads, whose logs end with the
+bench_configs JSON line (leapfrogs of the warmup and the timed run) -- bytes per chain-leapfrog.
+usage: python scripts/traffic_summary.py gpurun_out/traffic > summary.json"""
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+KERNELS = {"logreg": ["k_logreg_x3<", "k_logreg_finalize"], "sv": ["k_wide_persistent"],
+           "gemm": ["k_gemm_x3<"], "funnel": ["k_gemm_x3<", "k_chain_step", "k_x3_split_b", "k_pack_rows",
+                                               "k_unpack_rows", "k_wide_fin", "k_wide_part"]}
+
+
+def per_dispatch(d, counter, pat):
+    vals = defaultdict(float)
+    names = {}
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] != counter or pat not in row["Kernel_Name"]:
+                    continue
+                key = (path, row.get("Dispatch_Id", row.get("Correlation_Id")))
+                vals[key] += float(row["Counter_Value"])
+                names[key] = row["Kernel_Name"]
+    return vals, names
+
+
+def leapfrogs(log):
+    try:
+        with open(log) as f:
+            for line in f:
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    return d.get("leapfrogs", 0) + d.get("warmup_leapfrogs", 0)
+    except OSError:
+        pass
+    return None
+
+
+out = {}
+for w, pats in KERNELS.items():
+    wd = os.path.join(root, w)
+    if not os.path.isdir(wd):
+        continue
+    lf = leapfrogs(os.path.join(wd, "f.log"))
+    for pat in pats:
+        fv, names = per_dispatch(os.path.join(wd, "f"), "FETCH_SIZE", pat)
+        wv, _ = per_dispatch(os.path.join(wd, "w"), "WRITE_SIZE", pat)
+        if not fv:
+            continue
+        fb = [2.0 * v * 1024 for v in fv.values()]
+        wb = [v * 1024 for v in wv.values()]
+        name = re.sub(r"\(.*", "", sorted(set(names.values()))[0]).replace("void ", "").replace("(anonymous namespace)::", "")
+        rec = {"kernel": name, "dispatches": len(fb), "read_bytes_median": statistics.median(fb),
+               "write_bytes_median": statistics.median(wb) if wb else None,
+               "hbm_bytes_per_dispatch_median": statistics.median(fb) + (statistics.median(wb) if wb else 0.0),
+               "hbm_bytes_total": sum(fb) + sum(wb)}
+        if lf:
+            rec["chain_leapfrogs"] = lf
+            rec["hbm_bytes_per_chain_leapfrog"] = rec["hbm_bytes_total"] / lf
+        out[f"{w}:{pat}"] = rec
+print(json.dumps(out, indent=1))
