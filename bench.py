@@ -138,6 +138,8 @@ def _located_parity(hist, dev_trace, dev_ns, dev_z, atol, rtol=0.0, to_model=Non
 # transitions, dense mass, roofline basis, CPU-comparator potential).  Each runs in an adapted
 # regime (mcmc.warmup with the reference's window schedule), the timed transitions after it.
 def _config_specs():
+    import numpy as np
+
     from numpyro_amd import datasets
     from numpyro_amd import potentials as P
     from oracle import batched as OB
@@ -150,17 +152,17 @@ def _config_specs():
         "c2": dict(name="funnel D=10000, dense mass (pooled), examples/funnel.py", model=P.funnel, args=(10000,),
                    chains=4096, warmup=CONFIG_WARMUP["c2"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * 10000 * 10000, basis="2 D^2 FLOP per chain-leapfrog (z = mu + T w, g_w = T^T g_z)",
-                   cpu=lambda: OB.FunnelBatch(10000), cpu_chains=16),
+                   cpu=lambda dt=np.float32: OB.FunnelBatch(10000, dtype=dt), cpu_chains=16),
         "c3": dict(name="BNN D_X=3 N=100 H=69 (D=5038), dense mass (pooled), examples/bnn.py", model=P.bnn,
                    args=(X, Y, H), chains=2048, warmup=CONFIG_WARMUP["c3"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * D_bnn * D_bnn + 6.0 * 100 * H * H + 6.0 * 100 * 3 * H,
                    basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog",
-                   cpu=lambda: OB.BNNBatch(X, Y, H), cpu_chains=16),
+                   cpu=lambda dt=np.float32: OB.BNNBatch(X, Y, H, dtype=dt), cpu_chains=16),
         "c4": dict(name="stochastic volatility T=2517 (D=2519), diag mass, examples/stochastic_volatility.py",
                    model=P.stochastic_volatility, args=(r,), chains=8192, warmup=CONFIG_WARMUP["c4"],
                    steps=10, dense=False, one_gpu=False, bytes=7 * 4 * 2519,
                    basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)",
-                   cpu=lambda: OB.SVBatch(r), cpu_chains=32),
+                   cpu=lambda dt=np.float32: OB.SVBatch(r, dtype=dt), cpu_chains=32),
     }
 
 
@@ -216,7 +218,50 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
            "potential_share": stats["pot_s"] / dt, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
     par = _located_parity(hist, dev_trace, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model,
                           label=f"parity {sp['name'].split(',')[0]}")
+    # rounding calibration (oracle/parity.py): the same chains and transitions under the potential
+    # in rounded float64 -- how far two float32-level implementations drift apart on this workload
+    T = min(len(h) for h in hist)
+    if T > 0:
+        from oracle import parity as PR
+
+        f64 = sp["cpu"](np.float64)
+        if eng.dense:
+            f64 = OB.Whitened(f64, wt.T.cpu().numpy(), wt.mu.cpu().numpy(), dtype=np.float64)
+        states, oracles = CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"],
+                                               st["mass_sqrt"], eng.iteration, seed, eng.num_warmup,
+                                               chain_offset=eng.chain_offset)
+        _, hist64, _, _ = CB.run_chains(f64, states, oracles, T, record=True)
+        ctr, cns, cz = _oracle_trace(hist64, dev_trace.shape[2])
+        if to_model is not None:
+            cz = np.stack([[to_model(w) for w in cc] for cc in cz])
+        cal = PR.compare_traced([h[:T] for h in hist], ctr, cns, cz, atol=1e-3, rtol=1e-3, to_model=to_model)
+        dev_T = PR.compare_traced([h[:T] for h in hist], dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3,
+                                  rtol=1e-3, to_model=to_model)
+        ok, msg = PR.like_calibration(dev_T, cal)
+        par["calibration"] = {"basis": "oracle (float32 batch) vs the oracle with the potential in rounded float64, "
+                                       f"same chains, first {T} transitions", **PR.counts(cal),
+                              "max_dE_err": cal["max_dE_err"], "device_like_calibration": ok}
+        print(f"[parity {sp['name'].split(',')[0]}] {msg}", file=sys.stderr)
     return out, par
+
+
+def _oracle_trace(hist, L):
+    """An oracle run in the device trace layout (oracle/parity.py oracle_to_trace)."""
+    import numpy as np
+
+    from oracle import parity as PR
+
+    C, T = len(hist), min(len(h) for h in hist)
+    tr = np.full((T, C, L, 8), np.nan, np.float32)
+    ns = np.zeros((C, T), np.int64)
+    z = np.zeros((C, T, np.size(hist[0][0][0].z)))
+    for c, h in enumerate(hist):
+        for t in range(T):
+            st_, _, leaves = h[t]
+            tr[t, c] = PR.oracle_to_trace(leaves, L)
+            ns[c, t] = st_.num_steps
+            z[c, t] = st_.z
+    return tr, ns, z
 
 
 def secondary_configs(which, rank, world, device, cpu_seconds):
@@ -240,8 +285,11 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
         lo, hi = shard_chains(sp["chains"], rank, world)
         # postprocess_fn: the draws stay unconstrained (model coordinates), as the CPU
         # comparator's chains hold them
+        # vectorized: this rank's chains on its own GPU (chain_method="parallel" would spread a
+        # single process over every visible GPU)
         mcmc = MCMC(NUTS(sp["model"], dense_mass=sp["dense"]), num_warmup=sp["warmup"], num_samples=sp["steps"],
-                    num_chains=hi - lo, chain_offset=lo, progress_bar=False, postprocess_fn=_identity)
+                    num_chains=hi - lo, chain_offset=lo, progress_bar=False, postprocess_fn=_identity,
+                    chain_method="vectorized")
         t0 = time.perf_counter()
         mcmc._fields_only = True  # the adaptation's tree sizes and divergences, not its draws
         mcmc.warmup(7, *sp["args"], collect_warmup=True, extra_fields=("num_steps", "diverging"))

@@ -100,7 +100,8 @@ class Timed:
 def run_model(name, model, args, chains, warmup, steps, flops_per_leapfrog=None, bytes_per_leapfrog=None,
               **kernel_kw):
     kernel = NUTS(model, **kernel_kw)
-    mcmc = MCMC(kernel, num_warmup=warmup, num_samples=steps, num_chains=chains, progress_bar=False)
+    mcmc = MCMC(kernel, num_warmup=warmup, num_samples=steps, num_chains=chains, progress_bar=False,
+                chain_method="vectorized")
     t0 = time.time()
     mcmc._fields_only = True  # warmup transitions' fields (tree sizes, divergences), no draws
     mcmc.warmup(0, *args, collect_warmup=True, extra_fields=("num_steps", "diverging"))
