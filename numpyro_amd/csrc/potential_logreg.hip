@@ -818,10 +818,14 @@ constexpr int X3_ROLE_WAVES = 8;
 // only for the DMAs of the tile pair it needs (A(k+1), labels(k)), leaving the later PA - 2
 // pairs in flight (counted vmcnt: with a plain vmcnt(0) every barrier waited for the DMAs
 // issued one iteration earlier, so the HBM latency was exposed once per tile whatever the
-// depth -- round 3 measured 2, 3 and 4 slots equal).  LDS at PA = 4: 6 A slots x 14 KB + 5
-// label slots + 32 KB of residual slots = 121 KB, one workgroup per CU as before.
+// depth -- round 3 measured 2, 3 and 4 slots equal).  Depth A/B with the counted waits
+// (profiles/r04/ab_tail_prefetch.txt): PA = 2 / 4 / 6 at 1-32 chains 0.077-0.078 / 0.085 /
+// 0.089-0.090 ms per evaluation, at 256 chains 0.235 / 0.247 / 0.255 ms; bench --chains 512
+// seeds 0-2 1.013M / 1.092M / 0.877M at PA = 2 vs 1.003M / 1.081M / 0.867M at 4: the deeper
+// rings cost more in LDS-DMA issue and barrier waits than they hide.  LDS at PA = 2: 4 A slots
+// x 14 KB + 3 label slots + 32 KB of residual slots = 91 KB, one workgroup per CU.
 #ifndef NMX_X3_ROLE_PA
-#define NMX_X3_ROLE_PA 4
+#define NMX_X3_ROLE_PA 2
 #endif
 constexpr int X3_ROLE_PA = NMX_X3_ROLE_PA;
 
