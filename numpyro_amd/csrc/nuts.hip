@@ -622,6 +622,15 @@ struct VecCtx {
   bool unit;  // cfg.unit_mass: inv_mass == mass_sqrt == 1, not loaded
 };
 
+// The frontier (the moving end's position z_eval, its gradient g_eval and its momentum, RR or RL
+// by the tree direction) of the persistent wide kernel's chain, LDS-resident when the kernel
+// carries it (k_wide_persistent<..., CARRY>): [D] floats each, row d at byte d * 4.
+struct Front {
+  float* z;
+  float* g;
+  float* r;
+};
+
 // L1 + L2 minus the proposal copy: finish the pending leapfrog (hmc_util.py:306-308),
 // kinetic energy, subtree r_sum, checkpoints and the U-turn partial dots.
 // red[0] = KE partial, red[1 + 2i + side] = checkpoint i, red[1 + 2 MAXD + side] = tree.
@@ -763,11 +772,22 @@ struct ApplyIn {
 
 __device__ __forceinline__ bool turn_around(const Act& A) { return A.prep_leaf && A.new_dir != A.dirR; }
 
-__device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32_t off, ApplyIn& x) {
+// CARRY (the persistent wide kernel with an LDS frontier, row d): the frontier's position,
+// gradient and momentum come from and go to fr; the arena's copies are written only where the
+// trajectory leaves them behind (a turn-around parks the frontier in its side arrays, RR / RL
+// included) and at the kernel's exit
+template <bool CARRY = false>
+__device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32_t off, ApplyIn& x,
+                                           const Front& fr = {}, int d = 0) {
   const Arena& a = *v.a;
   if (A.take_leaf || A.hmc_accept || A.prep_leaf) {
-    x.ze = nmx_at(AV(NMX_F_Z_EVAL), off);
-    x.ge = nmx_at(AV(NMX_F_G_EVAL), off);
+    if constexpr (CARRY) {
+      x.ze = fr.z[d];
+      x.ge = fr.g[d];
+    } else {
+      x.ze = nmx_at(AV(NMX_F_Z_EVAL), off);
+      x.ge = nmx_at(AV(NMX_F_G_EVAL), off);
+    }
   }
   if (A.done_sub) {
     x.rst = nmx_at(AV(NMX_F_RSUM), off);
@@ -790,7 +810,8 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32
   if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
   if (A.prep_leaf) {
     const int nd = A.new_dir;
-    x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+    if (CARRY && !turn_around(A)) x.rfn = fr.r[d];  // the frontier keeps growing
+    else x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
     if (turn_around(A)) {
       x.zfn = nmx_at((nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL)), off);
       x.gfn = nmx_at((nd ? AV(NMX_F_GR) : AV(NMX_F_GL)), off);
@@ -803,9 +824,11 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32
 
 // Returns the momentum KE partial (start_iter).
 // soff: offset of the row in the samples buffer ([S][D][ldc]; default: off, the arena's layout)
+template <bool CARRY = false>
 __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, float step_eff, int d, uint32_t off,
                                              ApplyIn& x, float mom, float* samp, const int8_t* transform,
-                                             const nmx_nuts_config& cfg, uint32_t soff = 0xFFFFFFFFu) {
+                                             const nmx_nuts_config& cfg, uint32_t soff = 0xFFFFFFFFu,
+                                             const Front& fr = {}) {
   const Arena& a = *v.a;
   if (A.take_leaf) {
     nmx_at(AV(NMX_F_ZSUB), off) = x.ze;
@@ -872,16 +895,27 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       nmx_at((nd ? AV(NMX_F_GL) : AV(NMX_F_GR)), off) = g;
       nmx_at((nd ? AV(NMX_F_RL) : AV(NMX_F_RR)), off) = r;
       const float rh = r - half * g;
-      nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
-      nmx_at(ZE, off) = z + es * (im * rh);
+      if constexpr (CARRY) {
+        fr.r[d] = rh;
+        fr.z[d] = z + es * (im * rh);
+      } else {
+        nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
+        nmx_at(ZE, off) = z + es * (im * rh);
+      }
     } else {
       if (turn_around(A)) {
         nmx_at((A.dirR ? AV(NMX_F_ZR) : AV(NMX_F_ZL)), off) = x.ze;
         nmx_at((A.dirR ? AV(NMX_F_GR) : AV(NMX_F_GL)), off) = x.ge;
+        if constexpr (CARRY) nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = fr.r[d];
       }
       const float rh = x.rfn - half * x.gfn;
-      nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
-      nmx_at(ZE, off) = x.zfn + es * (im * rh);
+      if constexpr (CARRY) {
+        fr.r[d] = rh;
+        fr.z[d] = x.zfn + es * (im * rh);
+      } else {
+        nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = rh;
+        nmx_at(ZE, off) = x.zfn + es * (im * rh);
+      }
     }
   }
   return ke0;
@@ -1139,6 +1173,9 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
 #ifndef NMX_PX_B
 #define NMX_PX_B 2  // rows per thread in flight in the persistent wide kernel (profiles/r03/ab_persistent_occ.txt)
+#endif
+#ifndef NMX_PX_BL
+#define NMX_PX_BL NMX_PX_B  // the same in its leaf phase
 #endif
 #ifndef NMX_V1_ROWS
 #define NMX_V1_ROWS 1
@@ -1617,10 +1654,19 @@ struct PRow {
   float rf, im, rs_old, rst, ro, ckr, ckrs;
 };
 
-template <bool NUTS>
-__device__ __forceinline__ void prow_load(const VecCtx& v, const Act& A, uint32_t off, PRow& x) {
+// frontier momentum of row d: the LDS carry (CARRY) or the arena (byte offset off)
+template <bool CARRY>
+__device__ __forceinline__ float& front_r(const VecCtx& v, const Act& A, const Front& fr, uint32_t off, int d) {
   const Arena& a = *v.a;
-  x.rf = nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+  if constexpr (CARRY) return fr.r[d];
+  else return nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+}
+
+template <bool NUTS, bool CARRY = false>
+__device__ __forceinline__ void prow_load(const VecCtx& v, const Act& A, uint32_t off, PRow& x, const Front& fr = {},
+                                          int d = 0) {
+  const Arena& a = *v.a;
+  x.rf = front_r<CARRY>(v, A, fr, off, d);
   x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
   if constexpr (NUTS) {
     x.rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
@@ -1636,14 +1682,17 @@ __device__ __forceinline__ void prow_load(const VecCtx& v, const Act& A, uint32_
 }
 
 // red[0] KE, red[1 + 2 MAXD + side] tree dots; dl / dr: the dots of checkpoint level imin
-template <bool NUTS>
+// TL: the index of the tree dots in red (red[0] = KE): the full partial-sum vector's 1 + 2 MAXD,
+// or 1 in the persistent kernel's compact accumulators (persist_leaf_rows)
+template <bool NUTS, bool CARRY = false, int TL = 1 + 2 * MAXD>
 __device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float seff, uint32_t off, const PRow& x,
-                                           float g, float* red, float& dl, float& dr) {
+                                           float g, float* red, float& dl, float& dr, const Front& fr = {},
+                                           int d = 0) {
   const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
   const float r = x.rf - half * g;
-  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
+  front_r<CARRY>(v, A, fr, off, d) = r;
   const float im = x.im;
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
@@ -1665,20 +1714,26 @@ __device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float 
       const float rlv = A.dirR ? x.ro : r;
       const float rrv = A.dirR ? r : x.ro;
       const float rss2 = rst - (rlv + rrv) / 2.0f;
-      red[1 + 2 * MAXD] += (im * rlv) * rss2;
-      red[2 + 2 * MAXD] += (im * rrv) * rss2;
+      red[TL] += (im * rlv) * rss2;
+      red[TL + 1] += (im * rrv) * rss2;
     }
   }
 }
 
-template <bool NUTS, int NT, int B, class M>
+template <bool NUTS, int NT, int B, bool CARRY, class M>
 __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A, const M& m,
-                                                  const typename M::Glob& gl, float seff, uint32_t base, float* red) {
+                                                  const typename M::Glob& gl, float seff, uint32_t base, float* red,
+                                                  const Front& fr) {
   const Arena& a = *v.a;
   const float* ZE = AV(NMX_F_Z_EVAL);
   float* GE = AV(NMX_F_G_EVAL);
   const int hi = m.hi();
   float dl = 0.0f, dr = 0.0f;
+  // compact accumulators through the row loop (KE, the tree dots, the model's sums: the unused
+  // checkpoint entries of red stay out of the registers), expanded into red after it
+  float acc[3 + M::NSUM];
+#pragma unroll
+  for (int i = 0; i < 3 + M::NSUM; ++i) acc[i] = 0.0f;
   for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B * NT) {
     PRow x[B];
     typename M::RowIn mi[B];
@@ -1687,8 +1742,9 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
       const int d = d0 + q * NT;
       if (d < hi) {
         const uint32_t off = base + ((uint32_t)d << 2);
-        prow_load<NUTS>(v, A, off, x[q]);
-        m.row_load(ZE, off, 4u, d, mi[q]);
+        prow_load<NUTS, CARRY>(v, A, off, x[q], fr, d);
+        if constexpr (CARRY) m.row_load(fr.z, (uint32_t)d << 2, 4u, d, mi[q]);  // stencil neighbours too
+        else m.row_load(ZE, off, 4u, d, mi[q]);
       }
     }
 #pragma unroll
@@ -1696,12 +1752,18 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
       const int d = d0 + q * NT;
       if (d < hi) {
         const uint32_t off = base + ((uint32_t)d << 2);
-        const float g = m.row_eval(mi[q], d, gl, red + NPART);
-        nmx_at(GE, off) = g;
-        prow_store<NUTS>(v, A, seff, off, x[q], g, red, dl, dr);
+        const float g = m.row_eval(mi[q], d, gl, acc + 3);
+        if constexpr (CARRY) fr.g[d] = g;
+        else nmx_at(GE, off) = g;
+        prow_store<NUTS, CARRY, 1>(v, A, seff, off, x[q], g, acc, dl, dr, fr, d);
       }
     }
   }
+  red[0] += acc[0];
+  red[1 + 2 * MAXD] += acc[1];
+  red[2 + 2 * MAXD] += acc[2];
+#pragma unroll
+  for (int k = 0; k < M::NSUM; ++k) red[NPART + k] += acc[3 + k];
   if constexpr (NUTS) {
 #pragma unroll
     for (int i = 0; i < MAXD; ++i)
@@ -1715,9 +1777,9 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
 // U-turn dots of checkpoint levels imin + 1 .. imax (after wave_sums_to_lds): one pass over the
 // thread's model rows per level, reloading the momentum / r_sum this leaf stored; each level's
 // wave sums go straight to its LDS entries.
-template <int NW, int NT, class M>
+template <int NW, int NT, bool CARRY = false, class M>
 __device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& A, const M& m, uint32_t base,
-                                                    float* lds) {
+                                                    float* lds, const Front& fr = {}) {
   constexpr int B2 = 4;
   const Arena& a = *v.a;
   const float* RF = A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL);
@@ -1736,7 +1798,8 @@ __device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& 
         const int d = d0 + q * NT;
         if (d < hi) {
           const uint32_t off = base + ((uint32_t)d << 2);
-          r[q] = nmx_at(RF, off);
+          if constexpr (CARRY) r[q] = fr.r[d];
+          else r[q] = nmx_at(RF, off);
           rs[q] = nmx_at(RS, off);
           im[q] = v.unit ? 1.0f : nmx_at(IM, off);
           rl[q] = nmx_at(CK, off);
@@ -1762,11 +1825,11 @@ __device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& 
 }
 
 // apply rows of thread t (model rows as in the leaf phase, then thread 0's scalar-site rows)
-template <int NT, int B, class M>
+template <int NT, int B, bool CARRY = false, class M>
 __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& A, const M& m, float step_eff,
                                                    uint32_t base, int c, uint64_t seed, uint32_t gch, int it,
                                                    float* samp, const int8_t* transform,
-                                                   const nmx_nuts_config& cfg) {
+                                                   const nmx_nuts_config& cfg, const Front& fr = {}) {
   float ke0 = 0.0f;
   const int hi = m.hi();
   auto rows = [&](int d0, int dstep, int dend, auto bc) {
@@ -1777,7 +1840,7 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
 #pragma unroll
       for (int q = 0; q < BB; ++q) {
         const int d = d0 + q * dstep;
-        if (d < dend) apply_load(v, A, base + ((uint32_t)d << 2), x[q]);
+        if (d < dend) apply_load<CARRY>(v, A, base + ((uint32_t)d << 2), x[q], fr, d);
       }
 #pragma unroll
       for (int q = 0; q < BB; ++q) {
@@ -1794,8 +1857,8 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
       for (int q = 0; q < BB; ++q) {
         const int d = d0 + q * dstep;
         if (d < dend)
-          ke0 += apply_store(v, A, step_eff, d, base + ((uint32_t)d << 2), x[q], n[q], samp, transform, cfg,
-                             nmx_row_off(d, v.ldc, c));
+          ke0 += apply_store<CARRY>(v, A, step_eff, d, base + ((uint32_t)d << 2), x[q], n[q], samp, transform, cfg,
+                                    nmx_row_off(d, v.ldc, c), fr);
       }
     }
   };
@@ -1849,14 +1912,14 @@ __device__ __forceinline__ const float* spre_src(const VecCtx& v, const Act& A, 
 }
 
 // leaf_load + leaf_store of one scalar-site row from its prefetched inputs (same arithmetic)
-template <bool NUTS>
+template <bool NUTS, bool CARRY = false>
 __device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float seff, uint32_t off, float g,
-                                          const float* pre, float* red) {
+                                          const float* pre, float* red, const Front& fr = {}, int d = 0) {
   const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
   const float r = pre[0] - half * g;
-  nmx_at((A.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = r;
+  front_r<CARRY>(v, A, fr, off, d) = r;
   const float im = v.unit ? 1.0f : pre[1];
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
@@ -1890,7 +1953,12 @@ __device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float s
 #ifndef NMX_PX_OCC
 #define NMX_PX_OCC 4  // waves per SIMD the kernel is compiled for: <= 128 VGPRs (3 waves: SV 8192 20.0M vs 24.2M)
 #endif
-template <int NT, int B, class M>
+// CARRY: the chain's frontier (Front) lives in LDS for the whole launch (12 D bytes of dynamic LDS,
+// within the occupancy the kernel is compiled for: persist_carry): per leaf and row the arena
+// then sees the subtree r_sum, the U-turn checkpoints, the inverse mass and the proposal copies,
+// not the frontier's position, gradient and momentum (loaded at entry, written back at exit and
+// at turn-arounds), and the stencil reads its neighbours from LDS.  Same arithmetic, bitwise equal.
+template <int NT, int B, class M, bool CARRY>
 __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
   constexpr int NW = NT / 64;
   constexpr int NR = NPART + M::NSUM;
@@ -1922,15 +1990,32 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     NMX_DCHECK(S.phase == NMX_PH_START || S.phase == NMX_PH_LEAF);
     Ssh = S;
   }
-  __syncthreads();
   const uint32_t base = ((uint32_t)c * (uint32_t)D) << 2;  // byte offset of the chain's row 0
+  extern __shared__ float front_lds[];
+  const Front fr{front_lds, front_lds + D, front_lds + 2 * D};
+  if constexpr (CARRY) {
+    // the frontier of the pending leaf (START: overwritten by the momentum draw before any use)
+    const int dir0 = uni_i(AI(NMX_F_DIR)[c]);
+    const float* ZE = AV(NMX_F_Z_EVAL);
+    const float* GE = AV(NMX_F_G_EVAL);
+    const float* RF = dir0 ? AV(NMX_F_RR) : AV(NMX_F_RL);
+    for (int d = tid; d < D; d += NT) {
+      const uint32_t off = base + ((uint32_t)d << 2);
+      fr.z[d] = nmx_at(ZE, off);
+      fr.g[d] = nmx_at(GE, off);
+      fr.r[d] = nmx_at(RF, off);
+    }
+  }
+  __syncthreads();
   for (int step = 0; step < max_steps; ++step) {
     // the field pointers are recomputed each leaf (cheap scalar arithmetic) rather than
     // hoisted out of the loop: ~40 loop-invariant 64-bit pointers overflowed the SGPRs
     Arena al = Pk.a;
-    asm volatile("" : "+s"(al.sbase), "+s"(al.vbase), "+s"(al.ckr), "+s"(al.ckrs), "+s"(al.sstride), "+s"(al.vstride));
     size_t ck_stride = (size_t)D * ldc;
+#ifndef NMX_DEBUG  // (the debug build's checks leave some of them in VGPRs: no SGPR constraint there)
+    asm volatile("" : "+s"(al.sbase), "+s"(al.vbase), "+s"(al.ckr), "+s"(al.ckrs), "+s"(al.sstride), "+s"(al.vstride));
     asm volatile("" : "+s"(ck_stride));
+#endif
     const VecCtx v{&al, ldc, D, ck_stride, cfg.unit_mass != 0};
     const int ph = uni_i(Ssh.phase);
     if (ph == NMX_PH_DONE) break;
@@ -1956,20 +2041,20 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         const int i = lane / SPRE, f = lane % SPRE;
         const float* src = spre_src(v, A, is_nuts, f);
         if (src) {
-          pv = nmx_at(src, base + ((uint32_t)m.scalar_row(i) << 2));
+          pv = (CARRY && f == 0) ? fr.r[m.scalar_row(i)] : nmx_at(src, base + ((uint32_t)m.scalar_row(i) << 2));
           pl = true;
         }
       }
-      const typename M::Glob gl = m.globals_at(AV(NMX_F_Z_EVAL), base, 4u);
+      const typename M::Glob gl = CARRY ? m.globals_at(fr.z, 0u, 4u) : m.globals_at(AV(NMX_F_Z_EVAL), base, 4u);
       {
         float red[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) red[i] = 0.0f;
-        if (is_nuts) persist_leaf_rows<true, NT, B>(v, A, m, gl, seff, base, red);
-        else persist_leaf_rows<false, NT, B>(v, A, m, gl, seff, base, red);
+        if (is_nuts) persist_leaf_rows<true, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
+        else persist_leaf_rows<false, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
-      if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT>(v, A, m, base, lds);
+      if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT, CARRY>(v, A, m, base, lds, fr);
       if (pl) lds_pre[lane] = pv;
       PX_T(1);
       PX_ADD(0, 0, 1);
@@ -1997,10 +2082,12 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
           for (int e = 0; e < NPART; ++e) rs[e] = 0.0f;
 #pragma unroll
           for (int i = 0; i < M::NSCALAR; ++i) {
-            const uint32_t off = base + ((uint32_t)m.scalar_row(i) << 2);
-            nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
-            if (is_nuts) spre_leaf<true>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs);
-            else spre_leaf<false>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs);
+            const int d = m.scalar_row(i);
+            const uint32_t off = base + ((uint32_t)d << 2);
+            if constexpr (CARRY) fr.g[d] = gs[i];
+            else nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
+            if (is_nuts) spre_leaf<true, CARRY>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs, fr, d);
+            else spre_leaf<false, CARRY>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs, fr, d);
           }
 #pragma unroll
           for (int e = 0; e < NPART; ++e)
@@ -2063,8 +2150,8 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
       if (act & VEC) {
         float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc
                                                                          : nullptr;
-        ke0 = persist_apply_rows<NT, B>(v, D2, m, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp,
-                                        P.transform, cfg);
+        ke0 = persist_apply_rows<NT, B, CARRY>(v, D2, m, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp,
+                                               P.transform, cfg, fr);
       }
       if (D2.start_iter) {
         const float t = wave_sum(ke0);
@@ -2088,6 +2175,20 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         Ssh.E0 = Ssh.pe + 0.5f * t;  // build_tree :1130
         Ssh.energy = Ssh.E0;         // proposal energy of the initial tree (:1137)
       }
+    }
+  }
+  if constexpr (CARRY) {
+    // the frontier back to the arena (every thread passed the loop's last barrier: its LDS is final)
+    const Arena& al = Pk.a;
+    const int dir1 = uni_i(Ssh.dir);
+    float* ZE = reinterpret_cast<float*>(al.vbase + (size_t)(NMX_F_Z_EVAL - NMX_F_Z) * al.vstride);
+    float* GE = reinterpret_cast<float*>(al.vbase + (size_t)(NMX_F_G_EVAL - NMX_F_Z) * al.vstride);
+    float* RF = reinterpret_cast<float*>(al.vbase + (size_t)((dir1 ? NMX_F_RR : NMX_F_RL) - NMX_F_Z) * al.vstride);
+    for (int d = tid; d < D; d += NT) {
+      const uint32_t off = base + ((uint32_t)d << 2);
+      nmx_at(ZE, off) = fr.z[d];
+      nmx_at(GE, off) = fr.g[d];
+      nmx_at(RF, off) = fr.r[d];
     }
   }
   if (tid == 0) {
@@ -2802,21 +2903,43 @@ int persist_nt(int dim) {
   return dim <= 4096 ? 256 : 512;
 }
 
+// Whether the persistent kernel keeps the chain's frontier in LDS (k_wide_persistent CARRY): its
+// 12 D bytes beside the static LDS must fit the share of a CU's 160 KB that the compiled
+// occupancy (NMX_PX_OCC waves per SIMD, NT / 64 waves per workgroup) leaves each workgroup, so
+// the carry never costs resident chains (SV D = 2519 at NT = 256: 30 KB of 40; funnel-10k at
+// NT = 512: 120 KB of 80, not carried).  No effect on results (bitwise equal either way); the
+// debug / experiment builds can turn it off (NMX_PERSIST_CARRY=0) for A/B runs.
+bool persist_carry(int dim, int nt) {
+#if defined(NMX_DEBUG) || defined(NMX_EXPERIMENT)
+  if (const char* e = getenv("NMX_PERSIST_CARRY"))
+    if (atoi(e) == 0) return false;
+#endif
+  const size_t share = (size_t)160 * 1024 * nt / (64 * 4 * NMX_PX_OCC);
+  constexpr size_t STATIC_LDS = 4096;  // k_wide_persistent's own arrays (< 2 KB), with margin
+  return (size_t)12 * dim + STATIC_LDS <= share;
+}
+
+template <int NT, class M>
+void launch_persistent_nt(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
+  const dim3 grid(args.cfg.num_chains);
+  if (persist_carry(args.cfg.dim, NT)) {
+    const size_t lds = (size_t)12 * args.cfg.dim;
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k_wide_persistent<NT, NMX_PX_B, M, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, true>), grid, dim3(NT), lds, s, args, m, max_steps);
+  } else {
+    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, false>), grid, dim3(NT), 0, s, args, m, max_steps);
+  }
+}
+
 template <class M>
 int launch_persistent(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
-  const dim3 grid(args.cfg.num_chains);
   switch (persist_nt(args.cfg.dim)) {
-    case 128:
-      hipLaunchKernelGGL((k_wide_persistent<128, NMX_PX_B, M>), grid, dim3(128), 0, s, args, m, max_steps);
-      break;
-    case 256:
-      hipLaunchKernelGGL((k_wide_persistent<256, NMX_PX_B, M>), grid, dim3(256), 0, s, args, m, max_steps);
-      break;
-    case 512:
-      hipLaunchKernelGGL((k_wide_persistent<512, NMX_PX_B, M>), grid, dim3(512), 0, s, args, m, max_steps);
-      break;
-    default:
-      hipLaunchKernelGGL((k_wide_persistent<1024, NMX_PX_B, M>), grid, dim3(1024), 0, s, args, m, max_steps);
+    case 128: launch_persistent_nt<128>(args, m, max_steps, s); break;
+    case 256: launch_persistent_nt<256>(args, m, max_steps, s); break;
+    case 512: launch_persistent_nt<512>(args, m, max_steps, s); break;
+    default: launch_persistent_nt<1024>(args, m, max_steps, s);
   }
   return nmx_check_launch("k_wide_persistent");
 }

@@ -58,7 +58,8 @@ for w, pats in KERNELS.items():
             continue
         fb = [2.0 * v * 1024 for v in fv.values()]
         wb = [v * 1024 for v in wv.values()]
-        name = re.sub(r"\(.*", "", sorted(set(names.values()))[0]).replace("void ", "").replace("(anonymous namespace)::", "")
+        name = sorted(set(names.values()))[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        name = re.sub(r"\(.*", "", name)
         rec = {"kernel": name, "dispatches": len(fb), "read_bytes_median": statistics.median(fb),
                "write_bytes_median": statistics.median(wb) if wb else None,
                "hbm_bytes_per_dispatch_median": statistics.median(fb) + (statistics.median(wb) if wb else 0.0),
