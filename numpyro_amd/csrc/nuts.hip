@@ -323,8 +323,15 @@ __device__ __forceinline__ void begin_act(const nmx_nuts_config& cfg, const Chai
 // Resolve WAIT (sync_chains) and set up the step's inputs.
 __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid,
                                           ChainScalars& S, Act& A) {
-  if (valid) load_scalars(a, c, S);
-  else S.phase = NMX_PH_DONE;
+  // the leaf's potential is loaded with the scalars, whatever the phase (a load behind the
+  // phase test would be one more dependent memory round per step)
+  float pe_ev = 0.0f;
+  if (valid) {
+    load_scalars(a, c, S);
+    pe_ev = AF(NMX_F_PE_EVAL)[c];
+  } else {
+    S.phase = NMX_PH_DONE;
+  }
   int ph = S.phase;
   if (ph == NMX_PH_WAIT) {
     const int slot_w = S.it - 1 - cfg.iter_begin;
@@ -334,7 +341,7 @@ __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Aren
     if (fin >= cfg.num_chains) ph = NMX_PH_START;
   }
   begin_act(cfg, S, ph, A);
-  A.pe_eval = A.leaf ? AF(NMX_F_PE_EVAL)[c] : 0.0f;
+  A.pe_eval = A.leaf ? pe_ev : 0.0f;
   return ph;
 }
 
@@ -623,12 +630,14 @@ struct VecCtx {
 };
 
 // The frontier (the moving end's position z_eval, its gradient g_eval and its momentum, RR or RL
-// by the tree direction) of the persistent wide kernel's chain, LDS-resident when the kernel
-// carries it (k_wide_persistent<..., CARRY>): [D] floats each, row d at byte d * 4.
+// by the tree direction) and the inverse mass of the persistent wide kernel's chain, LDS-resident
+// when the kernel carries them (k_wide_persistent<..., CARRY>): [D] floats each, row d at byte
+// d * 4.  The arena's inverse mass stays authoritative (the window finalize writes both).
 struct Front {
   float* z;
   float* g;
   float* r;
+  float* im;
 };
 
 // L1 + L2 minus the proposal copy: finish the pending leapfrog (hmc_util.py:306-308),
@@ -807,7 +816,7 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32
     x.w2 = nmx_at(AV(NMX_F_WF_M2), off);
   }
   if (A.start_iter) x.ms = v.unit ? 1.0f : nmx_at(AV(NMX_F_MASS_SQRT), off);
-  if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
+  if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : (CARRY ? fr.im[d] : nmx_at(AV(NMX_F_INV_MASS), off));
   if (A.prep_leaf) {
     const int nd = A.new_dir;
     if (CARRY && !turn_around(A)) x.rfn = fr.r[d];  // the frontier keeps growing
@@ -872,6 +881,7 @@ __device__ __forceinline__ float apply_store(const VecCtx& v, const Act& A, floa
       im = cov;
       x.ms = 1.0f / sqrtf(cov);
       nmx_at(AV(NMX_F_INV_MASS), off) = cov;
+      if constexpr (CARRY) fr.im[d] = cov;
       nmx_at(AV(NMX_F_MASS_SQRT), off) = x.ms;
       nmx_at(AV(NMX_F_WF_MEAN), off) = 0.0f;
       nmx_at(AV(NMX_F_WF_M2), off) = 0.0f;
@@ -1025,8 +1035,8 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
 
   ChainScalars S;
   Act A;
-  const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
   begin_step(cfg, a, c, valid, S, A);
+  const int ph_in = S.phase;  // the stored phase (begin_step's return resolves WAIT)
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   const float seff = valid ? S.step_eff : 0.0f;
 
@@ -1260,8 +1270,8 @@ __global__ __launch_bounds__(64) void k_wide_s(WideArgs W) {
 
   ChainScalars S;
   Act A;
-  const int ph_in = valid ? AI(NMX_F_PHASE)[c] : NMX_PH_DONE;
   begin_step(cfg, a, c, valid, S, A);
+  const int ph_in = S.phase;  // the stored phase (begin_step's return resolves WAIT)
   const bool ke0_pending = valid && (AI(NMX_F_ACTION)[c] & ACT_KE0_PENDING);
   const float* T = a.tot + c;
   if (ke0_pending) {
@@ -1667,7 +1677,7 @@ __device__ __forceinline__ void prow_load(const VecCtx& v, const Act& A, uint32_
                                           int d = 0) {
   const Arena& a = *v.a;
   x.rf = front_r<CARRY>(v, A, fr, off, d);
-  x.im = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), off);
+  x.im = v.unit ? 1.0f : (CARRY ? fr.im[d] : nmx_at(AV(NMX_F_INV_MASS), off));
   if constexpr (NUTS) {
     x.rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
     if (A.tree_chk) {
@@ -1801,7 +1811,7 @@ __device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& 
           if constexpr (CARRY) r[q] = fr.r[d];
           else r[q] = nmx_at(RF, off);
           rs[q] = nmx_at(RS, off);
-          im[q] = v.unit ? 1.0f : nmx_at(IM, off);
+          im[q] = v.unit ? 1.0f : (CARRY ? fr.im[d] : nmx_at(IM, off));
           rl[q] = nmx_at(CK, off);
           rls[q] = nmx_at(CKS, off);
         }
@@ -1953,27 +1963,49 @@ __device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float s
 #ifndef NMX_PX_OCC
 #define NMX_PX_OCC 4  // waves per SIMD the kernel is compiled for: <= 128 VGPRs (3 waves: SV 8192 20.0M vs 24.2M)
 #endif
-// CARRY: the chain's frontier (Front) lives in LDS for the whole launch (12 D bytes of dynamic LDS,
-// within the occupancy the kernel is compiled for: persist_carry): per leaf and row the arena
-// then sees the subtree r_sum, the U-turn checkpoints, the inverse mass and the proposal copies,
+// k_wide_persistent's static LDS, one struct (no padding between arrays; persist_carry sizes the
+// carry form's dynamic LDS by it).  lds: the leaf's wave sums.  The chain's scalar state lives in
+// LDS: wave 0 runs the scalar logic on it and publishes the decisions the vector phases need
+// (the act word of k_wide_v2 plus two values; the iteration and step size are the state's), so
+// no per-chain scalar is held in vector registers through the row loops.  sep: the momentum KE
+// wave sums, the scalar-site rows' terms, the block totals (entries, then U) and the prefetched
+// scalar-site row inputs; the carry form, where every byte of the workgroup's LDS share counts,
+// keeps the first three in lds itself (wave 0 writes them after its lanes read every wave sum;
+// the KE sums after the scalar logic, with a barrier before the next leaf's wave sums) and the
+// prefetched inputs in wave 0's registers.
+template <int NT, class M, bool CARRY>
+struct PersistShared {
+  static constexpr int NW = NT / 64, NR = NPART + M::NSUM;
+  static constexpr int NL = (CARRY && NR + 1 + NPART + NW > NR * NW) ? NR + 1 + NPART + NW : NR * NW;
+  float lds[NL];
+  ChainScalars S;
+  int act, slot, wfn;
+  float sep[CARRY ? 1 : NW + NPART + NR + 1 + M::NSCALAR * SPRE];
+};
+
+// CARRY: the chain's frontier and inverse mass (Front) live in LDS for the whole launch (16 D
+// bytes of dynamic LDS, within the occupancy the kernel is compiled for: persist_carry): per leaf
+// and row the arena then sees the subtree r_sum, the U-turn checkpoints and the proposal copies,
 // not the frontier's position, gradient and momentum (loaded at entry, written back at exit and
-// at turn-arounds), and the stencil reads its neighbours from LDS.  Same arithmetic, bitwise equal.
+// at turn-arounds) nor the inverse mass, and the stencil reads its neighbours from LDS: a
+// leaf's apply rows usually read nothing from HBM.  Same arithmetic, bitwise equal.
 template <int NT, int B, class M, bool CARRY>
 __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk, M m, int max_steps) {
   constexpr int NW = NT / 64;
   constexpr int NR = NPART + M::NSUM;
-  __shared__ float lds[NR * NW];
-  __shared__ float lds_ke[NW];
-  __shared__ float lds_sc[NPART];
-  __shared__ float lds_tot[NR + 1];  // block totals of the leaf's entries, then U
-  __shared__ float lds_pre[M::NSCALAR * SPRE];  // prefetched scalar-site row inputs
+  // lds: the leaf's wave sums.  CARRY (every byte of the workgroup's LDS share counts: four
+  // [D] vectors beside these arrays) keeps the block totals (lds_tot, NR + 1: the entries, then
+  // U) and the scalar-site rows' terms (lds_sc) in lds itself -- wave 0 writes them after its
+  // lanes read every wave sum -- and the scalar-site rows' prefetched inputs in wave 0's
+  // registers instead of lds_pre
+  __shared__ PersistShared<NT, M, CARRY> sh;
+  float* const lds = sh.lds;
+  ChainScalars& Ssh = sh.S;
+  float* const lds_sc = CARRY ? lds + NR + 1 : sh.sep + NW;
+  float* const lds_tot = CARRY ? lds : sh.sep + NW + NPART;  // block totals of the leaf's entries, then U
+  float* const lds_ke = CARRY ? lds + NR + 1 + NPART : sh.sep;  // (a transition's start: barrier below)
+  float* const lds_pre = CARRY ? nullptr : sh.sep + NW + NPART + NR + 1;  // prefetched scalar-site row inputs
   static_assert(M::NSCALAR * SPRE <= 64, "one lane per prefetched value");
-  // the chain's scalar state lives in LDS: wave 0 runs the scalar logic on it and publishes
-  // the decisions the vector phases need (the act word of k_wide_v2 plus four values), so no
-  // per-chain scalar is held in vector registers through the row loops
-  __shared__ ChainScalars Ssh;
-  __shared__ int sh_act, sh_slot, sh_wfn, sh_it;
-  __shared__ float sh_seff;
   const StepArgs& P = Pk;
   const nmx_nuts_config& cfg = P.cfg;
   const Arena& a = P.a;
@@ -1992,18 +2024,21 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
   }
   const uint32_t base = ((uint32_t)c * (uint32_t)D) << 2;  // byte offset of the chain's row 0
   extern __shared__ float front_lds[];
-  const Front fr{front_lds, front_lds + D, front_lds + 2 * D};
+  const Front fr{front_lds, front_lds + D, front_lds + 2 * D, front_lds + 3 * D};
   if constexpr (CARRY) {
     // the frontier of the pending leaf (START: overwritten by the momentum draw before any use)
     const int dir0 = uni_i(AI(NMX_F_DIR)[c]);
     const float* ZE = AV(NMX_F_Z_EVAL);
     const float* GE = AV(NMX_F_G_EVAL);
     const float* RF = dir0 ? AV(NMX_F_RR) : AV(NMX_F_RL);
+    const float* IM = AV(NMX_F_INV_MASS);
+    const bool unit = cfg.unit_mass != 0;
     for (int d = tid; d < D; d += NT) {
       const uint32_t off = base + ((uint32_t)d << 2);
       fr.z[d] = nmx_at(ZE, off);
       fr.g[d] = nmx_at(GE, off);
       fr.r[d] = nmx_at(RF, off);
+      fr.im[d] = unit ? 1.0f : nmx_at(IM, off);
     }
   }
   __syncthreads();
@@ -2034,14 +2069,16 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     if (!A.leaf) __syncthreads();
     if (A.leaf) {
       const float seff = uni_f(Ssh.step_eff);
-      // the last wave prefetches the scalar-site rows' inputs (stored to LDS after its rows)
+      // the scalar-site rows' inputs are prefetched: by the last wave into lds_pre after its rows,
+      // or (CARRY) by wave 0 into the register pv, read by its lane 0 in the potential's finish
       float pv = 0.0f;
       bool pl = false;
-      if (wv == NW - 1 && lane < M::NSCALAR * SPRE) {
+      if (wv == (CARRY ? 0 : NW - 1) && lane < M::NSCALAR * SPRE) {
         const int i = lane / SPRE, f = lane % SPRE;
         const float* src = spre_src(v, A, is_nuts, f);
         if (src) {
-          pv = (CARRY && f == 0) ? fr.r[m.scalar_row(i)] : nmx_at(src, base + ((uint32_t)m.scalar_row(i) << 2));
+          const int d = m.scalar_row(i);
+          pv = (CARRY && f == 0) ? fr.r[d] : (CARRY && f == 1) ? fr.im[d] : nmx_at(src, base + ((uint32_t)d << 2));
           pl = true;
         }
       }
@@ -2055,7 +2092,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
       if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT, CARRY>(v, A, m, base, lds, fr);
-      if (pl) lds_pre[lane] = pv;
+      if (!CARRY && pl) lds_pre[lane] = pv;
       PX_T(1);
       PX_ADD(0, 0, 1);
       __syncthreads();
@@ -2084,10 +2121,20 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
           for (int i = 0; i < M::NSCALAR; ++i) {
             const int d = m.scalar_row(i);
             const uint32_t off = base + ((uint32_t)d << 2);
-            if constexpr (CARRY) fr.g[d] = gs[i];
-            else nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
-            if (is_nuts) spre_leaf<true, CARRY>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs, fr, d);
-            else spre_leaf<false, CARRY>(v, A, seff, off, gs[i], lds_pre + i * SPRE, rs, fr, d);
+            float prer[CARRY ? SPRE : 1];
+            const float* pre;
+            if constexpr (CARRY) {
+#pragma unroll
+              for (int f = 0; f < SPRE; ++f)
+                prer[f] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), i * SPRE + f));
+              pre = prer;
+              fr.g[d] = gs[i];
+            } else {
+              pre = lds_pre + i * SPRE;
+              nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
+            }
+            if (is_nuts) spre_leaf<true, CARRY>(v, A, seff, off, gs[i], pre, rs, fr, d);
+            else spre_leaf<false, CARRY>(v, A, seff, off, gs[i], pre, rs, fr, d);
           }
 #pragma unroll
           for (int e = 0; e < NPART; ++e)
@@ -2116,11 +2163,9 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
           [&](int side) { return lds_tot[1 + 2 * MAXD + side]; }, seed, gch, P.fields, c, lane == 0);
       if (lane == 0) {
         Ssh = S;
-        sh_act = pack_act(A);
-        sh_slot = A.slot;
-        sh_wfn = A.wfn;
-        sh_it = S.it;
-        sh_seff = S.step_eff;
+        sh.act = pack_act(A);
+        sh.slot = A.slot;
+        sh.wfn = A.wfn;
         if (A.fin_done) atomicAdd(&a.counters[0], 1);
       }
     }
@@ -2128,7 +2173,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     PX_ADD(3, 3, 4);
     __syncthreads();  // decisions published
     PX_T(5);
-    const int act = uni_i(sh_act);
+    const int act = uni_i(sh.act);
     {
       Act D2{};
       D2.take_leaf = act & ACT_TAKE_LEAF;
@@ -2142,15 +2187,15 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
       D2.prep_leaf = act & ACT_PREP;
       D2.dirR = (act & ACT_DIRR) ? 1 : 0;
       D2.new_dir = (act & ACT_NEWDIR) ? 1 : 0;
-      D2.slot = uni_i(sh_slot);
-      D2.wfn = uni_i(sh_wfn);
+      D2.slot = uni_i(sh.slot);
+      D2.wfn = uni_i(sh.wfn);
       constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE |
                           ACT_START | ACT_PREP;
       float ke0 = 0.0f;
       if (act & VEC) {
         float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc
                                                                          : nullptr;
-        ke0 = persist_apply_rows<NT, B, CARRY>(v, D2, m, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp,
+        ke0 = persist_apply_rows<NT, B, CARRY>(v, D2, m, uni_f(Ssh.step_eff), base, c, seed, gch, uni_i(Ssh.it), samp,
                                                P.transform, cfg, fr);
       }
       if (D2.start_iter) {
@@ -2175,6 +2220,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         Ssh.E0 = Ssh.pe + 0.5f * t;  // build_tree :1130
         Ssh.energy = Ssh.E0;         // proposal energy of the initial tree (:1137)
       }
+      if (CARRY && D2.start_iter) __syncthreads();  // lds_ke read before the next leaf's wave sums
     }
   }
   if constexpr (CARRY) {
@@ -2903,27 +2949,27 @@ int persist_nt(int dim) {
   return dim <= 4096 ? 256 : 512;
 }
 
-// Whether the persistent kernel keeps the chain's frontier in LDS (k_wide_persistent CARRY): its
-// 12 D bytes beside the static LDS must fit the share of a CU's 160 KB that the compiled
-// occupancy (NMX_PX_OCC waves per SIMD, NT / 64 waves per workgroup) leaves each workgroup, so
-// the carry never costs resident chains (SV D = 2519 at NT = 256: 30 KB of 40; funnel-10k at
-// NT = 512: 120 KB of 80, not carried).  No effect on results (bitwise equal either way); the
-// debug / experiment builds can turn it off (NMX_PERSIST_CARRY=0) for A/B runs.
-bool persist_carry(int dim, int nt) {
+// Whether the persistent kernel keeps the chain's frontier and inverse mass in LDS
+// (k_wide_persistent CARRY): its 16 D bytes beside the static LDS must fit the share of a CU's
+// 160 KB that the compiled occupancy (NMX_PX_OCC waves per SIMD, NT / 64 waves per workgroup)
+// leaves each workgroup, so the carry never costs resident chains (SV D = 2519 at NT = 256:
+// 40.9 KB of 40 KB; funnel-10k at NT = 512: 160 KB of 80, not carried).  No effect on results
+// (bitwise equal either way); the debug / experiment builds can turn it off
+// (NMX_PERSIST_CARRY=0) for A/B runs.
+bool persist_carry(int dim, int nt, size_t static_lds) {
 #if defined(NMX_DEBUG) || defined(NMX_EXPERIMENT)
   if (const char* e = getenv("NMX_PERSIST_CARRY"))
     if (atoi(e) == 0) return false;
 #endif
   const size_t share = (size_t)160 * 1024 * nt / (64 * 4 * NMX_PX_OCC);
-  constexpr size_t STATIC_LDS = 4096;  // k_wide_persistent's own arrays (< 2 KB), with margin
-  return (size_t)12 * dim + STATIC_LDS <= share;
+  return (size_t)16 * dim + static_lds <= share;
 }
 
 template <int NT, class M>
 void launch_persistent_nt(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
   const dim3 grid(args.cfg.num_chains);
-  if (persist_carry(args.cfg.dim, NT)) {
-    const size_t lds = (size_t)12 * args.cfg.dim;
+  if (persist_carry(args.cfg.dim, NT, (sizeof(PersistShared<NT, M, true>) + 15) / 16 * 16)) {
+    const size_t lds = (size_t)16 * args.cfg.dim;
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)k_wide_persistent<NT, NMX_PX_B, M, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2944,6 +2990,27 @@ int launch_persistent(const StepArgs& args, const M& m, int max_steps, hipStream
   return nmx_check_launch("k_wide_persistent");
 }
 }  // namespace
+
+#if defined(NMX_DEBUG) || defined(NMX_EXPERIMENT)
+// kernel experiments: resident workgroups per CU of the persistent SV kernel at dim (and whether
+// it carries the frontier in LDS), from the HIP occupancy calculator
+extern "C" int nmx_debug_persist_occupancy(int dim, int* blocks_per_cu, int* carry) {
+  const NmxWideSV m{nullptr, dim - 2};
+  (void)m;
+  const int nt = persist_nt(dim);
+  if (nt != 256) return nmx_fail(NMX_ERR_UNSUPPORTED, "occupancy probe: NT = 256 dims only");
+  const bool cr = persist_carry(dim, 256, (sizeof(PersistShared<256, NmxWideSV, true>) + 15) / 16 * 16);
+  *carry = cr;
+  hipError_t e;
+  if (cr)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_B, NmxWideSV, true>,
+                                                     256, (size_t)16 * dim);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_B, NmxWideSV, false>,
+                                                     256, 0);
+  return e == hipSuccess ? NMX_OK : nmx_fail(NMX_ERR_HIP, "occupancy: %s", hipGetErrorString(e));
+}
+#endif
 
 extern "C" int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float* samples, float* fields,
                                  const int8_t* transform, int model, const float* data, int n, int max_steps,
