@@ -424,30 +424,51 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 // d] for j = 4 jh + q: exactly the B piece's bytes, so the products are bitwise the same.
 // The reads are inline asm (a compiler-visible LDS read after the ring's DMA issue gets a
 // vmcnt(0) wait that would drain the prefetch, as for x3_labels); x3_tr_wait before use.
-template <int KB, int DT>
+//
+// COMPACT (the tail form with H): the slot holds the A part without the last k-block's plane
+// pieces (x3_ai / x3_ci COMPACT positions), whose columns 48..55 the combined pieces carry:
+// piece c0 = (plane 0 | plane 1) in lane halves h = 0 | 1, c1 = (plane 2 | plane 0).  The last
+// k-block's reads (lane bit g1 of dt = DT - 1) take plane 0 and 2 from the h = 0 halves of c0 /
+// c1 and plane 1 from the h = 1 half of c0 (32 lanes = 512 bytes further).  Those reads'
+// columns 56..63 (zero in the plane pieces) then read the neighbouring half instead: they only
+// feed GEMM2 output rows >= 56 > D, which are never stored.  Columns < D read the same bytes.
+template <int KB, int DT, bool COMPACT = false>
 __device__ __forceinline__ void x3_gemm2_tr_load(const char* aslot, bf16x8 (&fb)[3][DT][2]) {
   static_assert(KB >= 2 * DT, "the GEMM1 image must cover GEMM2's 32 DT columns");
+  static_assert(!COMPACT || KB == 2 * DT, "compact slot: the last k-block is GEMM2's last column half");
   const int L = threadIdx.x & 63;
   const int p = L & 3, q = (L >> 2) & 3, g1 = (L >> 4) & 1, h = L >> 5;
-  const unsigned base = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)aslot) + g1 * 1024 +
-                        (q + 32 * (p >> 1) + 4 * h) * 16 + 8 * (p & 1);
+  const unsigned base0 = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)aslot) +
+                         (q + 32 * (p >> 1) + 4 * h) * 16 + 8 * (p & 1);
 #pragma unroll
   for (int plane = 0; plane < 3; ++plane)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < DT; ++dt) {
+      // byte offsets of the k-blocks 2 dt (g1 = 0) and 2 dt + 1 (g1 = 1) in the slot
+      const int kb0 = 2 * dt, kb1 = 2 * dt + 1;
+      int o0, o1;
+      if constexpr (COMPACT) {
+        o0 = x3_ai<KB, true>(plane, kb0) * 1024;
+        o1 = kb1 < KB - 1 ? x3_ai<KB, true>(plane, kb1) * 1024
+                          : (plane == 2 ? x3_ci<KB, true>(1) * 1024 : x3_ci<KB, true>(0) * 1024 + (plane == 1 ? 512 : 0));
+      } else {
+        o0 = (plane * KB + kb0) * 1024;
+        o1 = (plane * KB + kb1) * 1024;
+      }
+      const unsigned base = base0 + (g1 ? o1 : o0);
 #pragma unroll
       for (int sidx = 0; sidx < 2; ++sidx) {
         typedef short s4 __attribute__((ext_vector_type(4)));
         s4 lo, hi;
         asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
                      : "=&v"(lo), "=&v"(hi)
-                     : "v"(base), "i"((plane * KB + 2 * dt) * 1024 + (16 * sidx) * 16),
-                       "i"((plane * KB + 2 * dt) * 1024 + (16 * sidx + 8) * 16));
+                     : "v"(base), "i"((16 * sidx) * 16), "i"((16 * sidx + 8) * 16));
         const s4 lh[2] = {lo, hi};
         bf16x8 f;
         __builtin_memcpy(&f, lh, 16);
         fb[plane][dt][sidx] = f;
       }
+    }
 }
 template <int DT>
 __device__ __forceinline__ void x3_tr_wait(bf16x8 (&fb)[3][DT][2]) {
@@ -834,9 +855,17 @@ constexpr int X3_ROLE_PA = NMX_X3_ROLE_PA;
 template <int PA>
 constexpr int x3_roles_aslots() { return PA + 2; }
 
+// A-part pieces a tail-form slot holds: with H the compact image (the last k-block's plane
+// pieces left out: x3_gemm2_tr_load<..., true> takes those columns from the combined pieces), so
+// the tail launches stream 11 + 1 KB per 32-row tile for covtype -- 218 MB of X per launch, which
+// the 256 MB Infinity Cache keeps across a run's back-to-back tail launches (14 + 1 KB, 272 MB,
+// did not fit)
+template <int KB, int H>
+constexpr int x3_roles_na() { return H ? 3 * (KB - 1) + 2 : 3 * KB; }
+
 template <int KB, int DT, int H, int PA>
 inline size_t x3_roles_lds_bytes() {
-  constexpr int NA = 3 * KB + 2 * H;
+  constexpr int NA = x3_roles_na<KB, H>();
   // A ring, the label ring (one 1-KB piece per tile, PA + 1 slots), the residual ring
   return (size_t)(x3_roles_aslots<PA>() * NA + (PA + 1)) * 1024 + (size_t)2 * 4 * 4096;
 }
@@ -846,9 +875,10 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
                                                                          int64_t ntiles, int D, int S, int Gt,
                                                                          nmx_eval_batch ev, float* __restrict__ gpart,
                                                                          double* __restrict__ pepart) {
-  // the A ring holds the whole A part (the tile's GEMM1 image incl. the combined pieces): the B
-  // waves read GEMM2's X^T operand from its plane pieces
-  constexpr int NP = 3 * KB + 2 * H + 6 * DT + 1, NA = 3 * KB + 2 * H;
+  // the A ring holds the tile's GEMM1 image (with H the compact one: x3_roles_na), from which the
+  // B waves also read GEMM2's X^T operand
+  constexpr int NP = 3 * KB + 2 * H + 6 * DT + 1, NA = x3_roles_na<KB, H>();
+  constexpr bool CMP = H != 0;
   static_assert(KB == 4, "role-split tail form: D in (48, 64]");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x;
@@ -878,9 +908,9 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
   const int nt = (int)(t1 - t0);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
-  // The tail launch is bound by streaming X (~7 TB/s): it reads each tile's GEMM1 image and its
-  // labels only, and the B waves take GEMM2's X^T operand from the GEMM1 image by transposed LDS
-  // reads (x3_gemm2_tr_load), so the B pieces (half the packed bytes) stay in HBM.
+  // The tail launch streams each tile's GEMM1 image (compact with H) and its labels only, and the
+  // B waves take GEMM2's X^T operand from that image by transposed LDS reads (x3_gemm2_tr_load),
+  // so the B pieces (half the packed bytes) stay in HBM.
   constexpr int PB = PA + 1, PAS = x3_roles_aslots<PA>();
   char* aring = lds;
   char* bring = lds + PAS * NA * 1024;  // labels: [slot][1 KB]
@@ -889,9 +919,11 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
     char* dst = aring + (k % PAS) * NA * 1024;
 #pragma unroll
     for (int j = 0; j < (NA + X3_ROLE_WAVES - 1) / X3_ROLE_WAVES; ++j) {
-      const int i = w + X3_ROLE_WAVES * j;
-      if (i < NA)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+      const int il = w + X3_ROLE_WAVES * j;  // slot position; i = the tile's piece
+      const int i = !CMP ? il
+                         : (il < 3 * (KB - 1) ? (il / (KB - 1)) * KB + il % (KB - 1) : 3 * KB + (il - 3 * (KB - 1)));
+      if (il < NA)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(dst + il * 1024), 16,
                                                  lane * 16, (unsigned)((k * NP + i) * 1024), 0, 0);
     }
   };
@@ -928,7 +960,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         if (p < nt) issue_b(p);
       }
       f32x16 accA, accB;
-      if (active) accA = x3_gemm1<KB, H>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
+      if (active) accA = x3_gemm1<KB, H, CMP>(reinterpret_cast<const bf16x8*>(aring) + lane, z1, z2, z3);
       auto stepA = [&](int k, const f32x16& acc, f32x16& nxt) {
         x3_roles_barrier_rt(in_flight(k));  // A(k+1), B(k) landed; R slot k&1 was read by B in iteration k-1
         if (k + PA < nt) issue_a(k + PA);
@@ -946,17 +978,18 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
         float lin = 0.0f;
         float prod[2] = {1.0f, 1.0f};
-        bf16x8 a1 = fa[0 * 64], a2 = fa[KB * 64], a3 = fa[2 * KB * 64];
+        bf16x8 a1 = fa[x3_ai<KB, CMP>(0, 0) * 64], a2 = fa[x3_ai<KB, CMP>(1, 0) * 64],
+               a3 = fa[x3_ai<KB, CMP>(2, 0) * 64];
 #pragma unroll
         for (int kb = 0; kb < KB - H; ++kb) {
           bf16x8 n1, n2, n3;
           if (kb + 1 < KB - H) {
-            n1 = fa[(kb + 1) * 64];
-            n2 = fa[(KB + kb + 1) * 64];
-            n3 = fa[(2 * KB + kb + 1) * 64];
+            n1 = fa[x3_ai<KB, CMP>(0, kb + 1) * 64];
+            n2 = fa[x3_ai<KB, CMP>(1, kb + 1) * 64];
+            n3 = fa[x3_ai<KB, CMP>(2, kb + 1) * 64];
           } else if (H && kb + 1 == KB - 1) {  // the combined pieces (a1 | a2), (a3 | a1)
-            n1 = fa[(3 * KB) * 64];
-            n2 = fa[(3 * KB + 1) * 64];
+            n1 = fa[x3_ci<KB, CMP>(0) * 64];
+            n2 = fa[x3_ci<KB, CMP>(1) * 64];
           }
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
           x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
@@ -1013,7 +1046,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
       for (int r = 0; r < 16; ++r) g[dt][r] = 0.0f;
     auto gemm2 = [&](int k) {  // GEMM2 of tile k
       bf16x8 fb[3][DT][2];
-      x3_gemm2_tr_load<KB, DT>(aring + (k % PAS) * NA * 1024, fb);
+      x3_gemm2_tr_load<KB, DT, CMP>(aring + (k % PAS) * NA * 1024, fb);
       float res[16];
       x3_res_load(rmine + (k & 1) * 4 * 4096, res);  // (waits for every LDS read, the above too)
       x3_tr_wait<DT>(fb);
