@@ -130,7 +130,13 @@ def _located_parity(hist, dev_trace, dev_ns, dev_z, atol, rtol=0.0, to_model=Non
         print(f"[{label}] " + PR.describe(m), file=sys.stderr)
     par["mismatches"] = [{k: (float(v) if isinstance(v, (np.floating, float)) else v) for k, v in m.items()}
                          for m in par["mismatches"]]
-    par["unexplained"] = len(par["mismatches"]) - par["explained"]
+    # one classification for the device record and its rounding calibration (oracle/parity.py
+    # counts): per kind of parting ("take_leaf", "turning", ... located at their leaf; "draw" = every
+    # decision equal, the positions drifted), and unexplained = a located parting outside its
+    # leaf's bound, or a decision the trace cannot place
+    c = PR.counts(par)
+    par["kinds"] = {k: v for k, v in c.items() if k not in ("chains", "matched", "unexplained")}
+    par["unexplained"] = c["unexplained"]
     return par
 
 
@@ -427,9 +433,25 @@ def _ext_stream(s):
     return _STREAMS[s]
 
 
+def _heartbeat(t_start, period=30.0):
+    """A line on stderr every `period` seconds (rank 0): the long untimed phases (adaptation of the
+    configs, the CPU baselines) print nothing else for minutes, and runners that watch output take
+    a silent process for a hung one.  Daemon thread, stderr only: the JSON line stays alone on stdout."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"[bench] running, {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     t_start = time.perf_counter()
     args = parse()
+    if int(os.environ.get("RANK", "0")) == 0:
+        _heartbeat(t_start)
     if args.lib:
         from numpyro_amd import native as _native
 
