@@ -834,6 +834,47 @@ __device__ __forceinline__ void x3_roles_barrier_rt(int n) {  // n wave-uniform
   }
 }
 
+// NMX_ROLES_EXP (timing experiments only, wrong results): bit 1 = the B waves skip the residual's
+// three-term split (its raw bits as the three bf16 operands), bit 2 = the A waves skip the
+// epilogue (the accumulator as the residual)
+#ifndef NMX_ROLES_EXP
+#define NMX_ROLES_EXP 0
+#endif
+#if NMX_ROLES_EXP
+template <int DT>
+__device__ __forceinline__ void x3_gemm2_regs_nosplit(const bf16x8 (&fb)[3][DT][2], const float (&res)[16],
+                                                      f32x16 (&g)[DT]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    u32x4 w;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) w[p] = __float_as_uint(res[8 * s + 2 * p]) ^ (__float_as_uint(res[8 * s + 2 * p + 1]) >> 16);
+    const bf16x8 r1 = __builtin_bit_cast(bf16x8, w), r2 = r1, r3 = r1;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16x8 b1 = fb[0][dt][s], b2 = fb[1][dt][s], b3 = fb[2][dt][s];
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
+      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
+    }
+  }
+}
+#define X3_ROLES_EPI(acc, y4, p, res, lin, prod) \
+  do {                                           \
+    if (NMX_ROLES_EXP & 2) {                     \
+      res[2 * (p)] = acc[2 * (p)];               \
+      res[2 * (p) + 1] = acc[2 * (p) + 1];       \
+    } else {                                     \
+      x3_epi_pair(acc, y4, p, res, lin, prod);   \
+    }                                            \
+  } while (0)
+#else
+#define X3_ROLES_EPI(acc, y4, p, res, lin, prod) x3_epi_pair(acc, y4, p, res, lin, prod)
+#endif
+
 constexpr int X3_ROLE_WAVES = 8;
 // Prefetch depth: tile k + PA is issued in iteration k, and the barrier of iteration k waits
 // only for the DMAs of the tile pair it needs (A(k+1), labels(k)), leaving the later PA - 2
@@ -992,12 +1033,12 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
             n2 = fa[x3_ci<KB, CMP>(1) * 64];
           }
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+          X3_ROLES_EPI(acc, y4, 2 * kb, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+          X3_ROLES_EPI(acc, y4, 2 * kb + 1, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
@@ -1017,10 +1058,10 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         if constexpr (H) {  // x3_gemm1's combined products (a1 = (a1 | a2), a2 = (a3 | a1) here)
           constexpr int kb = KB - 1;
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z3[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+          X3_ROLES_EPI(acc, y4, 2 * kb, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+          X3_ROLES_EPI(acc, y4, 2 * kb + 1, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
@@ -1050,7 +1091,11 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
       float res[16];
       x3_res_load(rmine + (k & 1) * 4 * 4096, res);  // (waits for every LDS read, the above too)
       x3_tr_wait<DT>(fb);
+#if NMX_ROLES_EXP & 1
+      x3_gemm2_regs_nosplit<DT>(fb, res, g);
+#else
       x3_gemm2_regs<DT>(fb, res, g);
+#endif
     };
     if (nt > 0) {
       issue_a(0);
