@@ -66,12 +66,18 @@ struct NmxWideSV {
     float s, sp, sn, r;
   };
   __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t ldc4, int d, RowIn& x) const {
+    row_load_z(z, off, ldc4, d, x);
+    row_load_data(d, x);
+  }
+  // the two halves of row_load: the positions (the LDS frontier in the persistent kernel) and the
+  // data (HBM / L2), so a caller can batch the memory loads of several rows ahead of the rest
+  __device__ __forceinline__ void row_load_z(const float* z, uint32_t off, uint32_t ldc4, int d, RowIn& x) const {
     const int t = d - 1;
     x.s = nmx_at(z, off);
     x.sp = t > 0 ? nmx_at(z, off - ldc4) : 0.0f;
     x.sn = t + 1 < T ? nmx_at(z, off + ldc4) : 0.0f;
-    x.r = ret[t];
   }
+  __device__ __forceinline__ void row_load_data(int d, RowIn& x) const { x.r = ret[d - 1]; }
   __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
                                        float* sums) const {
     RowIn x;
@@ -145,6 +151,10 @@ struct NmxWideFunnel {
   __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
     in.x = nmx_at(z, off);
   }
+  __device__ __forceinline__ void row_load_z(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
+    in.x = nmx_at(z, off);
+  }
+  __device__ __forceinline__ void row_load_data(int, RowIn&) const {}
   __device__ __forceinline__ float row_eval(const RowIn& in, int, const Glob& g, float* sums) const {
     sums[0] += in.x * in.x;
     return in.x * g.e;
@@ -191,6 +201,10 @@ struct NmxWideFunnelNC {
   __device__ __forceinline__ void row_load(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
     in.x = nmx_at(z, off);
   }
+  __device__ __forceinline__ void row_load_z(const float* z, uint32_t off, uint32_t, int, RowIn& in) const {
+    in.x = nmx_at(z, off);
+  }
+  __device__ __forceinline__ void row_load_data(int, RowIn&) const {}
   __device__ __forceinline__ float row_eval(const RowIn& in, int, const Glob&, float* sums) const {
     sums[0] += in.x * in.x;
     return in.x;

@@ -1730,6 +1730,85 @@ __device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float 
   }
 }
 
+// The carry form's leaf rows: the frontier momentum, inverse mass and positions are LDS reads,
+// so a row's HBM loads (subtree r_sum, the first checkpoint level, the tree's r_sum and other
+// end at subtree completion, the model's data) are all that must be in flight across a batch:
+// BC rows' worth of them go out first, then each row reads its LDS inputs and runs.  Five floats
+// per row in flight instead of the arena form's eleven: larger batches fit the registers, fewer
+// dependent memory rounds per leaf.  Same arithmetic as persist_leaf_rows.
+#ifndef NMX_PX_BC
+#define NMX_PX_BC 3
+#endif
+struct PRowG {
+  float rs_old, rst, ro, ckr, ckrs;
+};
+template <bool NUTS, int NT, int BC, class M>
+__device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const Act& A, const M& m,
+                                                        const typename M::Glob& gl, float seff, uint32_t base,
+                                                        float* red, const Front& fr) {
+  const Arena& a = *v.a;
+  const int hi = m.hi();
+  float dl = 0.0f, dr = 0.0f;
+  float acc[3 + M::NSUM];
+#pragma unroll
+  for (int i = 0; i < 3 + M::NSUM; ++i) acc[i] = 0.0f;
+  for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += BC * NT) {
+    PRowG xg[BC];
+    typename M::RowIn mi[BC];
+#pragma unroll
+    for (int q = 0; q < BC; ++q) {
+      const int d = d0 + q * NT;
+      if (d < hi) {
+        const uint32_t off = base + ((uint32_t)d << 2);
+        if constexpr (NUTS) {
+          xg[q].rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
+          if (A.tree_chk) {
+            xg[q].rst = nmx_at(AV(NMX_F_RSUM), off);
+            xg[q].ro = nmx_at((A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR)), off);
+          }
+          if (A.imin <= A.imax) {
+            xg[q].ckr = nmx_at(a.ckr + A.imin * v.ck_stride, off);
+            xg[q].ckrs = nmx_at(a.ckrs + A.imin * v.ck_stride, off);
+          }
+        }
+        m.row_load_data(d, mi[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BC; ++q) {
+      const int d = d0 + q * NT;
+      if (d < hi) {
+        const uint32_t off = base + ((uint32_t)d << 2);
+        PRow x;
+        x.rf = fr.r[d];
+        x.im = v.unit ? 1.0f : fr.im[d];
+        x.rs_old = xg[q].rs_old;
+        x.rst = xg[q].rst;
+        x.ro = xg[q].ro;
+        x.ckr = xg[q].ckr;
+        x.ckrs = xg[q].ckrs;
+        m.row_load_z(fr.z, (uint32_t)d << 2, 4u, d, mi[q]);  // stencil neighbours too
+        const float g = m.row_eval(mi[q], d, gl, acc + 3);
+        fr.g[d] = g;
+        prow_store<NUTS, true, 1>(v, A, seff, off, x, g, acc, dl, dr, fr, d);
+      }
+    }
+  }
+  red[0] += acc[0];
+  red[1 + 2 * MAXD] += acc[1];
+  red[2 + 2 * MAXD] += acc[2];
+#pragma unroll
+  for (int k = 0; k < M::NSUM; ++k) red[NPART + k] += acc[3 + k];
+  if constexpr (NUTS) {
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i)
+      if (i == A.imin && A.imin <= A.imax) {
+        red[1 + 2 * i] = dl;
+        red[2 + 2 * i] = dr;
+      }
+  }
+}
+
 template <bool NUTS, int NT, int B, bool CARRY, class M>
 __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A, const M& m,
                                                   const typename M::Glob& gl, float seff, uint32_t base, float* red,
@@ -2087,8 +2166,13 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         float red[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) red[i] = 0.0f;
-        if (is_nuts) persist_leaf_rows<true, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
-        else persist_leaf_rows<false, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
+        if constexpr (CARRY) {
+          if (is_nuts) persist_leaf_rows_carry<true, NT, NMX_PX_BC>(v, A, m, gl, seff, base, red, fr);
+          else persist_leaf_rows_carry<false, NT, NMX_PX_BC>(v, A, m, gl, seff, base, red, fr);
+        } else {
+          if (is_nuts) persist_leaf_rows<true, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
+          else persist_leaf_rows<false, NT, NMX_PX_BL, CARRY>(v, A, m, gl, seff, base, red, fr);
+        }
         wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);
       }
       if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT, CARRY>(v, A, m, base, lds, fr);
