@@ -9,6 +9,16 @@
 #pragma once
 #include <math.h>
 
+// NMX_SV_FAST (default): the SV row's q / (1 + q) by the hardware reciprocal and log1p(q) as
+// log(u) q / (u - 1), u = 1 + q, from the hardware log2 -- a few ulp instead of the libm forms'
+// ~1, 62 instead of 177 VALU instructions per row.  The persistent SV kernel is VALU-bound
+// (profiles/r04/sv_persistent_pmc_and_bc.txt): 29.9M -> 35.6M leapfrog/s at 8192 chains, 14.1M ->
+// 18.1M at 1024 (profiles/r04/ab_sv_row_math.txt).  Every schedule includes this header, so they
+// stay bitwise equal to each other; against the float64 oracle the potential keeps its tolerance.
+#ifndef NMX_SV_FAST
+#define NMX_SV_FAST 1
+#endif
+
 #include "nmx_common.h"
 
 // digamma for x > 0: recurrence up to x >= 6, then the asymptotic series.
@@ -91,9 +101,18 @@ struct NmxWideSV {
     const float dn = t + 1 < T ? sn - s : 0.0f;
     const float r = x.r;
     const float q = r * r * expf(-2.0f * s) * g.inv_nu;
+#if NMX_SV_FAST
+    const float u = 1.0f + q;
+    const float qq = q * __builtin_amdgcn_rcpf(u);
+    const float l1q = (u == 1.0f || !(u < INFINITY)) ? q
+                                                     : __builtin_amdgcn_logf(u) * 0.6931471805599453f *
+                                                           (q * __builtin_amdgcn_rcpf(u - 1.0f));
+#else
     const float qq = q / (1.0f + q);
+    const float l1q = log1pf(q);
+#endif
     sums[0] += dd * dd;
-    sums[1] += log1pf(q);
+    sums[1] += l1q;
     sums[2] += qq;
     sums[3] += s;
     // dU/ds_t = -( -(d_t - d_{t+1})/sigma^2 + (nu+1) q/(1+q) - 1 )
