@@ -133,6 +133,24 @@ __global__ __launch_bounds__(256) void k_rows_to_cols(const float* __restrict__ 
   }
 }
 
+// NMX_BNN_PROF (kernel experiments, scripts/bnn_profile.py): thread 0 of every workgroup adds the
+// shader-clock cycles of each phase to g_bnn_prof (read and reset by nmx_debug_bnn_profile)
+#ifdef NMX_BNN_PROF
+__device__ unsigned long long g_bnn_prof[16];
+#define BNN_T0() long long bnn_t = clock64()
+#define BNN_T(i)                                                                        \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      const long long bnn_n = clock64();                                                \
+      atomicAdd(&g_bnn_prof[i], (unsigned long long)(bnn_n - bnn_t));                   \
+      bnn_t = bnn_n;                                                                    \
+    }                                                                                   \
+  } while (0)
+#else
+#define BNN_T0()
+#define BNN_T(i)
+#endif
+
 // zr / gr: the evaluated chains' positions and gradients as rows [position][D].
 __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, const float* __restrict__ Y, BnnDims dm,
                                                nmx_eval_batch ev, const float* __restrict__ zr,
@@ -149,6 +167,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   if (c < 0) return;
   const int ldc = ev.ldc;
   const int t = threadIdx.x;
+  BNN_T0();
 
   float* W1 = sm;                  // Dx*H
   float* W2 = W1 + Dx * H;         // H*H
@@ -187,6 +206,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int i = t; i < N * Dx; i += THREADS) Xs[i] = X[i];
   for (int i = t; i < N; i += THREADS) Ys[i] = Y[i];
   __syncthreads();
+  BNN_T(0);
 
   // h1 = tanh(X W1)
   for (int e = t; e < N * H; e += THREADS) {
@@ -196,6 +216,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     h1[e] = tanhf(a);
   }
   __syncthreads();
+  BNN_T(1);
 
   // h2 = tanh(h1 W2): tiles over (n, j), K = i
   const int wv = t >> 6, l31 = t & 31;
@@ -230,6 +251,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
 #endif
   __syncthreads();
+  BNN_T(2);
 
   // yhat = h2 w3; residual; dU/dyhat = -p (Y - yhat)
   float esq = 0.0f;
@@ -243,6 +265,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     gy[n] = -p * e;
   }
   __syncthreads();
+  BNN_T(3);
 
   // grad w3 = w3 + h2^T gy
   for (int j = t; j < H; j += THREADS) {
@@ -252,6 +275,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     g[dm.o_w3 + j] = w3[j] + s;
   }
   __syncthreads();
+  BNN_T(4);
   // ga2 = (gy w3^T) * (1 - h2^2)   (in place of h2)
   for (int e = t; e < N * H; e += THREADS) {
     const int n = e / H, j = e % H;
@@ -259,6 +283,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     h2[e] = gy[n] * w3[j] * (1.0f - v * v);
   }
   __syncthreads();
+  BNN_T(5);
 
   // grad W2 = W2 + h1^T ga2: tiles over (i, j), K = n
 #if NMX_BNN_TILE == 16
@@ -289,6 +314,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
 #endif
   __syncthreads();
+  BNN_T(6);
 
   // ga1 = (ga2 W2^T) * (1 - h1^2): tiles over (n, i), K = j, in place of h1 (a tile reads h1
   // only at its own elements; grad W2 above finished reading h1 at the barrier)
@@ -328,6 +354,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   }
 #endif
   __syncthreads();
+  BNN_T(7);
 
   // grad W1 = W1 + X^T ga1
   for (int e = t; e < Dx * H; e += THREADS) {
@@ -338,6 +365,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     g[dm.o_w1 + e] = W1[e] + s;
   }
 
+  BNN_T(9);
   const float esq_t = block_sum256(esq, red);
   const float wsq_t = block_sum256(wsq, red);
   if (t == 0) {
@@ -350,6 +378,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     ev.pe[c] = -lp;
     g[0] = -(3.0f - p + 0.5f * Nf - 0.5f * p * esq_t);
   }
+  BNN_T(10);
 }
 
 size_t lds_bytes(int N, int Dx, int H) {
@@ -357,6 +386,16 @@ size_t lds_bytes(int N, int Dx, int H) {
 }
 
 }  // namespace
+
+#ifdef NMX_BNN_PROF
+extern "C" int nmx_debug_bnn_profile(unsigned long long* host16) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_bnn_prof), sizeof(unsigned long long) * 16) != hipSuccess)
+    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
+  unsigned long long z[16] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_bnn_prof), z, sizeof(z)) != hipSuccess) return nmx_fail(NMX_ERR_HIP, "reset");
+  return NMX_OK;
+}
+#endif
 
 extern "C" size_t nmx_pe_bnn_workspace_bytes(int Dx, int H, int num_chains) {
   const size_t D = 1 + (size_t)Dx * H + (size_t)H * H + H;
