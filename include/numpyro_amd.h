@@ -388,6 +388,12 @@ size_t nmx_gemm_x3_split_bytes(int lda, int ldc);
 int nmx_gemm_chains_x3(const void* Ap, int lda, int dim, const float* In, float* Out, const float* bias,
                        int triangle, int ldc, const int32_t* phase, const int32_t* active_count, int num_chains,
                        void* split, void* workspace, void* stream);
+/* nmx_gemm_chains_x3 with In gathered from a chain-row arena field: column p of the operand is
+ * rows[list[p]][0..dim) (p < *active_count; [ldc][dim] rows, NMX_LAYOUT_CHAIN_ROWS) -- the
+ * nmx_pack_rows + nmx_gemm_chains_x3 pair in one call, bitwise the same product columns. */
+int nmx_gemm_chains_x3_rows(const void* Ap, int lda, int dim, const float* rows, const int32_t* list, float* Out,
+                            const float* bias, int triangle, int ldc, const int32_t* active_count, int num_chains,
+                            void* split, void* workspace, void* stream);
 /* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
  * (p < *count, device-side count, grid sized for ldo / ldi positions). */
 int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,

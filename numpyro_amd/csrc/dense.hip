@@ -430,6 +430,46 @@ __global__ __launch_bounds__(256) void k_x3_split_b(const float* __restrict__ In
   Bp[base + 128] = b3;
 }
 
+// The same split with the operand gathered from a chain-row arena: column p of In is the row of
+// chain list[p] (rows[list[p]][k], [ldc][D] rows, NMX_LAYOUT_CHAIN_ROWS) -- nmx_pack_rows and
+// k_x3_split_b in one pass.  Each lane reads 8 consecutive floats of its chain's row (two
+// 16-byte loads when D % 8 == 0); the k-steps run fastest over the grid, so one workgroup's
+// four waves read 256 contiguous bytes of each of 32 rows (the split image is laid out chain
+// tile fastest: each wave still writes 3 KB contiguous).  Positions >= *count split as zeros
+// (their product columns are never read).
+__global__ __launch_bounds__(256) void k_x3_split_b_rows(const float* __restrict__ rows, int D,
+                                                         const int32_t* __restrict__ list, int ldc, int n_ks,
+                                                         const int32_t* __restrict__ count, bf16x8* __restrict__ Bp) {
+  const int n_ct = ldc / 32;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n_ks * n_ct * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t qg = i >> 6;
+  const int ks = (int)(qg % n_ks), ct = (int)(qg / n_ks);
+  const int n = *count;
+  if (ct * 32 >= n) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int p = 32 * ct + r;
+  const int k0 = 16 * ks + 8 * h;
+  float v[8];
+  if (p < n && (D & 7) == 0) {
+    const float4* src = reinterpret_cast<const float4*>(rows + (size_t)list[p] * D + k0);
+    const float4 a = k0 < D ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = k0 < D ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+  } else {
+    const float* row = p < n ? rows + (size_t)list[p] * D : nullptr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (row && k0 + j < D) ? row[k0 + j] : 0.0f;
+  }
+  bf16x8 b1, b2, b3;
+  split3(v, b1, b2, b3);
+  const size_t base = ((size_t)ks * n_ct + ct) * 3 * 64 + lane;
+  Bp[base] = b1;
+  Bp[base + 64] = b2;
+  Bp[base + 128] = b3;
+}
+
 // chain tiles of 32 per workgroup (2: 128 x 64 outputs per workgroup, two per CU; 4: 128 x 128,
 // one per CU, 1.5x the MFMA work per staged byte)
 #ifndef NMX_GEMM_CT
@@ -716,9 +756,32 @@ int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out
 }
 }  // namespace
 
+namespace {
+int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_t* rows_list, float* Out,
+                   const float* bias, int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
+                   int num_chains, void* split, void* workspace, void* stream);
+}  // namespace
+
 extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* In, float* Out, const float* bias,
                                   int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
                                   int num_chains, void* split, void* workspace, void* stream) {
+  return gemm_chains_x3(Ap, lda, D, In, nullptr, Out, bias, triangle, ldc, phase, active_count, num_chains, split,
+                        workspace, stream);
+}
+
+extern "C" int nmx_gemm_chains_x3_rows(const void* Ap, int lda, int D, const float* rows, const int32_t* list,
+                                       float* Out, const float* bias, int triangle, int ldc,
+                                       const int32_t* active_count, int num_chains, void* split, void* workspace,
+                                       void* stream) {
+  if (!list || !active_count) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3_rows: needs the list and its count");
+  return gemm_chains_x3(Ap, lda, D, rows, list, Out, bias, triangle, ldc, nullptr, active_count, num_chains, split,
+                        workspace, stream);
+}
+
+namespace {
+int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_t* rows_list, float* Out,
+                   const float* bias, int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
+                   int num_chains, void* split, void* workspace, void* stream) {
   if (!Ap || !In || !Out || !split) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: NULL operand");
   if (D <= 0 || ldc % 64 || num_chains <= 0 || num_chains > ldc)
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: bad sizes (D=%d ldc=%d C=%d)", D, ldc, num_chains);
@@ -731,8 +794,12 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
   hipStream_t s = (hipStream_t)stream;
   const int n_ks = lda / 16;
   const int64_t nb = (int64_t)n_ks * (ldc / 32) * 64;
-  hipLaunchKernelGGL(k_x3_split_b, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, In, D, ldc, n_ks,
-                     active_count, (bf16x8*)split);
+  if (rows_list)
+    hipLaunchKernelGGL(k_x3_split_b_rows, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, In, D, rows_list, ldc,
+                       n_ks, active_count, (bf16x8*)split);
+  else
+    hipLaunchKernelGGL(k_x3_split_b, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, In, D, ldc, n_ks,
+                       active_count, (bf16x8*)split);
   if (int st = nmx_check_launch("k_x3_split_b")) return st;
   // K-splits: a function of D only (never of C), at most ksplit_for(D) (the workspace size);
   // measured at D = 10000 (profiles/r01): no split is fastest all-active (2.2 vs 2.4 ms per
@@ -762,6 +829,7 @@ extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* I
                        D, ldc, Out, bias, phase, active_count, num_chains);
   return nmx_check_launch("k_gemm_x3");
 }
+}  // namespace
 
 extern "C" int nmx_pe_mvn(const float* prec_t, int lda, const float* mu, const float* neg_prec_mu, int dim,
                           const nmx_eval_batch* ev, void* stream) {

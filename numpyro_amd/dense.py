@@ -27,6 +27,7 @@ n = the pooled sample count (PooledCovariance).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -86,6 +87,13 @@ class Whitening:
         else:
             check(lib().nmx_gemm_chains(ptr(at), self.lda, self.D, x, out, bias, tri, ldc, phase, count,
                                         int(num_chains), ws, stream), "nmx_gemm_chains")
+
+    def product_rows(self, rows, list_, count, out, num_chains, ldc, stream):
+        """Out = T In + mu on the listed chains' rows gathered in place (In column p = rows[list[p]]):
+        nmx_gemm_chains_x3_rows, the pack + forward product in one call (x3 only)."""
+        check(lib().nmx_gemm_chains_x3_rows(ptr(self.fwd_p), self.lda, self.D, rows, list_, out, ptr(self.mu), UPPER,
+                                            ldc, count, int(num_chains), ptr(self.split_buffer(ldc)),
+                                            ptr(self.workspace(ldc)), stream), "nmx_gemm_chains_x3_rows")
 
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
@@ -158,6 +166,8 @@ class WhitenedPotential(Potential):
         # the engine's arena is in chain rows ([ldc][D], k_chain_step): listed chains are
         # gathered from / scattered to rows (nmx_pack_rows / nmx_unpack_rows)
         self.rows = False
+        # (NMX_DENSE_PACK_ROWS=1, experiments: the separate nmx_pack_rows pass, for A/B runs)
+        self.fused_rows = os.environ.get("NMX_DENSE_PACK_ROWS", "0") != "1"
 
     def _bind(self, C, ldc, device):
         self.base.bind(C, ldc, device)
@@ -192,13 +202,17 @@ class WhitenedPotential(Potential):
         C, ldc, D = ev.num_chains, ev.ldc, self.dim
         if ev.active_idx:
             # compacted list: the products run on packed columns of the listed chains only
-            if self.rows:
-                check(L.nmx_pack_rows(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
-                      "nmx_pack_rows")
+            if self.rows and wt.x3 and self.fused_rows:
+                # gathered from the rows inside the operand split (no packed copy)
+                wt.product_rows(ev.z, ev.active_idx, ev.active_count, ptr(self.zb), C, ldc, stream)
             else:
-                check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
-                      "nmx_pack_columns")
-            wt.product(True, ptr(self.wp), ptr(self.zb), ptr(wt.mu), None, ev.active_count, C, ldc, stream)
+                if self.rows:
+                    check(L.nmx_pack_rows(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc, stream),
+                          "nmx_pack_rows")
+                else:
+                    check(L.nmx_pack_columns(ev.z, ldc, D, ev.active_idx, ev.active_count, ptr(self.wp), ldc,
+                                             stream), "nmx_pack_columns")
+                wt.product(True, ptr(self.wp), ptr(self.zb), ptr(wt.mu), None, ev.active_count, C, ldc, stream)
             self.base.evaluate(self._base_batch(ev), stream)
             wt.product(False, ptr(self.gb), ptr(self.wp), None, None, ev.active_count, C, ldc, stream)
             if self.rows:

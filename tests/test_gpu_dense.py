@@ -179,6 +179,42 @@ def test_gemm_chains_x3_tiles_agree(device, tri):
     assert np.all(np.isnan(outs[0][:, ~tiles])) and np.all(np.isnan(outs[1][:, ~tiles]))
 
 
+@pytest.mark.parametrize("D,ldc,n", [(5, 64, 3), (150, 256, 77), (200, 128, 100), (1001, 512, 300), (10000, 4096, 4000)])
+def test_gemm_chains_x3_rows_matches_pack_then_product(device, D, ldc, n):
+    """nmx_gemm_chains_x3_rows (the listed chains' rows gathered inside the operand split) gives
+    bitwise the product columns of nmx_pack_rows + nmx_gemm_chains_x3 for positions < count
+    (D = 10000 x 4000 listed: config 2's shape, the 256 x 128 tile)."""
+    rs = np.random.RandomState(D)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    At = np.zeros((lda, lda), np.float32)
+    At[:D, :D] = np.triu(rs.randn(D, D)).T
+    dAt = torch.from_numpy(At).to(device)
+    rows = torch.from_numpy(rs.randn(ldc, D).astype(np.float32)).to(device)
+    lst = torch.zeros(ldc, dtype=torch.int32, device=device)
+    lst[:n] = torch.from_numpy(rs.permutation(ldc)[:n].astype(np.int32)).to(device)
+    cnt = torch.tensor([n], dtype=torch.int32, device=device)
+    db = torch.from_numpy(rs.randn(D).astype(np.float32)).to(device)
+    Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=device)
+    sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, ldc), dtype=torch.uint8, device=device)
+    s = native.stream_ptr()
+    P_ = native.ptr
+    native.check(lib.nmx_gemm_x3_pack_a(P_(dAt), lda, P_(Ap), s))
+    packed = torch.full((D, ldc), 7.0, device=device)  # stale values past the count
+    native.check(lib.nmx_pack_rows(P_(rows), ldc, D, P_(lst), P_(cnt), P_(packed), ldc, s))
+    ref = torch.full((D, ldc), float("nan"), device=device)
+    native.check(lib.nmx_gemm_chains_x3(P_(Ap), lda, D, P_(packed), P_(ref), P_(db), 1, ldc, None, P_(cnt), ldc,
+                                        P_(sp), None, s))
+    out = torch.full((D, ldc), float("nan"), device=device)
+    native.check(lib.nmx_gemm_chains_x3_rows(P_(Ap), lda, D, P_(rows), P_(lst), P_(out), P_(db), 1, ldc, P_(cnt),
+                                             ldc, P_(sp), None, s))
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :n], ref[:, :n])
+    assert not torch.isnan(out[:, :n]).any()
+    assert lib.nmx_gemm_chains_x3_rows(P_(Ap), lda, D, P_(rows), None, P_(out), None, 0, ldc, P_(cnt), ldc,
+                                       P_(sp), None, s) != 0  # a list is required
+
+
 def _corr_cov(D, seed=0):
     rs = np.random.RandomState(seed)
     a = np.tril(0.5 * np.fliplr(np.eye(D)) + 0.1 * np.exp(rs.randn(D, D)))
