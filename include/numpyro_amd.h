@@ -394,6 +394,13 @@ int nmx_gemm_chains_x3(const void* Ap, int lda, int dim, const float* In, float*
 int nmx_gemm_chains_x3_rows(const void* Ap, int lda, int dim, const float* rows, const int32_t* list, float* Out,
                             const float* bias, int triangle, int ldc, const int32_t* active_count, int num_chains,
                             void* split, void* workspace, void* stream);
+/* nmx_gemm_chains_x3 with the product column p (< *active_count) stored to the chain-row arena
+ * row rows[list[p]][0..dim) (and pe_out[list[p]] = pe_in[p] when pe_in is given) -- the
+ * nmx_gemm_chains_x3 + nmx_unpack_rows pair in one call; never K-split (no workspace), so for
+ * dim <= 16384 bitwise the same values. */
+int nmx_gemm_chains_x3_to_rows(const void* Ap, int lda, int dim, const float* In, const int32_t* list, float* rows,
+                               const float* bias, int triangle, int ldc, const int32_t* active_count, int num_chains,
+                               void* split, const float* pe_in, float* pe_out, void* stream);
 /* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
  * (p < *count, device-side count, grid sized for ldo / ldi positions). */
 int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,

@@ -504,7 +504,8 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
                                                     const int32_t* __restrict__ phase,
                                                     const int32_t* __restrict__ count, int C,
                                                     float* __restrict__ part, int ksplit, int order, int n_rt,
-                                                    int n_ct) {
+                                                    int n_ct, const int32_t* __restrict__ out_list,
+                                                    const float* __restrict__ pe_in, float* __restrict__ pe_out) {
   extern __shared__ __attribute__((aligned(16))) float lds_f[];  // (the TU's one dynamic-LDS symbol)
   char* const lds = reinterpret_cast<char*>(lds_f);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l31 = lane & 31;
@@ -624,6 +625,33 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
     }
     buf = buf + 1 == NBUF ? 0 : buf + 1;
   }
+  if (out_list) {
+    // scattered to the listed chains' rows (Out [.][D], NMX_LAYOUT_CHAIN_ROWS; one K-split): a
+    // lane holds 4 consecutive coordinates per register group -- 16-byte stores when D % 4 == 0
+    const int n = *count;
+#pragma unroll
+    for (int cl = 0; cl < CT; ++cl) {
+      const int cc = c0 + 32 * cl + l31;
+      if (cc >= n) continue;
+      float* const row = Out + (size_t)out_list[cc] * D;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = i0 + w * 32 + 8 * rg + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[cl][4 * rg + j] + ((bias && i + j < D) ? bias[i + j] : 0.0f);
+        if ((D & 3) == 0) {
+          if (i < D) *reinterpret_cast<float4*>(row + i) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (i + j < D) row[i + j] = v[j];
+        }
+      }
+      if (pe_in && rt_i == 0 && w == 0 && h == 0) pe_out[out_list[cc]] = pe_in[cc];
+    }
+    return;
+  }
   float* const dst = ksplit > 1 ? part + (size_t)z * D * ldc : Out;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -740,7 +768,7 @@ namespace {
 template <int CT, int NBUF, int RW>
 int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out, const float* bias, int triangle,
                    int ldc, const int32_t* phase, const int32_t* active_count, int num_chains, void* workspace,
-                   int ks, hipStream_t s) {
+                   int ks, hipStream_t s, const int32_t* out_list, const float* pe_in, float* pe_out) {
   const int n_rt = (lda + 32 * RW - 1) / (32 * RW), n_ct = (ldc + 32 * CT - 1) / (32 * CT);
   const dim3 grid((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
   constexpr size_t lds = (size_t)NBUF * x3_pieces<CT, RW>() * 1024;
@@ -751,7 +779,7 @@ int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out
   }
   hipLaunchKernelGGL((k_gemm_x3<CT, NBUF, RW>), grid, dim3(64 * RW), lds, s, (const char*)Ap, lda, D,
                      (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
-                     ks, 1, n_rt, n_ct);
+                     ks, 1, n_rt, n_ct, out_list, pe_in, pe_out);
   return NMX_OK;
 }
 }  // namespace
@@ -759,7 +787,8 @@ int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out
 namespace {
 int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_t* rows_list, float* Out,
                    const float* bias, int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
-                   int num_chains, void* split, void* workspace, void* stream);
+                   int num_chains, void* split, void* workspace, void* stream, const int32_t* out_list = nullptr,
+                   const float* pe_in = nullptr, float* pe_out = nullptr);
 }  // namespace
 
 extern "C" int nmx_gemm_chains_x3(const void* Ap, int lda, int D, const float* In, float* Out, const float* bias,
@@ -778,10 +807,21 @@ extern "C" int nmx_gemm_chains_x3_rows(const void* Ap, int lda, int D, const flo
                         workspace, stream);
 }
 
+extern "C" int nmx_gemm_chains_x3_to_rows(const void* Ap, int lda, int D, const float* In, const int32_t* list,
+                                          float* rows, const float* bias, int triangle, int ldc,
+                                          const int32_t* active_count, int num_chains, void* split,
+                                          const float* pe_in, float* pe_out, void* stream) {
+  if (!list || !active_count || (pe_in && !pe_out))
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3_to_rows: needs the list and its count (and pe_out with pe_in)");
+  return gemm_chains_x3(Ap, lda, D, In, nullptr, rows, bias, triangle, ldc, nullptr, active_count, num_chains, split,
+                        nullptr, stream, list, pe_in, pe_out);
+}
+
 namespace {
 int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_t* rows_list, float* Out,
                    const float* bias, int triangle, int ldc, const int32_t* phase, const int32_t* active_count,
-                   int num_chains, void* split, void* workspace, void* stream) {
+                   int num_chains, void* split, void* workspace, void* stream, const int32_t* out_list,
+                   const float* pe_in, float* pe_out) {
   if (!Ap || !In || !Out || !split) return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: NULL operand");
   if (D <= 0 || ldc % 64 || num_chains <= 0 || num_chains > ldc)
     return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3: bad sizes (D=%d ldc=%d C=%d)", D, ldc, num_chains);
@@ -804,7 +844,7 @@ int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_
   // K-splits: a function of D only (never of C), at most ksplit_for(D) (the workspace size);
   // measured at D = 10000 (profiles/r01): no split is fastest all-active (2.2 vs 2.4 ms per
   // triangular product at C = 4096), 2 splits at C = 512 (0.33 vs 0.37)
-  const int ks = workspace ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
+  const int ks = (workspace && !out_list) ? (D <= 16384 ? 1 : (D + 8191) / 8192) : 1;
   // XCD-aware order always: the chain tiles of a row tile run on one XCD and share its A
   // stages in L2 (the split operand is 1.5x the f32 bytes; 2.7 vs 4.2 ms at D = 10000)
   // Two workgroup tiles, the same products bitwise (an output's k sequence and its MFMAs do
@@ -816,12 +856,12 @@ int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_
   const bool big = NMX_GEMM_BIG && ks == 1 && (int64_t)((lda + 255) / 256) * ((num_chains + 127) / 128) >= 512;
   if (big) {
     if (int st = launch_gemm_x3<4, 2, 8>(Ap, lda, D, split, Out, bias, triangle, ldc, phase, active_count,
-                                         num_chains, workspace, ks, s))
+                                         num_chains, workspace, ks, s, out_list, pe_in, pe_out))
       return st;
   } else {
     if (int st = launch_gemm_x3<NMX_GEMM_CT, NMX_GEMM_NBUF, NMX_GEMM_RW>(Ap, lda, D, split, Out, bias, triangle, ldc,
                                                                        phase, active_count, num_chains, workspace,
-                                                                       ks, s))
+                                                                       ks, s, out_list, pe_in, pe_out))
       return st;
   }
   if (ks > 1)

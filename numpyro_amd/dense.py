@@ -95,6 +95,13 @@ class Whitening:
                                             ldc, count, int(num_chains), ptr(self.split_buffer(ldc)),
                                             ptr(self.workspace(ldc)), stream), "nmx_gemm_chains_x3_rows")
 
+    def product_to_rows(self, x, list_, count, rows, pe_in, pe_out, num_chains, ldc, stream):
+        """rows[list[p]] = (T^T In)[:, p] for p < count, pe_out[list[p]] = pe_in[p]:
+        nmx_gemm_chains_x3_to_rows, the backward product + unpack in one call (x3 only)."""
+        check(lib().nmx_gemm_chains_x3_to_rows(ptr(self.bwd_p), self.lda, self.D, x, list_, rows, None, LOWER, ldc,
+                                               count, int(num_chains), ptr(self.split_buffer(ldc)), pe_in, pe_out,
+                                               stream), "nmx_gemm_chains_x3_to_rows")
+
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
         imm = torch.as_tensor(inverse_mass_matrix, dtype=torch.float64).to(self.device)
@@ -214,6 +221,11 @@ class WhitenedPotential(Potential):
                                              stream), "nmx_pack_columns")
                 wt.product(True, ptr(self.wp), ptr(self.zb), ptr(wt.mu), None, ev.active_count, C, ldc, stream)
             self.base.evaluate(self._base_batch(ev), stream)
+            if self.rows and wt.x3 and self.fused_rows:
+                # stored to the chain rows by the product's epilogue (no packed copy)
+                wt.product_to_rows(ptr(self.gb), ev.active_idx, ev.active_count, ev.grad, ptr(self.pe_p), ev.pe, C,
+                                   ldc, stream)
+                return
             wt.product(False, ptr(self.gb), ptr(self.wp), None, None, ev.active_count, C, ldc, stream)
             if self.rows:
                 check(L.nmx_unpack_rows(ptr(self.wp), ldc, D, ev.active_idx, ev.active_count, ev.grad, ldc,

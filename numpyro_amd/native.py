@@ -160,6 +160,8 @@ SIGNATURES: dict[str, tuple] = {
                                    c_vp]),
     "nmx_gemm_chains_x3_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int, c_vp,
                                         c_vp, c_vp]),
+    "nmx_gemm_chains_x3_to_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int,
+                                           c_vp, c_vp, c_vp, c_vp]),
     "nmx_pack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_chain_matvec": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_chain_welford": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

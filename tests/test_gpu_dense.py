@@ -215,6 +215,47 @@ def test_gemm_chains_x3_rows_matches_pack_then_product(device, D, ldc, n):
                                        P_(sp), None, s) != 0  # a list is required
 
 
+@pytest.mark.parametrize("D,ldc,n", [(5, 64, 3), (150, 256, 77), (200, 128, 100), (1001, 512, 300),
+                                     (10000, 4096, 4000)])
+def test_gemm_chains_x3_to_rows_matches_product_then_unpack(device, D, ldc, n):
+    """nmx_gemm_chains_x3_to_rows (the product stored to the listed chains' rows by its epilogue)
+    gives bitwise the rows and pe of nmx_gemm_chains_x3 + nmx_unpack_rows, and leaves the rows of
+    unlisted chains untouched."""
+    rs = np.random.RandomState(D + 1)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    At = np.zeros((lda, lda), np.float32)
+    At[:D, :D] = np.tril(rs.randn(D, D)).T
+    dAt = torch.from_numpy(At).to(device)
+    cols = torch.from_numpy(rs.randn(D, ldc).astype(np.float32)).to(device)
+    lst = torch.zeros(ldc, dtype=torch.int32, device=device)
+    chosen = rs.permutation(ldc)[:n].astype(np.int32)
+    lst[:n] = torch.from_numpy(chosen).to(device)
+    cnt = torch.tensor([n], dtype=torch.int32, device=device)
+    pe_in = torch.from_numpy(rs.randn(ldc).astype(np.float32)).to(device)
+    Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=device)
+    sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, ldc), dtype=torch.uint8, device=device)
+    s = native.stream_ptr()
+    P_ = native.ptr
+    native.check(lib.nmx_gemm_x3_pack_a(P_(dAt), lda, P_(Ap), s))
+    prod = torch.full((D, ldc), float("nan"), device=device)
+    native.check(lib.nmx_gemm_chains_x3(P_(Ap), lda, D, P_(cols), P_(prod), None, 2, ldc, None, P_(cnt), ldc,
+                                        P_(sp), None, s))
+    ref = torch.full((ldc, D), float("nan"), device=device)
+    pe_ref = torch.full((ldc,), float("nan"), device=device)
+    native.check(lib.nmx_unpack_rows(P_(prod), ldc, D, P_(lst), P_(cnt), P_(ref), ldc, P_(pe_in), P_(pe_ref), s))
+    out = torch.full((ldc, D), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    native.check(lib.nmx_gemm_chains_x3_to_rows(P_(Ap), lda, D, P_(cols), P_(lst), P_(out), None, 2, ldc, P_(cnt),
+                                                ldc, P_(sp), P_(pe_in), P_(pe), s))
+    torch.cuda.synchronize()
+    others = torch.from_numpy(np.setdiff1d(np.arange(ldc), chosen)).to(device)
+    sel = torch.from_numpy(chosen.astype(np.int64)).to(device)
+    assert torch.equal(out[sel], ref[sel]) and torch.equal(pe[sel], pe_ref[sel])
+    assert not torch.isnan(out[sel]).any()
+    assert torch.isnan(out[others]).all() and torch.isnan(pe[others]).all()
+
+
 def _corr_cov(D, seed=0):
     rs = np.random.RandomState(seed)
     a = np.tril(0.5 * np.fliplr(np.eye(D)) + 0.1 * np.exp(rs.randn(D, D)))
