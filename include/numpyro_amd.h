@@ -337,6 +337,11 @@ size_t nmx_pe_wide_workspace_bytes(int dim, int num_chains);
  * bytes <= 160 KiB). */
 int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev, void* workspace,
                void* stream);
+/* nmx_pe_bnn on operands already in rows: position p of the batch reads z_rows[p][0..D) and
+ * writes g_rows[p][0..D) (D = 1 + Dx H + H^2 + H; pe to ev->pe[chain(p)]), without the
+ * column <-> row transposes (the whitened dense path hands its products over in rows). */
+int nmx_pe_bnn_rows(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev,
+                    const float* z_rows, float* g_rows, void* stream);
 /* Workspace of nmx_pe_bnn: the evaluated chains' z and gradient transposed to rows. */
 size_t nmx_pe_bnn_workspace_bytes(int Dx, int H, int num_chains);
 
@@ -401,6 +406,13 @@ int nmx_gemm_chains_x3_rows(const void* Ap, int lda, int dim, const float* rows,
 int nmx_gemm_chains_x3_to_rows(const void* Ap, int lda, int dim, const float* In, const int32_t* list, float* rows,
                                const float* bias, int triangle, int ldc, const int32_t* active_count, int num_chains,
                                void* split, const float* pe_in, float* pe_out, void* stream);
+/* The general form of the two above: In gathered from rows through in_list (or [dim][ldc]
+ * columns when NULL), Out stored to rows through out_list (or columns when NULL); positions
+ * < *active_count; pe_out[out_list[p]] = pe_in[p] when pe_in is given.  Never K-split. */
+int nmx_gemm_chains_x3_lists(const void* Ap, int lda, int dim, const float* In, const int32_t* in_list, float* Out,
+                             const int32_t* out_list, const float* bias, int triangle, int ldc,
+                             const int32_t* active_count, int num_chains, void* split, const float* pe_in,
+                             float* pe_out, void* stream);
 /* Column compaction around the dense products: packed[d][p] = in[d][list[p]] and back
  * (p < *count, device-side count, grid sized for ldo / ldi positions). */
 int nmx_pack_columns(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,

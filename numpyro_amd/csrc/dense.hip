@@ -817,6 +817,16 @@ extern "C" int nmx_gemm_chains_x3_to_rows(const void* Ap, int lda, int D, const 
                         nullptr, stream, list, pe_in, pe_out);
 }
 
+extern "C" int nmx_gemm_chains_x3_lists(const void* Ap, int lda, int D, const float* In, const int32_t* in_list,
+                                        float* Out, const int32_t* out_list, const float* bias, int triangle, int ldc,
+                                        const int32_t* active_count, int num_chains, void* split, const float* pe_in,
+                                        float* pe_out, void* stream) {
+  if (!active_count || (pe_in && (!pe_out || !out_list)))
+    return nmx_fail(NMX_ERR_INVALID, "gemm_chains_x3_lists: needs the count (and out_list, pe_out with pe_in)");
+  return gemm_chains_x3(Ap, lda, D, In, in_list, Out, bias, triangle, ldc, nullptr, active_count, num_chains, split,
+                        nullptr, stream, out_list, pe_in, pe_out);
+}
+
 namespace {
 int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_t* rows_list, float* Out,
                    const float* bias, int triangle, int ldc, const int32_t* phase, const int32_t* active_count,

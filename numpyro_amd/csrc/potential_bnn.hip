@@ -428,3 +428,22 @@ extern "C" int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, 
   hipLaunchKernelGGL(k_rows_to_cols, tgrid, dim3(256), 0, s, gr, D, *ev, ev->grad);
   return nmx_check_launch("k_bnn");
 }
+
+extern "C" int nmx_pe_bnn_rows(const float* X, const float* Y, int N, int Dx, int H, const nmx_eval_batch* ev,
+                               const float* z_rows, float* g_rows, void* stream) {
+  if (!ev || !ev->pe || !X || !Y || !z_rows || !g_rows) return nmx_fail(NMX_ERR_INVALID, "bnn_rows: NULL operand");
+  if (N <= 0 || Dx <= 0 || H <= 0) return nmx_fail(NMX_ERR_INVALID, "bnn_rows: bad sizes");
+  if (ev->num_chains <= 0 || ev->ldc < ev->num_chains || ev->ldc % 64)
+    return nmx_fail(NMX_ERR_INVALID, "bad num_chains/ldc (%d/%d)", ev->num_chains, ev->ldc);
+  const size_t lds = lds_bytes(N, Dx, H);
+  if (lds > 160 * 1024)
+    return nmx_fail(NMX_ERR_UNSUPPORTED, "bnn: N=%d, H=%d needs %zu bytes of LDS (> 160 KiB)", N, H, lds);
+  BnnDims dm{N, Dx, H, 1, 1 + Dx * H, 1 + Dx * H + H * H};
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "bnn: hipFuncSetAttribute: %s", hipGetErrorString(e));
+  }
+  const int D = 1 + Dx * H + H * H + H;
+  hipLaunchKernelGGL(k_bnn, dim3(ev->ldc), dim3(THREADS), lds, (hipStream_t)stream, X, Y, dm, *ev, z_rows, g_rows, D);
+  return nmx_check_launch("k_bnn");
+}

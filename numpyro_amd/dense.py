@@ -102,6 +102,15 @@ class Whitening:
                                                count, int(num_chains), ptr(self.split_buffer(ldc)), pe_in, pe_out,
                                                stream), "nmx_gemm_chains_x3_to_rows")
 
+    def product_lists(self, forward, x, in_list, out, out_list, bias, count, num_chains, ldc, stream, pe_in=None,
+                      pe_out=None):
+        """nmx_gemm_chains_x3_lists: In gathered from rows through in_list (or columns), Out stored to
+        rows through out_list (or columns), positions < count (x3 only)."""
+        ap, tri = (self.fwd_p, UPPER) if forward else (self.bwd_p, LOWER)
+        check(lib().nmx_gemm_chains_x3_lists(ptr(ap), self.lda, self.D, x, in_list, out, out_list, bias, tri, ldc,
+                                             count, int(num_chains), ptr(self.split_buffer(ldc)), pe_in, pe_out,
+                                             stream), "nmx_gemm_chains_x3_lists")
+
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
         imm = torch.as_tensor(inverse_mass_matrix, dtype=torch.float64).to(self.device)
@@ -180,6 +189,7 @@ class WhitenedPotential(Potential):
         self.base.bind(C, ldc, device)
         if self.whitening is None or self.whitening.device != device:
             self.whitening = Whitening(self.dim, device)
+        self._rows_zg = None
         self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self.wp = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)   # packed w / g_w
@@ -203,10 +213,29 @@ class WhitenedPotential(Potential):
             self._batches[key] = b
         return b
 
+    def _row_buffers(self, ldc):
+        """Model-space z and gradient of the packed positions in rows ([ldc][D]), allocated on
+        first use (the base potentials with evaluate_rows)."""
+        if getattr(self, "_rows_zg", None) is None or self._rows_zg[0].shape[0] != ldc:
+            self._rows_zg = tuple(torch.zeros(ldc, self.dim, dtype=torch.float32, device=self.zb.device)
+                                  for _ in range(2))
+        return self._rows_zg
+
     def evaluate(self, ev, stream):
         wt = self.whitening
         L = lib()
         C, ldc, D = ev.num_chains, ev.ldc, self.dim
+        if ev.active_idx and self.rows and wt.x3 and self.fused_rows and hasattr(self.base, "evaluate_rows"):
+            # a base potential that reads and writes rows (BNN): both products gather from and
+            # store to rows -- the chain rows through the list, the model-space rows through the
+            # identity -- and no transpose runs on either side of the base kernel
+            zr, gr = self._row_buffers(ldc)
+            wt.product_lists(True, ev.z, ev.active_idx, ptr(zr), ptr(self.ident), ptr(wt.mu), ev.active_count, C,
+                             ldc, stream)
+            self.base.evaluate_rows(self._base_batch(ev), ptr(zr), ptr(gr), stream)
+            wt.product_lists(False, ptr(gr), ptr(self.ident), ev.grad, ev.active_idx, None, ev.active_count, C, ldc,
+                             stream, ptr(self.pe_p), ev.pe)
+            return
         if ev.active_idx:
             # compacted list: the products run on packed columns of the listed chains only
             if self.rows and wt.x3 and self.fused_rows:

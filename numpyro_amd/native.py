@@ -145,6 +145,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_pe_wide_workspace_bytes": (c_size, [c_int, c_int]),
     "nmx_pe_bnn": (c_int, [c_vp, c_vp, c_int, c_int, c_int, _evp, c_vp, c_vp]),
     "nmx_pe_bnn_workspace_bytes": (c_size, [c_int, c_int, c_int]),
+    "nmx_pe_bnn_rows": (c_int, [c_vp, c_vp, c_int, c_int, c_int, _evp, c_vp, c_vp, c_vp]),
     "nmx_logreg_packed_bytes": (c_size, [c_i64, c_int]),
     "nmx_logreg_pack": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp]),
     "nmx_logreg_workspace_bytes": (c_size, [c_i64, c_int, c_int]),
@@ -162,6 +163,8 @@ SIGNATURES: dict[str, tuple] = {
                                         c_vp, c_vp]),
     "nmx_gemm_chains_x3_to_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int,
                                            c_vp, c_vp, c_vp, c_vp]),
+    "nmx_gemm_chains_x3_lists": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp,
+                                         c_int, c_vp, c_vp, c_vp, c_vp]),
     "nmx_pack_columns": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_chain_matvec": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_chain_welford": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

@@ -285,6 +285,12 @@ class BNN(Potential):
         check(lib().nmx_pe_bnn(ptr(self.X), ptr(self.Y), self.N, self.Dx, self.H, ctypes.byref(ev),
                                ptr(self.workspace), stream), "nmx_pe_bnn")
 
+    def evaluate_rows(self, ev, z_rows, g_rows, stream):
+        """The same on operands in rows (position p: z_rows[p], g_rows[p]; raw pointers):
+        nmx_pe_bnn_rows, no transposes (WhitenedPotential on a chain-row arena)."""
+        check(lib().nmx_pe_bnn_rows(ptr(self.X), ptr(self.Y), self.N, self.Dx, self.H, ctypes.byref(ev), z_rows,
+                                    g_rows, stream), "nmx_pe_bnn_rows")
+
     def flops_per_eval(self, num_chains):
         """Forward + adjoint: ~6 N H^2 + 6 N Dx H FLOPs per chain."""
         return (6.0 * self.N * self.H * self.H + 6.0 * self.N * self.Dx * self.H) * num_chains

@@ -505,6 +505,47 @@ def test_whitened_packed_list_matches_dense_batch(device):
     assert np.all(np.isnan(pe_l[others])) and np.all(np.isnan(g_l[:, others]))
 
 
+def test_whitened_bnn_rows_path_matches_packed_columns(device):
+    """On a chain-row arena the whitened BNN runs its products from and to rows around
+    nmx_pe_bnn_rows (no transposes); the packed-column path (NMX_DENSE_PACK_ROWS=1: pack, column
+    products, transposes in nmx_pe_bnn, unpack) gives bitwise the same pe and gradient rows for
+    the listed chains, and neither touches the others."""
+    rs = np.random.RandomState(11)
+    N, Dx, H = 40, 5, 7
+    X = rs.randn(N, Dx).astype(np.float32)
+    Y = rs.randn(N).astype(np.float32)
+    base = P.BNN(X, Y, H)
+    D = base.dim
+    C, ldc, n = 150, 192, 61
+    wp = WhitenedPotential(base)
+    wp.bind(C, ldc, device)
+    wp.rows = True
+    a = rs.randn(D, D) * 0.05
+    wp.whitening.set(torch.from_numpy(a @ a.T + np.eye(D)), torch.from_numpy(rs.randn(D) * 0.1))
+    Z = torch.from_numpy(rs.randn(ldc, D).astype(np.float32)).to(device)
+    chosen = rs.permutation(C)[:n].astype(np.int32)
+    idx = torch.zeros(ldc, dtype=torch.int32, device=device)
+    idx[:n] = torch.from_numpy(chosen).to(device)
+    cnt = torch.tensor([n], dtype=torch.int32, device=device)
+    s = native.stream_ptr()
+    res = []
+    for fused in (True, False):
+        wp.fused_rows = fused
+        g = torch.full((ldc, D), float("nan"), device=device)
+        pe = torch.full((ldc,), float("nan"), device=device)
+        ev = native.EvalBatch(z=native.ptr(Z), grad=native.ptr(g), pe=native.ptr(pe), phase=None,
+                              active_idx=native.ptr(idx), active_count=native.ptr(cnt), num_chains=C, ldc=ldc)
+        wp.evaluate(ev, s)
+        torch.cuda.synchronize()
+        res.append((pe.cpu().numpy(), g.cpu().numpy()))
+    (pe_f, g_f), (pe_p, g_p) = res
+    np.testing.assert_array_equal(pe_f[chosen], pe_p[chosen])
+    np.testing.assert_array_equal(g_f[chosen], g_p[chosen])
+    assert np.all(np.isfinite(pe_f[chosen])) and np.all(np.isfinite(g_f[chosen]))
+    others = np.setdiff1d(np.arange(ldc), chosen)
+    assert np.all(np.isnan(pe_f[others])) and np.all(np.isnan(g_f[others]))
+
+
 def test_funnel_10k_dense_nuts_runs(device):
     """BASELINE config 2 shape (examples/funnel.py at dim 10000, dense mass) end to end at
     reduced chains and iterations: W = 20 (windows [0-2], [3-17], [18-19]: one pooled
