@@ -69,53 +69,128 @@ def _cpu_model():
     return "unknown"
 
 
+def _c_baseline(cn, st, seed, it0, seconds, chain_offset=0, flop=None):
+    """Time the C restatement of NUTS (oracle/c/nuts_cpu.c, OpenMP) on `st`'s chains resumed from
+    the GPU's state on the GPU's stream, running continuously for `seconds` (every chain starts
+    its next transition at once: a fixed batch); the CPU baseline record."""
+    out = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, it0,
+                 1 << 14, chain_offset=chain_offset, min_transitions=1, seconds=seconds, keep_z=False)
+    leap, wall, pot = out["leapfrogs"], out["wall_s"], out["potential_s"]
+    rec = {"value": leap / wall, "unit": "leapfrog/s", "cores": cn.threads(), "kind": "port",
+           "potential_only": {"value": leap / pot, "unit": "leapfrog/s",
+                              "basis": "the same leapfrogs over the seconds inside the batched potential calls"},
+           "potential_share": pot / wall, "transitions": int(out["done"].sum()), "leapfrogs": int(leap),
+           "wall_s": wall, "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+           "threads_note": "OpenMP threads = the GPU box's CPU share (OMP_NUM_THREADS; nproc is the whole host)"}
+    if flop is not None:
+        rec["potential_gflops"] = flop * leap / pot / 1e9
+    return rec
+
+
+def _gpu_state(state, chains):
+    cols = lambda t: t[:chains].detach().cpu().numpy().copy()  # noqa: E731
+    return {"z": cols(state.z["coefs"]), "zgrad": cols(state.z_grad), "pe": cols(state.potential_energy),
+            "step_size": cols(state.adapt_state.step_size), "inv_mass": cols(state.adapt_state.inverse_mass_matrix),
+            "mass_sqrt": cols(state.adapt_state.mass_matrix_sqrt)}
+
+
 def cpu_baseline(X, y, state, seed, it0, num_warmup, chains, seconds, dev_ns=None, dev_z=None, dev_trace=None):
-    """Reduced-chain CPU comparator (SURVEY.md §8d CPU side 2): `chains` chains of the oracle's
-    NUTS (oracle/hmc_ref.py, float32) started from the GPU's adapted state of the first chains
-    (z, U, grad, step size, diagonal mass) and the same Philox stream, so they run the timed
-    workload's trees; their potential calls are batched into the OpenMP C restatement of the
-    covtype potential (oracle/c/logreg_batch.c: register-blocked AVX-512 GEMMs over the full
-    data).  Chains run on continuously until `seconds` have elapsed (a fixed batch: no chain
-    waits for the others between transitions); returns leapfrogs/s.
+    """CPU comparator (SURVEY.md §8d CPU side 2): the C restatement of the NUTS sampling kernel
+    (oracle/c/nuts_cpu.c: the per-chain tree state machine in C, OpenMP over chains; the covtype
+    potential's two GEMMs over the full data batched over the chains, register-blocked AVX-512,
+    oracle/c/logreg_batch.c), `chains` chains started from the GPU's adapted state of the first
+    chains on the same Philox stream, so they run the timed workload's trees; running continuously
+    for `seconds`.  Returns leapfrogs/s, the potential-only rate and the potential's share.
 
     Full-size parity (with dev_ns [chains, T] / dev_z [chains, T, D], the GPU's timed
-    transitions of those chains, and dev_trace, their per-leaf decision trace): the oracle chains'
-    tree sizes and draws are compared with the GPU's transitions from the same state on the same
-    stream, and every chain that leaves the GPU's path is located at its parting leaf."""
+    transitions of those chains, and dev_trace, their per-leaf decision trace): the NumPy oracle
+    (oracle/hmc_ref.py, the C float32 potential) runs the same T transitions from the same state;
+    tree sizes and draws are compared with the GPU's, every chain that leaves the GPU's path is
+    located at its parting leaf; the C restatement's own T transitions are compared too."""
     import numpy as np
 
     from oracle import cpu_batched as CB
+    from oracle import cpu_nuts as CN
 
-    f = CB.LogRegBatch(X, y)
     D = X.shape[1]
-    cols = lambda t: t[:chains].detach().cpu().numpy()  # noqa: E731
-    states, oracles = CB.chains_from_state(
-        cols(state.z["coefs"]), cols(state.z_grad), cols(state.potential_energy), cols(state.adapt_state.step_size),
-        cols(state.adapt_state.inverse_mass_matrix), cols(state.adapt_state.mass_matrix_sqrt), it0, seed, num_warmup)
-    f(np.zeros((chains, D), np.float32))  # untimed: OpenMP pool and first-touch of the partials
-    stats = {}
-    t0 = time.perf_counter()
-    _, hist, leap, calls = CB.run_chains(f, states, oracles, 1 << 30, deadline=t0 + seconds,
-                                         record=dev_ns is not None, stats=stats)
-    dt = time.perf_counter() - t0
-    trans = sum(len(h) for h in hist)
-    gflops = 4.0 * X.shape[0] * D * leap / stats["pot_s"] / 1e9
-    out = {"value": leap / dt, "unit": "leapfrog/s", "cores": f.threads(), "kind": "port",
-           "sample": f"reduced C={chains}: {chains} chains of the timed workload (GPU-adapted state, same "
-                     f"stream) run continuously for {dt:.1f}s: {trans} transitions = {leap} leapfrogs in {calls} "
-                     f"batched potential calls; NumPy oracle NUTS (oracle/hmc_ref.py) with the potential batched "
-                     f"over chains into the OpenMP C restatement (oracle/c/logreg_batch.c, register-blocked "
-                     f"AVX-512, full {X.shape[0]}x{D} f32 data)",
-           "potential_gflops": gflops, "potential_share": stats["pot_s"] / dt,
-           "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    st = _gpu_state(state, chains)
+    cn = CN.CpuNuts("covtype", X, y)
+    cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, it0, 1,
+           max_tree_depth=1)  # untimed: OpenMP pool, first touch
+    out = _c_baseline(cn, st, seed, it0, seconds, flop=4.0 * X.shape[0] * D)
+    out["sample"] = (f"reduced C={chains}: {chains} chains of the timed workload (GPU-adapted state, same stream) "
+                     f"run continuously for {out['wall_s']:.1f}s: {out['transitions']} transitions = "
+                     f"{out['leapfrogs']} leapfrogs; C restatement of NUTS (oracle/c/nuts_cpu.c) with the covtype "
+                     f"potential batched over chains (oracle/c/logreg_batch.c, register-blocked AVX-512, full "
+                     f"{X.shape[0]}x{D} f32 data)")
     if dev_ns is not None:
+        T = dev_ns.shape[1]
+        resume = lambda: CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"],  # noqa: E731
+                                              st["inv_mass"], st["mass_sqrt"], it0, seed, num_warmup)
+        _, hist, _, _ = CB.run_chains(CB.LogRegBatch(X, y), *resume(), T, record=True)
         par = _located_parity(hist, dev_trace, dev_ns[:chains], dev_z[:chains], atol=1e-4, label="parity")
-        par["basis"] = ("oracle NUTS (C potential, full data) vs the GPU's timed transitions of the same chains "
-                        "from the same state on the same Philox stream: equal tree sizes and draws within 1e-4 "
-                        "per transition; a chain that parts is located at the first leaf where a decision differs "
-                        "(device decision trace vs oracle leaf records, oracle/parity.py) and checked there")
+        par["basis"] = ("oracle NUTS (NumPy, oracle/hmc_ref.py, with the C float32 potential over the full data) vs "
+                        "the GPU's timed transitions of the same chains from the same state on the same Philox stream: "
+                        "equal tree sizes and draws within 1e-4 per transition; a chain that parts is located at the "
+                        "first leaf where a decision differs (device decision trace vs oracle leaf records, "
+                        "oracle/parity.py) and checked there; a draw that differs with every decision equal is "
+                        "checked against the rounding calibration (the device and the C float32 oracle each against "
+                        "the float64-potential oracle on that chain: device drift <= DRAW_MULT x the C oracle's)")
+        draws = [m for m in par["mismatches"] if m["kind"] == "draw"]
+        if draws:
+            _headline_draw_calibration(par, draws, X, y, hist, dev_trace, dev_ns[:chains], dev_z[:chains], D, resume)
+        # the C restatement over the same transitions: a second, independent float32 implementation
+        c = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, it0, T)
+        ok = [bool(np.array_equal(c["num_steps"][i], dev_ns[i]) and np.allclose(c["z"][i], dev_z[i], atol=1e-4))
+              for i in range(chains)]
+        par["c_restatement"] = {"chains": chains, "matched": int(sum(ok)),
+                                "basis": "oracle/c/nuts_cpu.c chains (same state, same stream) vs the GPU's timed "
+                                         "transitions: equal tree sizes and draws within 1e-4"}
         out["parity"] = par
     return out
+
+
+def _headline_draw_calibration(par, draws, X, y, hist, dev_trace, dev_ns, dev_z, D, resume):
+    """The headline's draw mismatches bounded by a rounding calibration (oracle/parity.py
+    bound_draws): on the chains with a `draw` mismatch only, the oracle with the potential in
+    rounded float64 (the reference) re-runs their transitions; the device and the C float32
+    oracle are each compared with it, and the device's drift must be within DRAW_MULT x the C
+    oracle's at that transition."""
+    import numpy as np
+
+    from oracle import cpu_batched as CB
+    from oracle import parity as PR
+    from oracle import potentials as OP
+
+    chains = sorted({m["chain"] for m in draws})
+    T = max(m["transition"] for m in draws) + 1
+    r64 = OP.LogisticRegression(X.astype(np.float64), y.astype(np.float64), dtype=np.float64)
+    f64 = lambda Z: tuple(np.asarray(v, np.float32) for v in r64.pe_grad_batch(Z))  # noqa: E731
+    states, oracles = resume()
+    _, h64, _, _ = CB.run_chains(f64, [states[c] for c in chains], [oracles[c] for c in chains], T, record=True)
+    del r64
+    sub32 = [hist[c][:T] for c in chains]
+    ctr, cns, cz = _oracle_trace(sub32, dev_trace.shape[2])
+    cal = PR.compare_traced(h64, ctr, cns, cz, atol=1e-4)
+    dev = PR.compare_traced(h64, dev_trace[:T, chains], dev_ns[chains, :T], dev_z[chains, :T], atol=1e-4)
+    PR.bound_draws(dev, cal)
+    for m in par["mismatches"]:
+        if m["kind"] != "draw":
+            continue
+        sub = [d for d in dev["mismatches"] if chains[d["chain"]] == m["chain"]]
+        if sub and sub[0]["kind"] == "draw":
+            for k in ("cal_drift", "cal_basis", "ratio", "bound", "explained"):
+                m[k] = sub[0][k]
+            m["drift_vs_f64"] = sub[0]["drift"]
+        elif sub:  # vs the float64 reference the device parts at a located decision: judged there
+            m["explained"], m["vs_f64"] = sub[0]["explained"], sub[0]["kind"]
+        print(f"[parity] chain {m['chain']} draw drift vs the float64 reference: " +
+              (PR.describe(sub[0]) if sub else "device matches the float64 reference"), file=sys.stderr)
+        if not sub:  # the device is on the float64 reference's path: the C float32 oracle drifted
+            m["explained"], m["ratio"] = True, 0.0
+    c = PR.counts(par)
+    par["unexplained"] = c["unexplained"]
+    par["draw_drift"] = dev["draw_drift"]
 
 
 def _located_parity(hist, dev_trace, dev_ns, dev_z, atol, rtol=0.0, to_model=None, label="parity"):
@@ -137,6 +212,7 @@ def _located_parity(hist, dev_trace, dev_ns, dev_z, atol, rtol=0.0, to_model=Non
     c = PR.counts(par)
     par["kinds"] = {k: v for k, v in c.items() if k not in ("chains", "matched", "unexplained")}
     par["unexplained"] = c["unexplained"]
+    par.pop("drift")  # per-transition drifts: summarised by bound_draws / drift_stats where calibrated
     return par
 
 
@@ -158,19 +234,26 @@ def _config_specs():
         "c2": dict(name="funnel D=10000, dense mass (pooled), examples/funnel.py", model=P.funnel, args=(10000,),
                    chains=4096, warmup=CONFIG_WARMUP["c2"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * 10000 * 10000, basis="2 D^2 FLOP per chain-leapfrog (z = mu + T w, g_w = T^T g_z)",
-                   cpu=lambda dt=np.float32: OB.FunnelBatch(10000, dtype=dt), cpu_chains=16),
+                   cpu=lambda dt=np.float32: OB.FunnelBatch(10000, dtype=dt), cpu_chains=16,
+                   c_model="funnel", c_args=(10000,)),
         "c3": dict(name="BNN D_X=3 N=100 H=69 (D=5038), dense mass (pooled), examples/bnn.py", model=P.bnn,
                    args=(X, Y, H), chains=2048, warmup=CONFIG_WARMUP["c3"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * D_bnn * D_bnn + 6.0 * 100 * H * H + 6.0 * 100 * 3 * H,
                    basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog",
-                   cpu=lambda dt=np.float32: OB.BNNBatch(X, Y, H, dtype=dt), cpu_chains=16),
+                   cpu=lambda dt=np.float32: OB.BNNBatch(X, Y, H, dtype=dt), cpu_chains=8, parity_transitions=2,
+                   c_model="bnn", c_args=(X, Y, H)),
         "c4": dict(name="stochastic volatility T=2517 (D=2519), diag mass, examples/stochastic_volatility.py",
                    model=P.stochastic_volatility, args=(r,), chains=8192, warmup=CONFIG_WARMUP["c4"],
                    steps=10, dense=False, one_gpu=False, bytes=7 * 4 * 2519,
                    basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)",
-                   cpu=lambda dt=np.float32: OB.SVBatch(r, dtype=dt), cpu_chains=32),
+                   cpu=lambda dt=np.float32: OB.SVBatch(r, dtype=dt), cpu_chains=32,
+                   c_model="sv", c_args=(r,)),
     }
 
+
+# chains of the C restatement's timed CPU run (the GPU's first chains): enough for the batched
+# potentials (covtype's and the whitening's GEMMs) to stream their operand once per many chains
+TIMING_CHAINS = 64
 
 # adaptation transitions per config (the reference examples use 1000; bounded so that the
 # default bench run stays within a few minutes)
@@ -178,77 +261,104 @@ CONFIG_WARMUP = {"c2": 100, "c3": 100, "c4": 200}
 
 
 def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
-    """CPU side of a secondary config (SURVEY.md §8d CPU side 2): `cpu_chains` of the oracle's
-    NUTS resumed from the GPU's adapted state of the first chains (whitened coordinates and the
-    pooled whitening T, mu for dense mass; step size, diagonal mass otherwise) on the same
-    Philox stream, their potential calls batched over chains (oracle/batched.py: NumPy float32,
-    products on multithreaded BLAS), run continuously for `seconds`.  Returns the baseline and a
-    parity record of the oracle's transitions against the GPU's timed ones (tree sizes, draws
-    in model space to 1e-3 relative), each parting located at its leaf with dev_trace (the
-    engine's decision trace of the timed transitions)."""
+    """CPU side of a secondary config (SURVEY.md §8d CPU side 2): `cpu_chains` chains of the C
+    restatement of NUTS (oracle/c/nuts_cpu.c, the config's potential in C; dense mass as whitened
+    identity-mass chains with the GPU's pooled T, mu) resumed from the GPU's adapted state of the
+    first chains on the same Philox stream, running continuously for `seconds`.
+
+    Parity over the first T timed transitions (T = min(steps, sp["parity_transitions"])): the
+    reference is the NumPy oracle (oracle/hmc_ref.py) with the potential in rounded float64
+    (oracle/batched.py, float64) from the same states; the device's transitions (decision trace
+    dev_trace) and the C restatement's (float32 potentials in C, its own decision trace: the
+    rounding calibration) are each compared with it (oracle/parity.py): partings located at their
+    leaf, draws with every decision equal bounded by the calibration's drift there, the records
+    compared by like_calibration."""
     import numpy as np
-    import threadpoolctl
 
     from oracle import batched as OB
     from oracle import cpu_batched as CB
+    from oracle import cpu_nuts as CN
+    from oracle import parity as PR
 
     k = min(sp["cpu_chains"], eng.C)
-    st = {n: eng.chain_state(n)[:k].detach().cpu().numpy().copy()
-          for n in ("z", "zgrad", "pe", "step_size", "inv_mass", "mass_sqrt")}
-    f = sp["cpu"]()
-    to_model = None
+    kt = min(TIMING_CHAINS, eng.C)
+    stt = {n: eng.chain_state(n)[:kt].detach().cpu().numpy().copy()
+           for n in ("z", "zgrad", "pe", "step_size", "inv_mass", "mass_sqrt")}
+    to_model, whiten = None, None
     if eng.dense:
         wt = eng.potential.whitening
-        f = OB.Whitened(f, wt.T.cpu().numpy(), wt.mu.cpu().numpy())
-        st["inv_mass"] = np.ones_like(st["z"])  # identity mass on w (unit_mass on the device)
-        st["mass_sqrt"] = np.ones_like(st["z"])
-        to_model = lambda w: f.to_model(np.asarray(w)[None])[0]  # noqa: E731
+        whiten = (wt.T.cpu().numpy(), wt.mu.cpu().numpy())
+        stt["inv_mass"] = np.ones_like(stt["z"])  # identity mass on w (unit_mass on the device)
+        stt["mass_sqrt"] = np.ones_like(stt["z"])
+        f32w = OB.Whitened(sp["cpu"](), *whiten)
+        to_model = lambda w: f32w.to_model(np.asarray(w)[None])[0]  # noqa: E731
+    st = {n: v[:k] for n, v in stt.items()}  # the parity chains: the first k of them
+    cn = CN.CpuNuts(sp["c_model"], *sp["c_args"], whitening=whiten)
+    out = _c_baseline(cn, stt, seed, eng.iteration, seconds, chain_offset=eng.chain_offset)
+    out["sample"] = (f"reduced C={kt}: {kt} chains of the timed workload (GPU-adapted state, same stream) run "
+                     f"continuously for {out['wall_s']:.1f}s: {out['transitions']} transitions = {out['leapfrogs']} "
+                     f"leapfrogs; C restatement of NUTS (oracle/c/nuts_cpu.c) with the model's potential in C" +
+                     ("; dense mass as the whitened identity-mass chain with the GPU's pooled T, mu (two GEMMs per "
+                      "evaluation, OpenMP)" if eng.dense else ""))
+    T = min(dev_ns.shape[1], sp.get("parity_transitions", dev_ns.shape[1]))
+    label = f"parity {sp['name'].split(',')[0]}"
+    f64 = sp["cpu"](np.float64)
+    if eng.dense:
+        f64 = OB.Whitened(f64, *whiten, dtype=np.float64)
     states, oracles = CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"],
                                            st["mass_sqrt"], eng.iteration, seed, eng.num_warmup,
                                            chain_offset=eng.chain_offset)
-    f(np.zeros((k, eng.D), np.float32))  # untimed: BLAS pool, page faults
-    stats = {}
-    t0 = time.perf_counter()
-    _, hist, leap, calls = CB.run_chains(f, states, oracles, 1 << 30, deadline=t0 + seconds, record=True,
-                                         stats=stats)
-    dt = time.perf_counter() - t0
-    trans = sum(len(h) for h in hist)
-    blas = max([p.get("num_threads", 1) for p in threadpoolctl.threadpool_info()] or [1])
-    out = {"value": leap / dt, "unit": "leapfrog/s", "cores": blas, "kind": "port",
-           "sample": f"reduced C={k}: {k} chains of the timed workload (GPU-adapted state, same stream) run "
-                     f"continuously for {dt:.1f}s: {trans} transitions = {leap} leapfrogs in {calls} batched "
-                     f"potential calls; NumPy oracle NUTS (oracle/hmc_ref.py) with the potential batched over "
-                     f"chains (oracle/batched.py, float32, BLAS products)" +
-                     ("; dense mass as the whitened identity-mass chain with the GPU's pooled T, mu"
-                      if eng.dense else ""),
-           "potential_share": stats["pot_s"] / dt, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
-    par = _located_parity(hist, dev_trace, dev_ns[:k], dev_z[:k], atol=1e-3, rtol=1e-3, to_model=to_model,
-                          label=f"parity {sp['name'].split(',')[0]}")
-    # rounding calibration (oracle/parity.py): the same chains and transitions under the potential
-    # in rounded float64 -- how far two float32-level implementations drift apart on this workload
-    T = min(len(h) for h in hist)
-    if T > 0:
-        from oracle import parity as PR
-
-        f64 = sp["cpu"](np.float64)
-        if eng.dense:
-            f64 = OB.Whitened(f64, wt.T.cpu().numpy(), wt.mu.cpu().numpy(), dtype=np.float64)
-        states, oracles = CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"],
-                                               st["mass_sqrt"], eng.iteration, seed, eng.num_warmup,
-                                               chain_offset=eng.chain_offset)
-        _, hist64, _, _ = CB.run_chains(f64, states, oracles, T, record=True)
-        ctr, cns, cz = _oracle_trace(hist64, dev_trace.shape[2])
-        if to_model is not None:
-            cz = np.stack([[to_model(w) for w in cc] for cc in cz])
-        cal = PR.compare_traced([h[:T] for h in hist], ctr, cns, cz, atol=1e-3, rtol=1e-3, to_model=to_model)
-        dev_T = PR.compare_traced([h[:T] for h in hist], dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3,
-                                  rtol=1e-3, to_model=to_model)
-        ok, msg = PR.like_calibration(dev_T, cal)
-        par["calibration"] = {"basis": "oracle (float32 batch) vs the oracle with the potential in rounded float64, "
-                                       f"same chains, first {T} transitions", **PR.counts(cal),
-                              "max_dE_err": cal["max_dE_err"], "device_like_calibration": ok}
-        print(f"[parity {sp['name'].split(',')[0]}] {msg}", file=sys.stderr)
+    t64 = time.perf_counter()
+    _, hist64, _, _ = CB.run_chains(f64, states, oracles, T, record=True)
+    t64 = time.perf_counter() - t64
+    c = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, eng.iteration,
+               T, chain_offset=eng.chain_offset, trace=True)
+    cz = c["z"].astype(np.float64)
+    if to_model is not None:
+        cz = np.stack([[to_model(w) for w in cc] for cc in cz])
+    L = dev_trace.shape[2]
+    cal = PR.compare_traced(hist64, c["trace"][:, :, :L], c["num_steps"], cz, atol=1e-3, rtol=1e-3, to_model=to_model)
+    PR.bound_draws(cal, cal)
+    par = _located_parity(hist64, dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3, rtol=1e-3,
+                          to_model=to_model, label=label)
+    dev_full = PR.compare_traced(hist64, dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3, rtol=1e-3,
+                                 to_model=to_model)
+    ok, msg = PR.like_calibration(dev_full, cal)
+    for m in dev_full["mismatches"]:
+        if m["kind"] == "draw":
+            print(f"[{label}] " + PR.describe(m), file=sys.stderr)
+    print(f"[{label}] {msg}", file=sys.stderr)
+    _adopt_draw_bounds(par, dev_full)
+    par["basis"] = ("the GPU's timed transitions vs the NumPy oracle NUTS with the potential in rounded float64 (the "
+                    f"reference), same chains from the same state on the same Philox stream, first {T} transitions "
+                    "per chain; partings located at their leaf; draws with every decision equal bounded by the "
+                    f"calibration's drift (DRAW_MULT = {PR.DRAW_MULT})")
+    par["calibration"] = {"basis": "the C restatement (oracle/c/nuts_cpu.c, float32 potentials in C) vs the same "
+                                   "reference, with its own decision trace", **PR.counts(cal),
+                          "max_dE_err": cal["max_dE_err"], "max_dE_rel": cal["max_dE_rel"],
+                          "device_like_calibration": ok}
+    par["draw_drift"] = dev_full["draw_drift"]
+    par["max_dE_rel"], par["worst_dE"] = dev_full["max_dE_rel"], dev_full["worst_dE"]
+    par["transitions_per_chain"] = T
+    par["reference_seconds"] = t64
     return out, par
+
+
+def _adopt_draw_bounds(par, full):
+    """Copy bound_draws' verdict on each draw mismatch from the full record into the JSON one."""
+    import numpy as np
+
+    from oracle import parity as PR
+
+    by = {(m["chain"], m["transition"]): m for m in full["mismatches"]}
+    for m in par["mismatches"]:
+        f = by.get((m["chain"], m["transition"]))
+        if f is not None and m["kind"] == "draw":
+            for k in ("cal_drift", "cal_basis", "ratio", "bound", "explained", "drift"):
+                if k in f:
+                    m[k] = float(f[k]) if isinstance(f[k], (float, np.floating)) else f[k]
+    c = PR.counts(par)
+    par["unexplained"] = c["unexplained"]
 
 
 def _oracle_trace(hist, L):

@@ -3,6 +3,11 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "nmx_api_internal.h"
 
 static thread_local char g_last_error[512] = "";
@@ -18,6 +23,30 @@ int nmx_fail(int code, const char* fmt, ...) {
 int nmx_check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return NMX_OK;
+}
+
+// hipFuncSetAttribute holds per device: a kernel launched on several GPUs of one process needs
+// its dynamic-LDS limit raised on each.  Remembered per (kernel, device) so the host call is
+// made once; the device is the launch stream's (the calling thread's current device may be
+// another one).
+int nmx_lds_limit(const void* fn, size_t bytes, hipStream_t stream, const char* what) {
+  if (bytes <= 64 * 1024) return NMX_OK;
+  int dev = 0;
+  hipError_t e = stream ? hipStreamGetDevice(stream, &dev) : hipGetDevice(&dev);
+  if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "%s: device of the stream: %s", what, hipGetErrorString(e));
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = done.find({fn, dev});
+  if (it != done.end() && it->second >= bytes) return NMX_OK;
+  int cur = dev;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (cur != dev) (void)hipSetDevice(cur);
+  if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "%s: hipFuncSetAttribute: %s", what, hipGetErrorString(e));
+  done[{fn, dev}] = bytes;
   return NMX_OK;
 }
 

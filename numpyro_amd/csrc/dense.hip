@@ -772,11 +772,7 @@ int launch_gemm_x3(const void* Ap, int lda, int D, const void* split, float* Out
   const int n_rt = (lda + 32 * RW - 1) / (32 * RW), n_ct = (ldc + 32 * CT - 1) / (32 * CT);
   const dim3 grid((n_rt + 7) / 8 * 8 * n_ct, 1, ks);
   constexpr size_t lds = (size_t)NBUF * x3_pieces<CT, RW>() * 1024;
-  if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_gemm_x3<CT, NBUF, RW>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "gemm_x3: hipFuncSetAttribute: %s", hipGetErrorString(attr));
-  }
+  if (const int st = nmx_lds_limit((const void*)k_gemm_x3<CT, NBUF, RW>, lds, s, "gemm_x3")) return st;
   hipLaunchKernelGGL((k_gemm_x3<CT, NBUF, RW>), grid, dim3(64 * RW), lds, s, (const char*)Ap, lda, D,
                      (const char*)split, Out, bias, triangle, ldc, phase, active_count, num_chains, (float*)workspace,
                      ks, 1, n_rt, n_ct, out_list, pe_in, pe_out);

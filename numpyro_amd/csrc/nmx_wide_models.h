@@ -22,17 +22,16 @@
 #include "nmx_common.h"
 
 // digamma for x > 0: recurrence up to x >= 6, then the asymptotic series.
-__device__ __forceinline__ float nmx_digammaf(float x) {
-  float acc = 0.0f;
-  while (x < 6.0f) {
-    acc -= 1.0f / x;
-    x += 1.0f;
+__device__ __forceinline__ double nmx_digamma(double x) {  // x > 0: recurrence to x >= 6, asymptotic series
+  double acc = 0.0;
+  while (x < 6.0) {
+    acc -= 1.0 / x;
+    x += 1.0;
   }
-  const float inv = 1.0f / x;
-  const float inv2 = inv * inv;
-  const float series =
-      inv2 * (1.0f / 12.0f - inv2 * (1.0f / 120.0f - inv2 * (1.0f / 252.0f - inv2 * (1.0f / 240.0f - inv2 / 132.0f))));
-  return acc + logf(x) - 0.5f * inv - series;
+  const double inv = 1.0 / x, inv2 = inv * inv;
+  const double series =
+      inv2 * (1.0 / 12.0 - inv2 * (1.0 / 120.0 - inv2 * (1.0 / 252.0 - inv2 * (1.0 / 240.0 - inv2 / 132.0))));
+  return acc + log(x) - 0.5 * inv - series;
 }
 
 // Stochastic volatility (examples/stochastic_volatility.py:57-65), z = (a = log nu, s[T],
@@ -118,25 +117,29 @@ struct NmxWideSV {
     // dU/ds_t = -( -(d_t - d_{t+1})/sigma^2 + (nu+1) q/(1+q) - 1 )
     return (dd - dn) * g.inv_sig2 - (g.nu + 1.0f) * qq + 1.0f;
   }
-  // U and the gradients of the scalar rows (gs[0] = dU/da, gs[1] = dU/db)
+  // U and the gradients of the scalar rows (gs[0] = dU/da, gs[1] = dU/db), in double: the
+  // StudentT normaliser enters as T x (lgamma(nu/2) - lgamma((nu+1)/2)) and dU/da as
+  // T x (psi(nu/2) - psi((nu+1)/2)) -- differences of two O(1) values multiplied by T = 2517, and
+  // dU/da is a small difference of O(T) terms.  In float32 their rounding moved dU/da by ~1e-4
+  // relative and the draws 5-40x further from the float64 reference than a float32 NumPy
+  // implementation's (round-5 parity calibration, tests/test_gpu_nuts.py fixed-step SV); in double
+  // the scalar section costs a few dozen FP64 instructions per chain-leaf (wave 0 only).
   __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
-    const float a = g.a, b = g.b, nu = g.nu, inv_sig2 = g.inv_sig2, inv_nu = g.inv_nu;
-    const float Tf = (float)T;
-    const float sig = expf(b);
-    const float lg = lgammaf(0.5f * nu) - lgammaf(0.5f * (nu + 1.0f));
+    const double a = g.a, b = g.b, nu = exp(a), Tf = (double)T;
+    const double sig = exp(b), inv_sig2 = exp(-2.0 * b);
+    const double s0 = sums[0], s1 = sums[1], s2 = sums[2], s3 = sums[3];
+    const double lg = lgamma(0.5 * nu) - lgamma(0.5 * (nu + 1.0));
     // log p
-    float lp = 3.912023005428146f - 50.0f * sig + b;                        // Exponential(50) + log|J|
-    lp += -0.5f * sums[0] * inv_sig2 - Tf * b - Tf * 0.9189385332046727f;  // GaussianRandomWalk
-    lp += -2.302585092994046f - 0.1f * nu + a;                              // Exponential(0.1) + log|J|
-    lp += -0.5f * (nu + 1.0f) * sums[1] - sums[3] -
-          Tf * (0.5f * logf(nu) + 0.5723649429247001f + lg);               // StudentT(nu, 0, e^s)
-    const float dig = nmx_digammaf(0.5f * nu) - nmx_digammaf(0.5f * (nu + 1.0f));
-    const float ga = nu * (-0.1f - 0.5f * sums[1] + 0.5f * (nu + 1.0f) * inv_nu * sums[2] - 0.5f * Tf * inv_nu -
-                           0.5f * Tf * dig) + 1.0f;
-    const float gb = -50.0f * sig + 1.0f + sums[0] * inv_sig2 - Tf;
-    gs[0] = -ga;
-    gs[1] = -gb;
-    return -lp;
+    double lp = 3.912023005428146 - 50.0 * sig + b;                 // Exponential(50) + log|J|
+    lp += -0.5 * s0 * inv_sig2 - Tf * b - Tf * 0.9189385332046727;  // GaussianRandomWalk
+    lp += -2.302585092994046 - 0.1 * nu + a;                        // Exponential(0.1) + log|J|
+    lp += -0.5 * (nu + 1.0) * s1 - s3 - Tf * (0.5 * a + 0.5723649429247001 + lg);  // StudentT(nu, 0, e^s)
+    const double dig = nmx_digamma(0.5 * nu) - nmx_digamma(0.5 * (nu + 1.0));
+    const double ga = nu * (-0.1 - 0.5 * s1 + 0.5 * (nu + 1.0) / nu * s2 - 0.5 * Tf / nu - 0.5 * Tf * dig) + 1.0;
+    const double gb = -50.0 * sig + 1.0 + s0 * inv_sig2 - Tf;
+    gs[0] = (float)-ga;
+    gs[1] = (float)-gb;
+    return (float)-lp;
   }
 };
 

@@ -467,6 +467,22 @@ __device__ __forceinline__ void tree_phase(const nmx_nuts_config& cfg, ChainScal
     } else {
       const float u = nmx_u01(nmx_rng(seed, gch, S.it, NMX_EV_ACCEPT, 0, 0).x);
       A.hmc_accept = u < A.acc_new;
+      // decision trace: one record per HMC transition (leaf 0), the end point's delta energy
+      // and the Metropolis accept probability it is decided on
+      if (cfg.trace != nullptr && writer && c < cfg.trace_chains && S.it >= cfg.trace_it0 &&
+          S.it < cfg.trace_it0 + cfg.trace_iters && cfg.trace_leaves > 0) {
+        float* R = cfg.trace + ((size_t)(S.it - cfg.trace_it0) * cfg.trace_chains + c) * cfg.trace_leaves *
+                                   NMX_TRACE_REC;
+        R[NMX_T_DE] = -A.w_new;
+        R[NMX_T_P_LEAF] = A.acc_new;
+        R[NMX_T_DOT_SUB] = INFINITY;
+        R[NMX_T_P_BIASED] = -1.0f;
+        R[NMX_T_DOT_TREE] = INFINITY;
+        R[NMX_T_FLAGS] = (float)((A.hmc_accept ? NMX_TF_TAKE_LEAF : 0) | (A.div_new ? NMX_TF_DIVERGE : 0) |
+                                 NMX_TF_DONE_SUB | NMX_TF_ITER_DONE);
+        R[NMX_T_PE] = A.pe_eval;
+        R[NMX_T_LEAF] = 0.0f;
+      }
       if (A.hmc_accept) {
         S.pe = A.pe_eval;
         S.energy = A.E_new;
@@ -3050,27 +3066,29 @@ bool persist_carry(int dim, int nt, size_t static_lds) {
 }
 
 template <int NT, class M>
-void launch_persistent_nt(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
+int launch_persistent_nt(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
   const dim3 grid(args.cfg.num_chains);
   if (persist_carry(args.cfg.dim, NT, (sizeof(PersistShared<NT, M, true>) + 15) / 16 * 16)) {
     const size_t lds = (size_t)16 * args.cfg.dim;
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)k_wide_persistent<NT, NMX_PX_B, M, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (const int st = nmx_lds_limit((const void*)k_wide_persistent<NT, NMX_PX_B, M, true>, lds, s, "run_wide"))
+      return st;
     hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, true>), grid, dim3(NT), lds, s, args, m, max_steps);
   } else {
     hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, false>), grid, dim3(NT), 0, s, args, m, max_steps);
   }
+  return NMX_OK;
 }
 
 template <class M>
 int launch_persistent(const StepArgs& args, const M& m, int max_steps, hipStream_t s) {
+  int st;
   switch (persist_nt(args.cfg.dim)) {
-    case 128: launch_persistent_nt<128>(args, m, max_steps, s); break;
-    case 256: launch_persistent_nt<256>(args, m, max_steps, s); break;
-    case 512: launch_persistent_nt<512>(args, m, max_steps, s); break;
-    default: launch_persistent_nt<1024>(args, m, max_steps, s);
+    case 128: st = launch_persistent_nt<128>(args, m, max_steps, s); break;
+    case 256: st = launch_persistent_nt<256>(args, m, max_steps, s); break;
+    case 512: st = launch_persistent_nt<512>(args, m, max_steps, s); break;
+    default: st = launch_persistent_nt<1024>(args, m, max_steps, s);
   }
+  if (st != NMX_OK) return st;
   return nmx_check_launch("k_wide_persistent");
 }
 }  // namespace

@@ -414,10 +414,7 @@ extern "C" int nmx_pe_bnn(const float* X, const float* Y, int N, int Dx, int H, 
   if (lds > 160 * 1024)
     return nmx_fail(NMX_ERR_UNSUPPORTED, "bnn: N=%d, H=%d needs %zu bytes of LDS (> 160 KiB)", N, H, lds);
   BnnDims dm{N, Dx, H, 1, 1 + Dx * H, 1 + Dx * H + H * H};
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "bnn: hipFuncSetAttribute: %s", hipGetErrorString(e));
-  }
+  if (const int st = nmx_lds_limit((const void*)k_bnn, lds, (hipStream_t)stream, "bnn")) return st;
   const int D = 1 + Dx * H + H * H + H;
   float* zr = (float*)workspace;
   float* gr = zr + (size_t)ev->ldc * D;
@@ -439,10 +436,7 @@ extern "C" int nmx_pe_bnn_rows(const float* X, const float* Y, int N, int Dx, in
   if (lds > 160 * 1024)
     return nmx_fail(NMX_ERR_UNSUPPORTED, "bnn: N=%d, H=%d needs %zu bytes of LDS (> 160 KiB)", N, H, lds);
   BnnDims dm{N, Dx, H, 1, 1 + Dx * H, 1 + Dx * H + H * H};
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "bnn: hipFuncSetAttribute: %s", hipGetErrorString(e));
-  }
+  if (const int st = nmx_lds_limit((const void*)k_bnn, lds, (hipStream_t)stream, "bnn")) return st;
   const int D = 1 + Dx * H + H * H + H;
   hipLaunchKernelGGL(k_bnn, dim3(ev->ldc), dim3(THREADS), lds, (hipStream_t)stream, X, Y, dm, *ev, z_rows, g_rows, D);
   return nmx_check_launch("k_bnn");

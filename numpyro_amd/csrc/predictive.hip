@@ -129,9 +129,8 @@ extern "C" int nmx_predict_bnn(const float* X, int n, int dx, int dh, int dy, co
   const size_t lds = bnn_lds_bytes(n, dx, dh, dy);
   if (lds > 160 * 1024)
     return nmx_fail(NMX_ERR_INVALID, "predict_bnn: weights + activations need %zu B of LDS (> 160 KB)", lds);
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_predict_bnn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) return nmx_fail(NMX_ERR_HIP, "predict_bnn: hipFuncSetAttribute: %s", hipGetErrorString(attr));
+  if (const int st = nmx_lds_limit((const void*)k_predict_bnn, 160 * 1024, (hipStream_t)stream, "predict_bnn"))
+    return st;
   const int D = 1 + dx * dh + dh * dh + dh * dy;
   hipLaunchKernelGGL(k_predict_bnn, dim3(num_samples), dim3(256), lds, (hipStream_t)stream, X, n, dx, dh, dy, samples,
                      D, seed, out);

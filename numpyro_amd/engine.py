@@ -115,7 +115,11 @@ class Engine:
         # structured dense_mass's array, or a matrix for a diagonal mass take the reference's
         # structural form (hmc_util.py:439-487)
         imm = opts.inverse_mass_matrix
-        if imm is not None and (isinstance(imm, dict) or opts.dense_blocks or
+        # a plain array is in the reference's ravel_pytree order (sorted site names); the
+        # potential's layout may order its sites otherwise (front-end models renamed by their
+        # own site names): remap it then, so a vector and a matrix land on the same coordinates
+        layout_sorted = [n for n, _, _ in potential.sites] == sorted(n for n, _, _ in potential.sites)
+        if imm is not None and (isinstance(imm, dict) or opts.dense_blocks or not layout_sorted or
                                 (not self.dense and torch.as_tensor(imm).dim() == 2)):
             from .dense import assemble_inverse_mass_matrix
             structure = opts.dense_blocks if opts.dense_blocks else self.dense

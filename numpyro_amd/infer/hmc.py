@@ -93,11 +93,22 @@ def snapshot_state(eng, seed, keep_arena=True):
     return st
 
 
+def _refuse_combined(state):
+    """A state of a multi-device MCMC run (layout ('devices', ...)) holds one snapshot per device:
+    only that MCMC (post_warmup_state / last_state with the same devices) can resume it."""
+    lay = getattr(state, "_layout", None)
+    if isinstance(lay, tuple) and lay and lay[0] == "devices":
+        raise ValueError(f"this state comes from a run over {len(lay[1])} devices (MCMC(devices=...)) and holds "
+                         "one snapshot per device; resume it with an MCMC over the same devices (post_warmup_state "
+                         "= state), not with a single engine or kernel.sample()")
+
+
 def restore_state(eng, state):
     """Make `state` the engine's current state (no copy when it already is).  A state of
     another engine -- e.g. unpickled from another process -- is copied in when its layout
     matches (same model, chains, dimension, depth, mass-matrix mode), and is then bound to
     this engine."""
+    _refuse_combined(state)
     own = getattr(state, "_engine", None) is eng
     if not own:
         if getattr(state, "_engine", None) is not None or getattr(state, "_layout", None) != eng.layout():
@@ -319,6 +330,7 @@ class HMC(MCMCKernel):
         e.g. MCMC.post_warmup_state)."""
         import torch
 
+        _refuse_combined(state)
         eng = getattr(state, "_engine", None)
         if eng is None:
             if getattr(state, "_layout", None) is None:

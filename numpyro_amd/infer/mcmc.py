@@ -25,19 +25,41 @@ _FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
 from ..shard import shard_chains  # noqa: E402  (re-exported: contiguous chain shard per rank)
 
 
+_VMAP_CHUNK = 1 << 16  # draws per vmapped postprocess_fn call (bounds the batched intermediates)
+
+
+def _vmap_unsupported(e):
+    """An error torch.func.vmap raises for a function it cannot batch (data-dependent control
+    flow, .item() / Python numbers, an op without a batching rule), not a bug of the function."""
+    if not isinstance(e, (RuntimeError, TypeError, NotImplementedError, ValueError)):
+        return False
+    msg = str(e).lower()
+    return any(k in msg for k in ("vmap", "batched", "batching", "functorch", "data-dependent"))
+
+
 def _postprocess_per_draw(fn, sites):
     """postprocess_fn applied to each draw's site dict ({site: [*shape]}), as the reference's
     fori_collect does per iteration (util.py:277-407 _collect_and_postprocess, vmapped over
-    chains when vectorized, mcmc.py:422-442): vectorized over the C x S draws by torch.func.vmap,
-    or one call per draw when fn cannot be vmapped (e.g. it converts to Python numbers).
-    sites: {site: [C, S, *shape]} -> {name: [C, S, *out_shape]}."""
+    chains when vectorized, mcmc.py:422-442): vectorized over the C x S draws by torch.func.vmap
+    in chunks of _VMAP_CHUNK draws, or -- only when vmap cannot batch fn (e.g. it converts to
+    Python numbers) -- one call per draw, with a warning (8192 chains x 1000 draws is 8M calls).
+    Any other error of fn propagates.  sites: {site: [C, S, *shape]} -> {name: [C, S, *out_shape]}."""
+    import warnings
+
     v0 = next(iter(sites.values()))
     C, S = int(v0.shape[0]), int(v0.shape[1])
-    flat = {k: v.reshape(C * S, *v.shape[2:]) for k, v in sites.items()}
+    n = C * S
+    flat = {k: v.reshape(n, *v.shape[2:]) for k, v in sites.items()}
     try:
-        res = dict(torch.func.vmap(fn)(flat))
-    except Exception:  # noqa: BLE001  (not vmappable: per draw)
-        rows = [dict(fn({k: v[i] for k, v in flat.items()})) for i in range(C * S)]
+        parts = [dict(torch.func.vmap(fn)({k: v[i:i + _VMAP_CHUNK] for k, v in flat.items()}))
+                 for i in range(0, n, _VMAP_CHUNK)]
+        res = {k: torch.cat([torch.as_tensor(p[k]) for p in parts]) for k in parts[0]} if parts else {}
+    except Exception as e:  # noqa: BLE001  (re-raised unless vmap could not batch fn)
+        if not _vmap_unsupported(e):
+            raise
+        warnings.warn(f"postprocess_fn cannot be vmapped ({type(e).__name__}: {str(e)[:120]}); applying it "
+                      f"once per draw ({n} calls)", RuntimeWarning, stacklevel=3)
+        rows = [dict(fn({k: v[i] for k, v in flat.items()})) for i in range(n)]
         res = {k: torch.stack([torch.as_tensor(r[k], device=v0.device) for r in rows]) for k in rows[0]} if rows else {}
     return {k: torch.as_tensor(v).reshape(C, S, *torch.as_tensor(v).shape[1:]) for k, v in res.items()}
 
@@ -69,8 +91,12 @@ class MCMC:
         self.device = device
         # chain_method="parallel" (the reference's default: pmap over local devices,
         # mcmc.py:700-715) or a callable (pmap-of-vectorized, mcmc.py:296-320) shards the chains
-        # of this process over `devices` (default: every visible GPU when there are several and
-        # torch.distributed is not running), one engine and one host thread per device
+        # of this process over `devices` -- a list, or "all" for every visible GPU -- one engine
+        # and one host thread per device.  Opt-in: without `devices` a process runs one engine
+        # on its current GPU (one process per GPU under torch.distributed is the scaling path)
+        if devices == "all":
+            n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+            devices = [torch.device("cuda", i) for i in range(n)]
         self.devices = None if devices is None else [torch.device(d) for d in devices]
         self.sync_chains = sync_chains
         self.poll_every = int(poll_every)
@@ -110,13 +136,9 @@ class MCMC:
         """Devices of a multi-device run of this process's chains, or None (one engine)."""
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             return None  # one process per GPU: this rank's shard lives on its device
-        if self.devices is not None:
-            devs = self.devices
-        elif (self.chain_method == "parallel" or callable(self.chain_method)) and self.device is None:
-            n = torch.cuda.device_count() if torch.cuda.is_available() else 0
-            devs = [torch.device("cuda", i) for i in range(n)]
-        else:
+        if self.devices is None:
             return None
+        devs = self.devices
         devs = devs[:max(1, self.local_chains)]
         return devs if len(devs) > 1 else None
 

@@ -12,6 +12,11 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "_lib")
 FLAGS = ["-O3", "-march=x86-64-v4", "-ffast-math", "-fopenmp", "-fPIC", "-shared", "-std=c11", "-Wall"]
+# per-file flags: the C NUTS keeps IEEE semantics (NaN energies, float32 operation order) and links
+# the covtype potential of logreg_batch.c (built first: sorted order)
+FILE_FLAGS = {"nuts_cpu": ["-O3", "-march=x86-64-v4", "-fno-math-errno", "-fopenmp", "-fPIC", "-shared", "-std=gnu11",
+                           "-Wall"]}
+FILE_LIBS = {"nuts_cpu": ["-L{lib}", "-llogreg_batch", "-Wl,-rpath,$ORIGIN"]}
 
 
 def lib_path(name: str) -> str:
@@ -23,9 +28,13 @@ def build(verbose: bool = False) -> None:
     for src in sorted(glob.glob(os.path.join(HERE, "c", "*.c"))):
         name = os.path.splitext(os.path.basename(src))[0]
         out = lib_path(name)
-        if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        # a restatement may #include another (nuts_cpu.c includes logreg_batch.c): rebuild when any is newer
+        newest = max(os.path.getmtime(p) for p in glob.glob(os.path.join(HERE, "c", "*.[ch]")))
+        if os.path.exists(out) and os.path.getmtime(out) >= newest:
             continue
-        r = subprocess.run(["gcc", *FLAGS, src, "-o", out, "-lm"], capture_output=True, text=True)
+        libs = [a.format(lib=LIB_DIR) for a in FILE_LIBS.get(name, [])]
+        r = subprocess.run(["gcc", *FILE_FLAGS.get(name, FLAGS), src, "-o", out, *libs, "-lm"], capture_output=True,
+                           text=True)
         if r.returncode != 0:
             raise RuntimeError(f"gcc failed for {src}:\n{r.stdout}\n{r.stderr}")
         if verbose:

@@ -107,12 +107,14 @@ class _Batcher:
                 self.cv.notify_all()
 
 
-def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, record=False, stats=None):
+def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, record=False, stats=None,
+               min_transitions=0):
     """Advance every (oracle, state) pair by `num_transitions` transitions with batched
     potential evaluations.  `oracles[k]` must have been built with pe_grad = None; it is bound
     here.  With `deadline` (a time.perf_counter() value) a chain starts no further transition
     once it has passed (chains run on continuously until then, so the batch stays full: the
-    CPU comparator's fixed-batch mode).  With `record`, every history entry is (state,
+    CPU comparator's fixed-batch mode); every chain still runs at least `min_transitions` (the
+    parity legs need that many transitions of every chain).  With `record`, every history entry is (state,
     decisions of that transition: (kind, margin) list, see hmc_ref.record_decisions, per-leaf
     records, see hmc_ref.record_leaves and oracle/parity.py).  `stats`
     (a dict) receives the seconds spent inside the batched potential ("pot_s").
@@ -130,8 +132,8 @@ def run_chains(pe_grad_batch, states, oracles, num_transitions, deadline=None, r
             o.pe_grad = fn
             o.vv_init, o.vv_update = H.velocity_verlet(fn)
             st = states[k]
-            for _ in range(num_transitions):
-                if deadline is not None and time.perf_counter() >= deadline:
+            for i in range(num_transitions):
+                if deadline is not None and i >= min_transitions and time.perf_counter() >= deadline:
                     break
                 log = [] if record else None
                 leaves = [] if record else None
@@ -179,42 +181,3 @@ def chains_from_state(z, grad, pe, step_size, inverse_mass, mass_sqrt, it0, seed
                                  np.float32(pe[c]), None, None, None, 0, np.float32(0), np.float32(0), False, wa,
                                  (seed, chain_offset + c)))
     return states, oracles
-
-
-def compare_paths(hist, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, dev_pe=None):
-    """Per-chain parity of oracle histories (run_chains(record=True)) with the device's
-    transitions from the same state: a chain matches while its tree sizes are equal and its
-    draws agree to atol + rtol |z| (`to_model` maps the oracle's coordinates to the device
-    draws' first, e.g. whitened -> model space); at the first difference the oracle's closest
-    decision to a tie is reported.  With `dev_pe` ([chains, T] potential energies of the device
-    draws) the energy noise -- the largest |U_oracle - U_device| at the draws of transitions both
-    took identically -- widens the tie bound of transition / accept decisions to 4x it (the rule
-    of tests/test_gpu_nuts.py _explain_mismatches: a transition probability moves by up to twice
-    the largest leaf-energy discrepancy, taken as twice the one seen at a draw).  Returns
-    {chains, transitions, matched, max_abs_dz, energy_noise, mismatches: [(chain, transition,
-    kind, margin, is_tie)]}."""
-    matched, transitions, max_dz, mism, noise = 0, 0, 0.0, [], 0.0
-    for c, h in enumerate(hist):
-        T = min(len(h), dev_num_steps.shape[1])
-        transitions += T
-        bad = None
-        for t in range(T):
-            st, log = h[t][:2]
-            z = np.asarray(st.z, np.float64) if to_model is None else np.asarray(to_model(st.z), np.float64)
-            ref = np.asarray(dev_z[c, t], np.float64)
-            dz = float(np.max(np.abs(z - ref) - rtol * np.abs(ref)))
-            if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
-                bad = t
-                mism.append((c, t, H.closest_decision(log)))
-                break
-            max_dz = max(max_dz, dz)
-            if dev_pe is not None:
-                noise = max(noise, abs(float(st.potential_energy) - float(dev_pe[c, t])))
-        if bad is None:
-            matched += 1
-    bound = dict(H.TIE)
-    for k in ("transition", "accept"):
-        bound[k] = max(bound[k], 4.0 * noise)
-    out = [(c, t, k, m, bool(k in bound and m <= bound[k])) for c, t, (k, m) in mism]
-    return {"chains": len(hist), "transitions": transitions, "matched": matched, "max_abs_dz": max_dz,
-            "energy_noise": noise if dev_pe is not None else None, "mismatches": out}

@@ -703,6 +703,13 @@ class NUTSOracle:
         u = philox.uniform(seed, chain, it, philox.EV_ACCEPT, 0, 0)
         if accept_prob < 1.0:
             _log("accept", abs(u - accept_prob))
+        log = _leaf_log()
+        if log is not None:  # one record per HMC transition: the Metropolis decision (device leaf 0)
+            log.append({"dE": float(delta_energy), "p_leaf": float(accept_prob), "u_leaf": float(u),
+                        "take_leaf": bool(u < accept_prob), "dot_sub": math.inf, "scale_sub": 0.0, "turn_sub": False,
+                        "diverge": bool(diverging), "pe": float(vv_state_new.potential_energy), "done_sub": True,
+                        "p_biased": -1.0, "u_biased": math.nan, "dot_tree": math.inf, "scale_tree": 0.0,
+                        "take_biased": False, "turn_tree": False, "iter_done": True, "depth": 0, "hmc": True})
         if u < accept_prob:
             return vv_state_new, energy_new, num_steps, accept_prob, diverging
         return vv_state, energy_old, num_steps, accept_prob, diverging

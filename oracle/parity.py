@@ -20,6 +20,8 @@ rounding flip -- `explained` -- when:
   1-Lipschitz in the largest leaf-energy change), so it moves by <= 2 dE_err / 4; the biased one
   min(1, exp(w_sub - w_tree)) moves by <= p * 2 dE_err.  Bound: twice those, plus 1e-6 for the
   probability's own f32 rounding;
+* an HMC Metropolis accept (hmc.py:401-414, one record per transition): as the biased
+  transition, the probability min(1, exp(-dE)) moving by <= p * 2 dE_err;
 * a divergence (hmc_util.py:872): the two delta energies lie on either side of
   max_delta_energy;
 * a U-turn (hmc_util.py:735-746): the two smallest dots have different signs and differ by no
@@ -28,14 +30,27 @@ rounding flip -- `explained` -- when:
 
 A transition whose decisions all agree but whose draw differs is reported as `draw`: the same
 leaf was selected, but the positions drifted apart along the trajectory (leapfrog dynamics of a
-tanh network or a stiff posterior amplify rounding over hundreds of leaves).
+tanh network or a stiff posterior amplify rounding over hundreds of leaves).  A draw has a
+bound too: it is explained only by a rounding calibration (below) -- when the device's drift
+at that chain and transition is within DRAW_MULT x the calibration's drift there (or, where the
+calibration already parted from the reference at an earlier transition, its largest drift at
+the same tree size).  Without a calibration a draw mismatch is unexplained: a bug that corrupts
+the proposal (the whitening's to_model, the collection) while every decision stays equal
+cannot pass as drift.  Drift is measured in tolerance units, max_i |z_i - ref_i| / (atol +
+rtol |ref_i|), so a draw mismatch has drift > 1.
 
 Calibration.  How far rounding alone carries two float32 implementations of the same
-algorithm apart is measured, not assumed: `compare_traced` run between the oracle and a second
-oracle whose potential is another float32 implementation (oracle/batched.py's NumPy batch vs
-oracle/potentials.py's rounded float64, or float32 vs rounded float64 sums) gives the reference
-spread of matched chains, located partings and drift; `like_calibration` requires the device's
-to be of the same order (tests/test_gpu_parity_trace.py)."""
+algorithm apart is measured, not assumed: `compare_traced` run between the reference oracle
+(potential in rounded float64, the most accurate float32 NUTS) and a second oracle whose
+potential is a float32 implementation (oracle/batched.py's NumPy batch, or float32 sums) gives
+the spread rounding alone produces -- matched chains, located partings, the drift of every
+transition whose decisions agree, the relative leaf-energy discrepancy.  The device is compared
+with the same reference; `bound_draws` explains (or not) its draw mismatches by the
+calibration's drift, and `like_calibration` requires its whole record to be of the
+calibration's order: drift distributions compared pairwise on the (chain, transition) pairs both
+reached on the reference's path (geometric mean of the ratios <= DRIFT_GEO_MAX), leaf-energy
+discrepancies relative to the energies' magnitude (tests/test_gpu_parity_trace.py, bench.py's
+config legs)."""
 from __future__ import annotations
 
 import math
@@ -49,6 +64,10 @@ TF_TAKE_LEAF, TF_TURN_SUB, TF_DIVERGE, TF_DONE_SUB, TF_TAKE_BIASED, TF_TURN_TREE
 
 DOT_FLOOR = 1e-5  # relative f32 rounding of a U-turn dot over D <= 1e4 terms
 P_FLOOR = 1e-6  # f32 rounding of a transition probability itself
+DRAW_MULT = 4.0  # a draw mismatch is explained when its drift <= DRAW_MULT x the calibration's there
+DRIFT_GEO_MAX = 2.0  # like_calibration: geometric mean of paired device / calibration drifts
+DRIFT_FLOOR = 1e-2  # drift (tolerance units) below which a ratio is not taken (floored on both sides)
+DE_REL_MULT = 10.0  # like_calibration: relative leaf-energy discrepancy vs the calibration's
 
 
 def _dev_flags(rec):
@@ -94,7 +113,11 @@ def locate(dev, orc, max_delta_energy=1000.0):
         if diff in ("take_leaf", "take_biased"):
             pk, uk = ("p_leaf", "u_leaf") if diff == "take_leaf" else ("p_biased", "u_biased")
             pd, po, u = float(d[T_P_LEAF if diff == "take_leaf" else T_P_BIASED]), o[pk], o[uk]
-            slope = 1.0 if diff == "take_leaf" else 4.0 * max(pd, po)
+            # in-subtree sigmoid: 1-Lipschitz in the leaf energies (x 2 for the logaddexp);
+            # biased / HMC Metropolis min(1, exp(-dE)): slope p per unit of energy
+            slope = 1.0 if diff == "take_leaf" and not o.get("hmc") else 4.0 * max(pd, po)
+            if o.get("hmc"):
+                diff = out["kind"] = "accept"
             bound = slope * de_err + P_FLOOR
             out.update(dev=pd, oracle=po, u=u, margin=abs(u - po), bound=bound,
                        explained=bool((pd - u) * (po - u) <= 0 and abs(pd - po) <= bound))
@@ -114,15 +137,28 @@ def locate(dev, orc, max_delta_energy=1000.0):
     return None
 
 
+def _drift(z, ref, atol, rtol):
+    """Largest coordinate difference in tolerance units (atol + rtol |ref|); raw when both are 0."""
+    den = atol + rtol * np.abs(ref)
+    d = np.abs(z - ref)
+    return float(np.max(d / den)) if np.all(den > 0) else float(np.max(d))
+
+
 def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, max_delta_energy=1000.0):
     """Per-chain parity of oracle histories (oracle.cpu_batched.run_chains(record=True): entries
     (state, decisions, leaves)) with the device's transitions from the same state, each
     mismatch located at its parting leaf.  dev_trace [T, chains, L, 8] is the engine's decision
     trace (Engine.set_trace) over the same transitions.  A chain matches while tree sizes are
     equal and draws agree to atol + rtol |z|.  Returns {chains, transitions, matched,
-    max_abs_dz, max_dE_err, mismatches: [{chain, transition, tree_dev, tree_oracle, leaf, kind,
-    dev, oracle, u, margin, bound, dE_err, explained}], explained}."""
-    matched, transitions, max_dz, max_de, mism = 0, 0, 0.0, 0.0, []
+    max_abs_dz, max_dE_err, max_dE_rel, worst_dE, drift, mismatches: [{chain, transition,
+    tree_dev, tree_oracle, leaf, kind, dev, oracle, u, margin, bound, dE_err, explained}],
+    explained}.  `drift` lists every transition whose decisions all agree (matched, or the
+    chain's `draw` mismatch): {chain, transition, tree, drift (tolerance units), dz}.
+    `worst_dE` locates the largest leaf-energy discrepancy on the common leaves (chain,
+    transition, leaf, the two delta energies, the leaf's potential energy and the discrepancy
+    relative to |U_leaf| + |dE|, the magnitude the energies' rounding scales with)."""
+    matched, transitions, max_dz, max_de, mism, drift = 0, 0, 0.0, 0.0, [], []
+    worst, max_rel = None, 0.0
     for c, h in enumerate(hist):
         T = min(len(h), dev_num_steps.shape[1], dev_trace.shape[0])
         transitions += T
@@ -132,26 +168,88 @@ def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_mod
             z = np.asarray(st.z, np.float64) if to_model is None else np.asarray(to_model(st.z), np.float64)
             ref = np.asarray(dev_z[c, t], np.float64)
             dz = float(np.max(np.abs(z - ref) - rtol * np.abs(ref)))
+            dr = _drift(z, ref, atol, rtol)
             dev = dev_trace[t, c]
             n = min(len(leaves), int(st.num_steps))
-            de = [abs(float(dev[i, T_DE]) - leaves[i]["dE"]) for i in range(n)
-                  if np.isfinite(dev[i, T_DE]) and np.isfinite(leaves[i]["dE"])]
+            de = []
+            for i in range(n):
+                ed, eo = float(dev[i, T_DE]), leaves[i]["dE"]
+                if not (np.isfinite(ed) and np.isfinite(eo)):
+                    continue
+                err = abs(ed - eo)
+                de.append(err)
+                rel = err / max(1.0, abs(float(leaves[i]["pe"])) + abs(eo))
+                if worst is None or rel > worst["rel"]:
+                    worst = {"chain": c, "transition": t, "leaf": i, "dev": ed, "oracle": eo,
+                             "pe": float(leaves[i]["pe"]), "err": err, "rel": rel}
+                max_rel = max(max_rel, rel)
             if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
                 loc = locate(dev, leaves, max_delta_energy)
                 if loc is None:
                     loc = {"leaf": None, "kind": "draw", "dev": None, "oracle": None, "u": None, "margin": dz,
-                           "bound": atol, "dE_err": max(de) if de else 0.0, "explained": False}
+                           "bound": atol, "dE_err": max(de) if de else 0.0, "explained": False, "drift": dr}
+                    drift.append({"chain": c, "transition": t, "tree": int(st.num_steps), "drift": dr, "dz": dz})
                 loc.update(chain=c, transition=t, tree_dev=int(dev_num_steps[c, t]), tree_oracle=int(st.num_steps))
                 mism.append(loc)
                 ok = False
                 break
+            drift.append({"chain": c, "transition": t, "tree": int(st.num_steps), "drift": dr, "dz": dz})
             max_dz = max(max_dz, dz)
             if de:
                 max_de = max(max_de, max(de))
         if ok:
             matched += 1
     return {"chains": len(hist), "transitions": transitions, "matched": matched, "max_abs_dz": max_dz,
-            "max_dE_err": max_de, "mismatches": mism, "explained": sum(1 for m in mism if m["explained"])}
+            "max_dE_err": max_de, "max_dE_rel": max_rel, "worst_dE": worst, "drift": drift,
+            "mismatches": mism, "explained": sum(1 for m in mism if m["explained"])}
+
+
+def bound_draws(par, cal, mult=DRAW_MULT):
+    """Explain (or not) the `draw` mismatches of the device record `par` by the rounding
+    calibration `cal` (compare_traced of a second float32 oracle against the same reference):
+    a draw is a rounding drift when the device's drift is within `mult` x the calibration's on
+    the same chain and transition; where the calibration left the reference's path before that
+    transition, its largest drift at the same tree size (any tree size if none) stands in.  Sets
+    cal_drift / ratio / explained on each draw and par["draw_drift"] (paired drift statistics,
+    see drift_stats); returns par."""
+    at = {(d["chain"], d["transition"]): d["drift"] for d in cal["drift"]}
+    by_tree = {}
+    for d in cal["drift"]:
+        by_tree[d["tree"]] = max(by_tree.get(d["tree"], 0.0), d["drift"])
+    top = max((d["drift"] for d in cal["drift"]), default=0.0)
+    for m in par["mismatches"]:
+        if m["kind"] != "draw":
+            continue
+        key = (m["chain"], m["transition"])
+        ref, how = (at[key], "same chain and transition") if key in at else (
+            (by_tree[m["tree_oracle"]], "largest at this tree size") if m["tree_oracle"] in by_tree
+            else (top, "largest of the calibration"))
+        m["cal_drift"], m["cal_basis"] = ref, how
+        m["ratio"] = m["drift"] / ref if ref > 0 else math.inf
+        m["bound"] = mult * ref
+        m["explained"] = bool(m["ratio"] <= mult)
+    par["explained"] = sum(1 for m in par["mismatches"] if m["explained"])
+    par["draw_drift"] = drift_stats(par, cal)
+    return par
+
+
+def drift_stats(par, cal):
+    """Paired drift of the device and the calibration on the (chain, transition) pairs where both
+    took the reference's decisions: {pairs, geo_mean_ratio, median_dev, median_cal, max_dev,
+    max_cal, draws, max_draw_ratio}.  Drifts in tolerance units; ratios floored at DRIFT_FLOOR units
+    on both sides: drift below 1% of the tolerance is bit-level agreement, whose ratio says nothing
+    (two float32 implementations of a diagonal normal differ there by 2x from a reciprocal)."""
+    a = {(d["chain"], d["transition"]): d["drift"] for d in par["drift"]}
+    b = {(d["chain"], d["transition"]): d["drift"] for d in cal["drift"]}
+    keys = sorted(set(a) & set(b))
+    fl = DRIFT_FLOOR
+    r = [math.log(max(a[k], fl) / max(b[k], fl)) for k in keys]
+    draws = [m for m in par["mismatches"] if m["kind"] == "draw"]
+    return {"pairs": len(keys), "geo_mean_ratio": math.exp(sum(r) / len(r)) if r else None,
+            "median_dev": float(np.median([a[k] for k in keys])) if keys else None,
+            "median_cal": float(np.median([b[k] for k in keys])) if keys else None,
+            "max_dev": max((a[k] for k in keys), default=None), "max_cal": max((b[k] for k in keys), default=None),
+            "draws": len(draws), "max_draw_ratio": max((m.get("ratio", math.inf) for m in draws), default=None)}
 
 
 def oracle_to_trace(leaves, L):
@@ -170,8 +268,13 @@ def oracle_to_trace(leaves, L):
 def describe(m):
     """One line per located mismatch (test / bench stderr)."""
     if m["leaf"] is None:
+        cal = "" if "cal_drift" not in m else (
+            f"; drift {m['drift']:.3g} vs calibration {m['cal_drift']:.3g} ({m['cal_basis']}) = {m['ratio']:.3g}x "
+            f"-> {'rounding drift' if m['explained'] else 'NOT explained by rounding'}")
+        if "cal_drift" not in m:
+            cal = "; no rounding calibration -> NOT explained"
         return (f"chain {m['chain']}: transition {m['transition']} draws differ by {m['margin']:.3g} with every "
-                f"decision equal")
+                f"decision equal{cal}")
     val = "" if m["dev"] is None else f" dev {m['dev']:.6g} oracle {m['oracle']:.6g}"
     u = "" if m["u"] is None else f" u {m['u']:.6g}"
     b = "" if m["bound"] is None else f" bound {m['bound']:.3g}"
@@ -181,24 +284,35 @@ def describe(m):
 
 
 def counts(par):
-    """{matched, chains, <kind>: n, unexplained} of a compare_traced record."""
+    """{matched, chains, <kind>: n, unexplained} of a compare_traced record (a draw counts as
+    unexplained unless bound_draws explained it by a calibration)."""
     out = {"chains": par["chains"], "matched": par["matched"], "unexplained": 0}
     for m in par["mismatches"]:
         out[m["kind"]] = out.get(m["kind"], 0) + 1
-        out["unexplained"] += 0 if (m["explained"] or m["kind"] == "draw") else 1
+        out["unexplained"] += 0 if m["explained"] else 1
     return out
 
 
 def like_calibration(dev, cal, slack=None):
-    """(ok, message): the device-vs-oracle record `dev` is of the same order as the rounding
-    calibration `cal` (oracle vs another float32 oracle on the same chains): every located
-    parting explained at its leaf, matched chains within `slack` (default max(4, chains / 10))
-    of the calibration's, and the largest leaf-energy discrepancy on matched paths within 10x
-    of the calibration's (floor 1e-3)."""
+    """(ok, message): the device-vs-reference record `dev` is of the same order as the rounding
+    calibration `cal` (a second float32 oracle vs the same reference, same chains): its draws
+    bounded by the calibration's drift (bound_draws) and every located parting explained at its
+    leaf; matched chains within `slack` (default max(4, chains / 10)) of the calibration's; the
+    paired drift's geometric-mean ratio <= DRIFT_GEO_MAX; and the largest relative leaf-energy
+    discrepancy within DE_REL_MULT x the calibration's (floor 1e-7, a few float32 ulps)."""
+    if "draw_drift" not in dev:
+        bound_draws(dev, cal)
+    if "draw_drift" not in cal:
+        bound_draws(cal, cal)  # the calibration's own draws are the rounding drift (ratio 1)
     a, b = counts(dev), counts(cal)
     slack = max(4, dev["chains"] // 10) if slack is None else slack
-    msg = (f"device {a} (max dE err {dev['max_dE_err']:.3g}) vs rounding calibration {b} "
-           f"(max dE err {cal['max_dE_err']:.3g})")
-    ok = (a["unexplained"] == 0 and a["matched"] >= b["matched"] - slack
-          and dev["max_dE_err"] <= 10.0 * max(cal["max_dE_err"], 1e-3))
+    g = dev["draw_drift"]["geo_mean_ratio"]
+    rel_ok = dev["max_dE_rel"] <= DE_REL_MULT * max(cal["max_dE_rel"], 1e-7)
+    msg = (f"device {a} (max dE err {dev['max_dE_err']:.3g}, relative {dev['max_dE_rel']:.3g}) vs rounding "
+           f"calibration {b} (max dE err {cal['max_dE_err']:.3g}, relative {cal['max_dE_rel']:.3g}); paired drift "
+           f"{dev['draw_drift']['pairs']} transitions, geometric-mean ratio "
+           f"{'n/a' if g is None else format(g, '.3g')}, median {dev['draw_drift']['median_dev']} vs "
+           f"{dev['draw_drift']['median_cal']} tolerance units")
+    ok = (a["unexplained"] == 0 and a["matched"] >= b["matched"] - slack and rel_ok
+          and (g is None or g <= DRIFT_GEO_MAX))
     return ok, msg

@@ -49,8 +49,8 @@ class LogisticRegression:
     def pe_grad_batch(self, Z):
         """Z [C, D] -> (pe [C], grad [C, D]) in float64."""
         Z = np.asarray(Z, np.float64)
-        X = self.X.astype(np.float64)
-        y = self.y.astype(np.float64)
+        X = np.asarray(self.X, np.float64)  # no copy when the potential holds float64 data
+        y = np.asarray(self.y, np.float64)
         L = X @ Z.T  # [N, C]
         bce = np.maximum(L, 0) + np.log1p(np.exp(-np.abs(L))) - L * y[:, None]
         pe = bce.sum(0) + 0.5 * (Z * Z).sum(1) + self.dim * 0.5 * LOG_2PI

@@ -61,10 +61,12 @@ def test_batched_chains_are_the_oracle_chains():
 
 def test_fixed_batch_mode_and_path_comparison():
     """run_chains(deadline=...) keeps every chain running until the deadline (the CPU
-    comparator's fixed batch); record=True returns each transition's decisions, and
-    compare_paths reports a chain whose tree sizes or draws leave the reference's with the
-    closest decision to a tie."""
+    comparator's fixed batch) and at least `min_transitions`; record=True returns each
+    transition's decisions and leaf records, and compare_traced reports a chain whose tree sizes
+    or draws leave the reference's."""
     import time
+
+    from oracle import parity as PR
 
     X, y = _data(N=200, D=5, seed=3)
     ref = OP.LogisticRegression(X, y, dtype=np.float32)
@@ -83,12 +85,20 @@ def test_fixed_batch_mode_and_path_comparison():
     st, log, leaves = hist[0][0]
     assert isinstance(log, list) and all(k in H.TIE for k, _ in log)
     assert len(leaves) == st.num_steps and leaves[-1]["iter_done"]
+    states, oracles = mk()
+    _, h3, _, _ = CB.run_chains(rowwise, states, oracles, 1 << 30, deadline=time.perf_counter(), min_transitions=3)
+    assert all(len(h) == 3 for h in h3)
     T = min(len(h) for h in hist)
+    tr = np.full((T, n, 1024, 8), np.nan, np.float32)
+    for c, h in enumerate(hist):
+        for t in range(T):
+            tr[t, c] = PR.oracle_to_trace(h[t][2], 1024)
     ns = np.array([[h[t][0].num_steps for t in range(T)] for h in hist])
     zs = np.array([[h[t][0].z for t in range(T)] for h in hist], np.float64)
-    par = CB.compare_paths(hist, ns, zs, atol=0.0)
+    par = PR.compare_traced(hist, tr, ns, zs, atol=0.0)
     assert par["matched"] == n and par["transitions"] == n * T and not par["mismatches"]
-    ns_bad = ns.copy()
-    ns_bad[1, 1] += 1
-    par = CB.compare_paths(hist, ns_bad, zs, atol=0.0)
-    assert par["matched"] == n - 1 and par["mismatches"][0][:2] == (1, 1)
+    zs_bad = zs.copy()
+    zs_bad[1, 1, 0] += 1e-3
+    par = PR.compare_traced(hist, tr, ns, zs_bad, atol=0.0)
+    assert par["matched"] == n - 1 and (par["mismatches"][0]["chain"], par["mismatches"][0]["transition"]) == (1, 1)
+    assert par["mismatches"][0]["kind"] == "draw" and not par["mismatches"][0]["explained"]

@@ -18,7 +18,9 @@ from numpyro_amd import native
 from numpyro_amd import potentials as P
 from numpyro_amd.dense import Whitening, WhitenedPotential
 from numpyro_amd.infer import HMC, MCMC, NUTS
+import parity_cases as PC
 from oracle import hmc_ref as H
+from oracle import parity as PR
 from oracle import philox
 from oracle import potentials as OP
 
@@ -631,7 +633,6 @@ def test_per_chain_dense_adaptation_matches_oracle(device, model):
     oracle's dense-mass NUTS (mass_matrix_sqrt @ eps momentum, M^-1 r in the leapfrog and the
     U-turn dots, hmc_util.py:1183-1220) takes the device's next three trees and draws (>= 95%
     of chains, every mismatch at a rounding-level decision tie)."""
-    from test_gpu_nuts import _explain_mismatches, _first_split
 
     seed, C, W, D = 17, 64, 150, 6
     rs = np.random.RandomState(3)
@@ -659,41 +660,27 @@ def test_per_chain_dense_adaptation_matches_oracle(device, model):
             wst = upd(draws[c, t], wst)
         cov_o = fin(wst, regularize=True)[0]
         np.testing.assert_allclose(imm[c], cov_o, rtol=1e-4, atol=1e-7, err_msg=f"chain {c}")
-    # (2) sampling transitions from the post-warmup state
+    # (2) sampling transitions from the post-warmup state (decision trace on)
+    mcmc._engine.set_trace(C, W, 3)
     mcmc.run(seed, *args, extra_fields=("num_steps",))
+    tr = mcmc._engine.trace_records()
     ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
     zs = mcmc.get_samples(True)[site].cpu().numpy()
     z0 = st.z[site].cpu().numpy()
     g0 = st.z_grad.cpu().numpy()
     pe0 = st.potential_energy.cpu().numpy()
     ss = st.adapt_state.step_size.cpu().numpy()
-    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
-                              for v in ref.pe_grad(z))
-    match, mism = 0, []
+    hist = []
     for c in range(C):
-        o = H.NUTSOracle(pe_grad, D, W, step_size=float(ss[c]), adapt_step_size=False, adapt_mass_matrix=False,
-                         dense_mass=True, inverse_mass_matrix=imm[c].astype(np.float32))
+        o = H.NUTSOracle(PC.f32(ref.pe_grad), D, W, step_size=float(ss[c]), adapt_step_size=False,
+                         adapt_mass_matrix=False, dense_mass=True, inverse_mass_matrix=imm[c].astype(np.float32))
         wa = o.wa_init((z0[c],), None, np.float32(ss[c]), inverse_mass_matrix=imm[c].astype(np.float32),
                        mass_matrix_size=D)
         s = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
                        0, np.float32(0), np.float32(0), False, wa, (seed, c))
-        ok, margins = [], []
-        for t in range(3):
-            H.DECISIONS = []
-            try:
-                s = o.sample(s)
-            finally:
-                d, H.DECISIONS = H.DECISIONS, None
-            margins.append(H.closest_decision(d))
-            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
-        t = _first_split(ok)
-        if t < 0:
-            match += 1
-        else:
-            mism.append((c, t, margins[t]))
-    print(f"[per-chain dense {model}] {match}/{C} chains reproduce the oracle's dense-mass transitions")
-    _explain_mismatches(mism, f"per-chain dense {model}")
-    assert match >= int(0.95 * C)
+        hist.append(PC.traced(o, s, 3))
+    par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
+    PC.report(par, f"per-chain dense {model}", frac=0.95)
 
 
 def test_structured_dense_mass_matches_oracle(device):
@@ -707,7 +694,6 @@ def test_structured_dense_mass_matches_oracle(device):
     momentum and kinetic energy are the reference's per-block ones) takes the device's next three
     trees and draws for >= 90% of chains, every mismatch at a rounding-level tie."""
     from numpyro_amd import datasets
-    from test_gpu_nuts import _explain_mismatches, _first_split
 
     seed, C, W, D = 23, 64, 150, 10
     args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
@@ -740,17 +726,17 @@ def test_structured_dense_mass_matches_oracle(device):
         np.testing.assert_allclose(dense_b[c], fin_d(sd, regularize=True)[0], rtol=1e-4, atol=1e-7,
                                    err_msg=f"chain {c} dense block")
         np.testing.assert_allclose(diag_b[c], fin_g(sg, regularize=True)[0], rtol=1e-5, err_msg=f"chain {c} tau")
-    # (2) sampling transitions from the post-warmup state
+    # (2) sampling transitions from the post-warmup state (decision trace on)
+    eng.set_trace(C, W, 3)
     mcmc.run(seed, *args, extra_fields=("num_steps",))
+    tr = eng.trace_records()
     ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
     zs = flat(mcmc.get_samples(True))
     z0 = torch.cat([st.z["mu"][:, None], st.z["tau"][:, None], st.z["theta"]], 1).cpu().numpy()
     g0, pe0 = st.z_grad.cpu().numpy(), st.potential_energy.cpu().numpy()
     ss = st.adapt_state.step_size.cpu().numpy()
     ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
-    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
-                              for v in ref.pe_grad(z))
-    match, mism = 0, []
+    hist = []
     for c in range(C):
         imm_f = np.zeros((D, D), np.float32)
         msq_f = np.zeros((D, D), np.float32)
@@ -759,29 +745,15 @@ def test_structured_dense_mass_matches_oracle(device):
         msq_f[np.ix_(order, order)] = sq_b
         i_t, sq_t, _ = H._initialize_mass_matrix(1, diag_b[c].astype(np.float32), False)
         imm_f[1, 1], msq_f[1, 1] = i_t[0], sq_t[0]
-        o = H.NUTSOracle(pe_grad, D, W, step_size=float(ss[c]), adapt_step_size=False, adapt_mass_matrix=False,
-                         dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32))
+        o = H.NUTSOracle(PC.f32(ref.pe_grad), D, W, step_size=float(ss[c]), adapt_step_size=False,
+                         adapt_mass_matrix=False, dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32))
         wa = o.wa_init((z0[c],), None, np.float32(ss[c]), inverse_mass_matrix=np.eye(D, dtype=np.float32),
                        mass_matrix_size=D)._replace(inverse_mass_matrix=imm_f, mass_matrix_sqrt=msq_f)
         s = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
                        0, np.float32(0), np.float32(0), False, wa, (seed, c))
-        ok, margins = [], []
-        for t in range(3):
-            H.DECISIONS = []
-            try:
-                s = o.sample(s)
-            finally:
-                d, H.DECISIONS = H.DECISIONS, None
-            margins.append(H.closest_decision(d))
-            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
-        t = _first_split(ok)
-        if t < 0:
-            match += 1
-        else:
-            mism.append((c, t, margins[t]))
-    print(f"[structured dense eight schools] {match}/{C} chains reproduce the oracle's block-mass transitions")
-    _explain_mismatches(mism, "structured dense eight schools")
-    assert match >= int(0.9 * C)
+        hist.append(PC.traced(o, s, 3))
+    par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
+    PC.report(par, "structured dense eight schools", frac=0.9)
 
 
 def _dense_wide_run(monkeypatch, rows_step, C=96, sync=False, chain_offset=None, W=20, S=4, seed=5, fixed=False):
@@ -837,8 +809,6 @@ def test_inverse_mass_matrix_dict_of_blocks_matches_oracle(device):
     group; the oracle's dense-mass NUTS with the blocks scattered into full matrices (momentum from
     each block's own factor) takes the device's trees and draws at a fixed step size."""
     from numpyro_amd import datasets
-    from oracle import philox
-    from test_gpu_nuts import _explain_mismatches, _first_split
 
     seed, C, T, D = 29, 32, 3, 10
     args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
@@ -849,7 +819,11 @@ def test_inverse_mass_matrix_dict_of_blocks_matches_oracle(device):
     mcmc = MCMC(NUTS(P.eight_schools, dense_mass=[("theta", "mu")], inverse_mass_matrix=imm, adapt_mass_matrix=False,
                      step_size=0.1, adapt_step_size=False), num_warmup=0, num_samples=T, num_chains=C,
                 postprocess_fn=lambda z: z)
+    eng = mcmc._get_engine(args, {})
+    eng.set_trace(C, 0, T)
     mcmc.run(seed, *args, extra_fields=("num_steps",))
+    assert mcmc._engine is eng
+    tr = eng.trace_records()
     st = mcmc.last_state.adapt_state.inverse_mass_matrix
     np.testing.assert_allclose(st[("theta", "mu")][0].cpu().numpy(), blk, rtol=1e-6)
     np.testing.assert_allclose(st[("tau",)][0].cpu().numpy(), [0.5], rtol=1e-6)
@@ -865,28 +839,12 @@ def test_inverse_mass_matrix_dict_of_blocks_matches_oracle(device):
     i_t, sq_t, _ = H._initialize_mass_matrix(1, np.array([0.5], np.float32), False)
     imm_f[1, 1], msq_f[1, 1] = i_t[0], sq_t[0]
     ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
-    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
-                              for v in ref.pe_grad(z))
-    match, mism = 0, []
+    hist = []
     for c in range(C):
-        o = H.NUTSOracle(pe_grad, D, 0, step_size=0.1, adapt_step_size=False, adapt_mass_matrix=False,
+        o = H.NUTSOracle(PC.f32(ref.pe_grad), D, 0, step_size=0.1, adapt_step_size=False, adapt_mass_matrix=False,
                          dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32))
         s = o.init(philox.init_uniform(seed, c, 0, D), seed, c)
         s = s._replace(adapt_state=s.adapt_state._replace(inverse_mass_matrix=imm_f, mass_matrix_sqrt=msq_f))
-        ok, margins = [], []
-        for t in range(T):
-            H.DECISIONS = []
-            try:
-                s = o.sample(s)
-            finally:
-                d, H.DECISIONS = H.DECISIONS, None
-            margins.append(H.closest_decision(d))
-            ok.append(s.num_steps == ns_dev[c, t] and np.allclose(zs[c, t], s.z, rtol=1e-3, atol=1e-3))
-        t = _first_split(ok)
-        if t < 0:
-            match += 1
-        else:
-            mism.append((c, t, margins[t]))
-    print(f"[inverse_mass_matrix dict] {match}/{C} chains reproduce the oracle's block-mass transitions")
-    _explain_mismatches(mism, "inverse_mass_matrix dict")
-    assert match >= int(0.9 * C)
+        hist.append(PC.traced(o, s, T))
+    par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
+    PC.report(par, "inverse_mass_matrix dict", frac=0.9)

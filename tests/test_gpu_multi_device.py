@@ -90,3 +90,30 @@ def test_parallel_pooled_dense_equals_torchrun(device, tmp_path):
     one_x, one_n = pooled_run(None)  # one engine pools in one GEMM: equal to rounding, not bitwise
     print(f"[pooled] one engine vs two: {float((one_x.cpu() - x2.cpu()).abs().max()):.2e} max |dx|, "
           f"{int((one_n.cpu() == n2.cpu()).sum())}/{n2.numel()} equal tree sizes")
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two distinct GPUs (the one-GPU box rehearses with two engines on cuda:0)")
+@pytest.mark.parametrize("model", ["logreg", "bnn_dense"])
+def test_parallel_two_distinct_devices(device, model):
+    """MCMC(devices=["cuda:0", "cuda:1"]) on two distinct GPUs: per-thread device contexts, the
+    per-device dynamic-LDS attribute of the big whitening tile (nmx_lds_limit: k_gemm_x3's 144 KB
+    and k_bnn's 79 KB must be raised on each device) and the peer copies of the pooled moments.
+    Diagonal mass draws bitwise what one engine draws; pooled dense equals the two-engines-on-one-
+    GPU rehearsal bitwise (same shards, same rank-order sums)."""
+    if model == "logreg":
+        X, y = datasets.covtype_synthetic(n_rows=4000, seed=1)
+        one, _ = _run(P.logistic_regression, (X, y), 100, None, chain_method="vectorized")
+        two, _ = _run(P.logistic_regression, (X, y), 100, ["cuda:0", "cuda:1"])
+        assert {str(e.device) for e in two._engines} == {"cuda:0", "cuda:1"}
+        for k, v in one.get_samples(True).items():
+            assert torch.equal(v.cpu(), two.get_samples(True)[k].cpu()), k
+        return
+    Xb, Yb = datasets.bnn_data(N=100, D_X=3)
+    runs = []
+    for devs in (["cuda:0", "cuda:0"], ["cuda:0", "cuda:1"]):
+        mcmc = MCMC(NUTS(P.bnn, dense_mass="pooled", max_tree_depth=5), num_warmup=30, num_samples=3,
+                    num_chains=64, devices=devs, progress_bar=False, postprocess_fn=lambda z: z)
+        mcmc.run(4, Xb, Yb, 69, extra_fields=("num_steps",))
+        runs.append((mcmc.get_samples(True)["w2"].cpu(), mcmc.get_extra_fields(True)["num_steps"].cpu()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])

@@ -13,16 +13,17 @@ import torch
 from numpyro_amd import datasets, native
 from numpyro_amd import potentials as P
 from numpyro_amd.infer import HMC, MCMC, NUTS
+import parity_cases as PC
 from oracle import hmc_ref as H
+from oracle import parity as PR
 from oracle import philox
 from oracle import potentials as OP
 
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS", z0=None, margins=None, **kw):
-    """Oracle states of one chain; with `margins` (a list) also the smallest decision margin
-    of every transition (kind, margin), see oracle.hmc_ref.DECISIONS."""
+def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS", z0=None, **kw):
+    """Oracle states of one chain."""
     o = H.NUTSOracle(lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)
                                      for v in pe_grad(z)),
                      dim, num_warmup, algo=algo, **kw)
@@ -31,43 +32,9 @@ def _oracle_chain(pe_grad, dim, seed, chain, num_warmup, num_iters, algo="NUTS",
     s = o.init(z0, seed, chain)
     out = []
     for _ in range(num_iters):
-        if margins is not None:
-            H.DECISIONS = []
-        try:
-            s = o.sample(s)
-        finally:
-            if margins is not None:
-                d, H.DECISIONS = H.DECISIONS, None
-                margins.append(H.closest_decision(d))
+        s = o.sample(s)
         out.append(s)
     return out
-
-
-TIE = H.TIE  # rounding-level tie bounds of each decision kind (oracle/hmc_ref.py)
-
-
-def _first_split(ok_per_transition):
-    bad = np.flatnonzero(~np.asarray(ok_per_transition))
-    return int(bad[0]) if bad.size else -1
-
-
-def _explain_mismatches(mism, label, energy_noise=0.0):
-    """mism: list of (chain, first differing transition, (kind, margin) of that transition's
-    closest decision).  Every mismatch must start at a rounding-level tie.  `energy_noise`:
-    the largest |U_device - U_oracle| seen at the draws of the transitions both took
-    identically.  A transition / accept probability is a sigmoid or min(1, exp) (slope <= 1) of
-    a difference of two subtree weights, each a logaddexp over that subtree's leaf energies, so
-    it moves between the two by up to twice the largest leaf-energy discrepancy; the draws
-    sample the leaves, so that discrepancy is taken as 2 x the largest one seen at a draw (the
-    bound is 4 x energy_noise)."""
-    bound = dict(TIE)
-    for k in ("transition", "accept"):
-        bound[k] = max(bound[k], 4.0 * energy_noise)
-    for c, t, (kind, m) in mism:
-        print(f"[{label}] chain {c}: first difference at transition {t}, closest decision {kind} "
-              f"margin {m:.3g} (tie bound {bound.get(kind, 0):.1e})")
-    unexplained = [(c, t, k, m) for c, t, (k, m) in mism if not (k in bound and m <= bound[k])]
-    assert not unexplained, f"[{label}] mismatches not at a rounding tie: {unexplained}"
 
 
 def _run_engine(model_args, model, num_chains, num_warmup, num_samples, seed, kernel_cls=NUTS,
@@ -123,39 +90,7 @@ def test_engine_matches_oracle_eight_schools(device, algo):
     assert match >= int(0.9 * C), f"only {match}/{C} chains reproduced the oracle path"
 
 
-def _fixed_step_case(model, dim, rs):
-    """(model args, fused model, oracle, checked site, oracle-z extractor, step, min match,
-    shared initial points or None for init_to_uniform)."""
-    if model == "logreg":
-        X = rs.randn(300, dim).astype(np.float32)
-        beta = rs.randn(dim) * 0.5 / np.sqrt(dim)
-        y = (rs.rand(300) < 1 / (1 + np.exp(-X @ beta))).astype(np.float32)
-        return (X, y), P.logistic_regression, OP.LogisticRegression(X, y, dtype=np.float32), "coefs", \
-            (lambda z: z), 0.02, 0.95, None
-    if model == "diag_normal":
-        mu = rs.randn(dim).astype(np.float32)
-        sd = (0.5 + rs.rand(dim)).astype(np.float32)
-        return (mu, sd), P.diag_normal, OP.IsoNormal(mu, sd, dtype=np.float32), "x", (lambda z: z), 0.05, 0.95, None
-    if model == "funnel":
-        return (dim,), P.funnel, OP.Funnel(dim, dtype=np.float32), "x", (lambda z: z[..., :-1]), 0.05, 0.9, None
-    if model == "sv":
-        r = datasets.sp500_synthetic(T=dim - 2)
-        return (r,), P.stochastic_volatility, OP.StochasticVolatility(r, dtype=np.float32), "s", \
-            (lambda z: z[..., 1:-1]), 0.005, 0.9, None
-    if model == "bnn":
-        # D = 5038 is BASELINE config 3 (examples/bnn.py: D_X = 3, N = 100, H = 69)
-        H = {46: 5, 321: 16, 5038: 69}[dim]
-        X, Y = datasets.bnn_data(N=100 if H == 69 else 30, D_X=3)
-        o = 1 + 3 * H
-        # shared well-conditioned start (small weights, prec ~ e): from U(-2, 2) the tanh
-        # layers saturate and |U| ~ 1e3, where fp32 energy rounding flips leaf choices; the
-        # hidden-to-hidden weights scale with 1/sqrt(H) so the second layer stays unsaturated
-        z0 = (0.3 * rs.randn(64, dim)).astype(np.float32)
-        z0[:, o:] *= np.float32(min(1.0, np.sqrt(5.0 / H)))
-        z0[:, 0] = 1.0
-        return (X, Y, H), P.bnn, OP.BNN(X, Y, H, dtype=np.float32), "w2", \
-            (lambda z: z[..., o:o + H * H]), 0.01, 0.9, z0
-    raise ValueError(model)
+_fixed_step_case = PC.fixed_step_case
 
 
 @pytest.mark.parametrize("algo", ["NUTS", "HMC"])
@@ -163,60 +98,50 @@ def _fixed_step_case(model, dim, rs):
                                        ("diag_normal", 1500), ("funnel", 600), ("sv", 302),
                                        ("bnn", 46), ("bnn", 321), ("bnn", 5038)])
 def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
-    """No adaptation, fixed step size: every transition is a deterministic function of
-    the Philox stream; device and oracle must take the same discrete path.  D < 257 runs the
-    fused step kernel (dim 40, 46: 8 waves per 64 chains), D >= 257 the wide D-split
-    schedule.  Funnel, SV and BNN check the fused potentials inside full trajectories; their
-    stiffer geometry lets fp32 rounding flip a few more decisions (>= 90% of chains)."""
+    """No adaptation, fixed step size: every transition is a deterministic function of the
+    Philox stream, so device and oracle take the same discrete path up to rounding.  D < 257
+    runs the fused step kernel (dim 4, 40, 46), SV / funnel / diagonal normal the persistent wide
+    kernel, the BNN the launched D-slice schedule.  Leaf-located (oracle/parity.py, the device's
+    decision trace): the reference is the oracle with the potential in rounded float64; a chain
+    that parts must do so at a leaf whose decision is a rounding flip of that leaf (HMC: the
+    Metropolis decision), and a draw that differs with every decision equal must lie within
+    DRAW_MULT x the drift of the rounding calibration (a second float32 potential against the
+    same reference) -- tests/parity_cases.py."""
     seed, C, T = 77, 64, 3
-    rs = np.random.RandomState(dim)
-    args, fm, ref, site, extract, step, frac, z0 = _fixed_step_case(model, dim, rs)
     if model == "bnn":
-        # BNN trees run 255-511 leapfrogs: tree sizes agree for every chain over 3
-        # transitions, but fp32 rounding grows along ~1000 chaotic leapfrogs, so the draws
-        # are compared over the first two (scripts/debug_bnn_parity.py prints the growth)
-        T = 2
-    kcls = NUTS if algo == "NUTS" else HMC
-    kw = dict(step_size=step, adapt_step_size=False, adapt_mass_matrix=False)
-    if algo == "HMC":
-        kw["trajectory_length"] = 15 * step
-    mcmc, warm = _run_engine(args, fm, C, 0, T, seed, kernel_cls=kcls,
-                             init_params=None if z0 is None else torch.from_numpy(z0), **kw)
-    ns_dev, sites = _dev_paths(mcmc, warm)
-    pe_dev = mcmc.get_extra_fields(True)["potential_energy"].cpu().numpy()
-    match, mism, du = 0, [], 0.0
-    tol = dict(rtol=1e-3, atol=1e-3 if frac < 0.95 else 1e-4)
+        T = 2  # BNN trees run 255-511 leapfrogs of a tanh network
+    extra = {"trajectory_length": 15 * PC.fixed_step_case(model, dim, np.random.RandomState(dim))[5]} \
+        if algo == "HMC" else {}
+    eng, ref, step, frac, z0, ns, z, _, _ = PC.engine_fixed(model, dim, C, T, seed, C, algo=algo, **extra)
+    tr = eng.trace_records()
+    kw = dict(algo=algo, **extra)
+    hist = PC.oracle_runs(PC.reference_f64(model, ref), dim, C, T, seed, step, z0, **kw)
+    constrain = PC.constrain_fn(eng)
+    tol = dict(atol=1e-3, rtol=1e-3) if frac < 0.95 else dict(atol=1e-4, rtol=1e-3)
+    par = PR.compare_traced(hist, tr, ns, z, to_model=constrain, **tol)
+    ctr, cns, cz = PC.as_trace(PC.oracle_runs(PC.second_f32(model, dim, ref), dim, C, T, seed, step, z0, **kw))
+    cal = PR.compare_traced(hist, ctr, cns, np.stack([[constrain(w) for w in cc] for cc in cz]), to_model=constrain,
+                            **tol)
+    PC.report(par, f"fixed-step {algo} {model} D={dim}", cal=cal, frac=frac)
+    # the trace's layout: a NUTS transition records every leaf of its tree, the last one ends it;
+    # an HMC transition records its Metropolis decision as leaf 0
     for c in range(C):
-        margins = []
-        states = _oracle_chain(ref.pe_grad, dim, seed, c, 0, T, algo=algo,
-                               z0=None if z0 is None else z0[c], margins=margins, **kw)
-        ns = np.array([s.num_steps for s in states])
-        z = extract(np.stack([s.z for s in states]))
-        got = sites[site][c].reshape(z.shape)
-        # a chain is reproduced when its discrete path (tree sizes) AND its draws agree
-        # (a rounding flip in a leaf weight can change the proposal inside an equal-size tree)
-        ok = [ns[t] == ns_dev[c, t] and np.allclose(got[t], z[t], **tol) for t in range(T)]
-        t = _first_split(ok)
-        for tt in range(T if t < 0 else t):
-            du = max(du, abs(float(pe_dev[c, tt]) - float(states[tt].potential_energy)))
-        if t < 0:
-            match += 1
-        else:
-            mism.append((c, t, margins[t]))
-    print(f"[fixed-step {algo} {model} D={dim}] {match}/{C} chains reproduce the oracle path and draws "
-          f"(max |U_dev - U_oracle| on identical transitions {du:.2e})")
-    _explain_mismatches(mism, f"{algo} {model} D={dim}", energy_noise=du)
-    assert match >= int(frac * C), f"only {match}/{C} chains reproduced the oracle path and draws"
+        for t in range(T):
+            n = int(ns[c, t]) if algo == "NUTS" else 1
+            assert np.all(np.isfinite(tr[t, c, :n, PR.T_FLAGS])) and np.all(np.isnan(tr[t, c, n:, PR.T_FLAGS]))
+            assert int(tr[t, c, n - 1, PR.T_FLAGS]) & PR.TF_ITER_DONE
 
 
 def test_covtype_full_size_nuts_matches_oracle(device):
     """BASELINE config 1 at its full data size (581012 x 55, synthetic covtype): after a device
-    warmup, 8 chains run 2 sampling transitions on the GPU; the oracle's NUTS resumes the same
-    chains from the device's post-warmup state on the same Philox stream, with its potential
-    evaluated by the C restatement over the full data (oracle/c/logreg_batch.c).  Tree sizes
-    must agree and draws to 1e-4 (posterior sd ~3e-3 at this N) for >= 7 of 8 chains, and a
-    chain that leaves the device's path must do so at a rounding-level tie
-    (hmc_util.py:1088-1180 build_tree, examples/covtype.py:66-71)."""
+    warmup, 8 chains run 2 traced sampling transitions on the GPU; the oracle's NUTS resumes the
+    same chains from the device's post-warmup state on the same Philox stream.  Reference: the
+    potential in rounded float64 over the full data (oracle/potentials.py pe_grad_batch);
+    calibration: the float32 C restatement (oracle/c/logreg_batch.c) against it.  Tree sizes
+    must agree and draws to 1e-4 (posterior sd ~3e-3 at this N) for >= 7 of 8 chains; a chain
+    that parts must do so at a leaf whose decision is a rounding flip of that leaf, a draw with
+    every decision equal within DRAW_MULT x the calibration's drift (hmc_util.py:1088-1180
+    build_tree, examples/covtype.py:66-71)."""
     from numpyro_amd.random import key_to_seed
     from oracle import cpu_batched as CB
 
@@ -227,21 +152,29 @@ def test_covtype_full_size_nuts_matches_oracle(device):
     mcmc = MCMC(NUTS(P.logistic_regression), num_warmup=W, num_samples=T, num_chains=C)
     mcmc.warmup(seed, Xd, yd)
     st = mcmc.post_warmup_state
-    mcmc.run(seed + 1, Xd, yd, extra_fields=("num_steps", "potential_energy"))
+    mcmc._engine.set_trace(C, W, T)
+    mcmc.run(seed + 1, Xd, yd, extra_fields=("num_steps",))
+    tr = mcmc._engine.trace_records()
+    mcmc._engine.set_trace(0, 0, 0)
     ns = mcmc.get_extra_fields(group_by_chain=True)["num_steps"].cpu().numpy()
-    pe = mcmc.get_extra_fields(group_by_chain=True)["potential_energy"].to(torch.float64).cpu().numpy()
     z = mcmc.get_samples(group_by_chain=True)["coefs"].to(torch.float64).cpu().numpy()
     cols = lambda t: t.detach().cpu().numpy()  # noqa: E731
-    states, oracles = CB.chains_from_state(
-        cols(st.z["coefs"]), cols(st.z_grad), cols(st.potential_energy), cols(st.adapt_state.step_size),
-        cols(st.adapt_state.inverse_mass_matrix), cols(st.adapt_state.mass_matrix_sqrt), W, key_to_seed(seed + 1), W)
-    _, hist, evals, _ = CB.run_chains(CB.LogRegBatch(X, y), states, oracles, T, record=True)
-    par = CB.compare_paths(hist, ns, z, atol=1e-4, dev_pe=pe)
-    print(f"[covtype 581012x55] {par['matched']}/{C} chains reproduce the device's {T} transitions "
-          f"({evals} oracle leapfrogs; max |dz| on matched paths {par['max_abs_dz']:.2e}, "
-          f"|U_dev - U_oracle| {par['energy_noise']:.2e})")
-    _explain_mismatches([(c, t, (k, m)) for c, t, k, m, _ in par["mismatches"]], "covtype full size",
-                        energy_noise=par["energy_noise"])
+
+    def resume():
+        return CB.chains_from_state(
+            cols(st.z["coefs"]), cols(st.z_grad), cols(st.potential_energy), cols(st.adapt_state.step_size),
+            cols(st.adapt_state.inverse_mass_matrix), cols(st.adapt_state.mass_matrix_sqrt), W, key_to_seed(seed + 1),
+            W)
+
+    r64 = OP.LogisticRegression(X.astype(np.float64), y.astype(np.float64), dtype=np.float64)
+    f64 = lambda Z: tuple(np.asarray(v, np.float32) for v in r64.pe_grad_batch(Z))  # noqa: E731
+    _, hist, evals, _ = CB.run_chains(f64, *resume(), T, record=True)
+    _, hist32, _, _ = CB.run_chains(CB.LogRegBatch(X, y), *resume(), T, record=True)
+    par = PR.compare_traced(hist, tr, ns, z, atol=1e-4)
+    ctr, cns, cz = PC.as_trace(hist32)
+    cal = PR.compare_traced(hist, ctr, cns, cz, atol=1e-4)
+    print(f"[covtype 581012x55] {evals} oracle leapfrogs per side")
+    PC.report(par, "covtype full size", cal=cal)
     assert par["matched"] >= C - 1
 
 
@@ -255,9 +188,15 @@ def _device_adapt_run(model, dim, C, seed, W):
     eng.initialize(seed, W)
     ends = [e + 1 for _, e in H.build_adaptation_schedule(W)]
     cols = {k: native.COLLECT.index(k) for k in ("step_size", "accept_prob", "num_steps")}
-    fl, zs, snaps = {k: [] for k in cols}, [], {}
+    fl, zs, snaps, traces = {k: [] for k in cols}, [], {}, {}
     for e in ends:
+        it0 = eng.iteration
+        if it0 in ends:  # the oracle restarts from this window end: trace its next 3 transitions
+            eng.set_trace(C, it0, 3)
         samples, fields, _ = eng.run(e - eng.iteration, seed)
+        if it0 in ends:
+            traces[it0] = eng.trace_records()
+            eng.set_trace(0, 0, 0)
         for k, i in cols.items():
             fl[k].append(fields[:, i, :C].cpu().numpy())
         zs.append(samples[:, :, :C].cpu().numpy())
@@ -266,7 +205,7 @@ def _device_adapt_run(model, dim, C, seed, W):
             "da_xt", "da_xavg", "da_gavg", "da_t", "da_prox", "window_idx", "mean_acc", "iter")}
     out = {k: np.concatenate(v).T for k, v in fl.items()}
     out["num_steps"] = out["num_steps"].round().astype(int)
-    return ref, out, np.concatenate(zs).transpose(2, 0, 1), snaps, ends
+    return ref, out, np.concatenate(zs).transpose(2, 0, 1), snaps, ends, traces
 
 
 @pytest.mark.parametrize("model,dim,C", [("diag_normal", 300, 64), ("logreg", 55, 64)])
@@ -289,7 +228,7 @@ def test_adaptation_matches_oracle(device, model, dim, C):
        (~1e-5) grows to 2e-4 step-size differences within 10 transitions even when every tree
        size agrees (measured; DESIGN.md "Adaptation parity")."""
     seed, W = 2024, 300
-    ref, dev, draws, snaps, ends = _device_adapt_run(model, dim, C, seed, W)
+    ref, dev, draws, snaps, ends, traces = _device_adapt_run(model, dim, C, seed, W)
     assert ends == [75, 100, 150, 250, 300]
     # 1. teacher-forced adapter
     wa_init, wa_update = H.warmup_adapter(W)
@@ -308,15 +247,15 @@ def test_adaptation_matches_oracle(device, model, dim, C):
                                                               st.inverse_mass_matrix - 1))))
                 assert int(snaps[t + 1]["window_idx"][c]) == st.window_idx
     print(f"[adapt {model} D={dim}] teacher-forced: max rel diff step size {worst_ss:.2e}, inverse mass {worst_imm:.2e}")
-    # 2. oracle restarts from the device state at each window end
+    # 2. oracle restarts from the device state at each window end, leaf-located against the
+    # device's decision trace of those transitions
     K = 3
-    match, mism, total, drift = 0, [], 0, 0.0
+    match, total, drift = 0, 0, 0.0
     for e in ends[:-1]:
         sn = snaps[e]
+        hist = []
         for c in range(C):
-            total += 1
-            o = H.NUTSOracle(lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)
-                                             for v in ref.pe_grad(z)), dim, W)
+            o = H.NUTSOracle(PC.f32(ref.pe_grad), dim, W)
             imm = sn["inv_mass"][c].astype(np.float32)
             wa = H.HMCAdaptState(
                 np.float32(sn["step_size"][c]), imm, sn["mass_sqrt"][c].astype(np.float32), np.sqrt(imm),
@@ -328,7 +267,7 @@ def test_adaptation_matches_oracle(device, model, dim, C):
             st = H.HMCState(e, sn["z"][c].astype(np.float32), sn["zgrad"][c].astype(np.float32),
                             np.float32(sn["pe"][c]), None, None, None, 0, np.float32(0),
                             np.float32(sn["mean_acc"][c]), False, wa, (seed, c))
-            ok, margins = [], []
+            h = []
             for k in range(K):
                 if k > 0:
                     # the step size the device adapted to (teacher-forced): dual averaging
@@ -338,26 +277,19 @@ def test_adaptation_matches_oracle(device, model, dim, C):
                     # check above the adapter
                     st = st._replace(adapt_state=st.adapt_state._replace(
                         step_size=np.float32(dev["step_size"][c, e + k - 1])))
-                H.DECISIONS = []
-                try:
-                    st = o.sample(st)
-                finally:
-                    d, H.DECISIONS = H.DECISIONS, None
-                margins.append(H.closest_decision(d))
-                t = e + k
-                ok.append(st.num_steps == dev["num_steps"][c, t]
-                          and np.isclose(dev["step_size"][c, t], st.adapt_state.step_size, rtol=1e-3, atol=0)
-                          and np.allclose(draws[c, t], st.z, rtol=1e-3, atol=1e-3))
-                drift = max(drift, abs(float(dev["step_size"][c, t]) / float(st.adapt_state.step_size) - 1))
-            t = _first_split(ok)
-            if t < 0:
-                match += 1
-            else:
-                mism.append((c, e + t, margins[t]))
+                h += PC.traced(o, st, 1)
+                st = h[-1][0]
+                drift = max(drift, abs(float(dev["step_size"][c, e + k]) / float(st.adapt_state.step_size) - 1))
+            hist.append(h)
+        par = PR.compare_traced(hist, traces[e], dev["num_steps"][:, e:e + K], draws[:, e:e + K], atol=1e-3,
+                                rtol=1e-3)
+        PC.report(par, f"adapt {model} D={dim} restart at {e}")
+        match += par["matched"]
+        total += C
     print(f"[adapt {model} D={dim}] restarts at window ends: {match}/{total} chain-windows reproduce "
           f"the next {K} transitions (max step-size rel drift {drift:.1e}: dual averaging restarts at "
           f"t = 0 after a window end, where its gain on accept-probability rounding is largest)")
-    _explain_mismatches(mism, f"adapt {model} D={dim}")
+    assert drift < 1e-2
     assert match >= int(0.95 * total)
 
 

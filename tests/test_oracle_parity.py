@@ -136,3 +136,39 @@ def test_calibration_between_two_float32_implementations():
     assert ok, msg
     bad = dict(par, matched=0, mismatches=par["mismatches"] + [{"kind": "take_leaf", "explained": False}])
     assert not PR.like_calibration(bad, par)[0]
+
+
+def test_draw_mismatch_needs_a_calibration_and_is_bounded_by_it():
+    """A transition whose decisions all agree but whose draw differs (kind `draw`) is explained
+    only by a rounding calibration: within DRAW_MULT x the calibration's drift on that chain and
+    transition.  A corrupted proposal (every decision equal, the draw moved far beyond the drift
+    rounding produces) is reported as unexplained -- with or without a calibration."""
+    rs = np.random.RandomState(4)
+    X = rs.randn(500, 5).astype(np.float32)
+    y = (rs.rand(500) < 0.5).astype(np.float32)
+    r32 = OP.LogisticRegression(X, y, dtype=np.float32)
+    r64 = OP.LogisticRegression(X, y, dtype=np.float64)
+    f64 = lambda z: tuple(np.asarray(v, np.float32) for v in r64.pe_grad(z))  # noqa: E731
+    T, n = 3, 8
+    ref = _run(f64, 5, n, 2, T, 0.1)
+    cal_tr, cal_ns, cal_z = _as_device(_run(r32.pe_grad, 5, n, 2, T, 0.1), T)
+    cal = PR.compare_traced(ref, cal_tr, cal_ns, cal_z, atol=1e-6, rtol=0.0)
+    # the "device": the calibration's own run with one draw corrupted by 1e-2
+    z_bad = cal_z.copy()
+    z_bad[3, 1, 2] += 1e-2
+    par = PR.compare_traced(ref, cal_tr, cal_ns, z_bad, atol=1e-6, rtol=0.0)
+    draws = [m for m in par["mismatches"] if m["kind"] == "draw"]
+    assert any(m["chain"] == 3 and m["transition"] <= 1 for m in draws)
+    assert PR.counts(par)["unexplained"] >= 1  # no calibration: a draw is never explained
+    PR.bound_draws(par, cal)
+    bad = [m for m in par["mismatches"] if m["chain"] == 3]
+    assert bad and not bad[0]["explained"] and bad[0]["ratio"] > PR.DRAW_MULT, bad
+    ok, msg = PR.like_calibration(par, cal)
+    assert not ok, msg
+    # the calibration against itself: every draw mismatch it has is its own drift (ratio 1)
+    same = PR.compare_traced(ref, cal_tr, cal_ns, cal_z, atol=1e-6, rtol=0.0)
+    PR.bound_draws(same, cal)
+    assert all(m["explained"] for m in same["mismatches"] if m["kind"] == "draw")
+    assert same["draw_drift"]["geo_mean_ratio"] == 1.0
+    ok, msg = PR.like_calibration(same, cal)
+    assert ok, msg
