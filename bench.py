@@ -42,8 +42,8 @@ def parse():
     p.add_argument("--design", default="iid", choices=["iid", "structured"],
                    help="synthetic covtype design: iid N(0,1) columns (default) or the real data's structure "
                         "(one-hot groups collinear with the intercept: depth-saturated trees, datasets.covtype_structured)")
-    p.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (headline)")
-    p.add_argument("--config-cpu-seconds", type=float, default=10.0, help="CPU baseline budget per config")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (headline)")
+    p.add_argument("--config-cpu-seconds", type=float, default=8.0, help="CPU baseline budget per config")
     p.add_argument("--cpu-chains", type=int, default=64, help="chains of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
@@ -72,9 +72,10 @@ def _cpu_model():
 def _c_baseline(cn, st, seed, it0, seconds, chain_offset=0, flop=None):
     """Time the C restatement of NUTS (oracle/c/nuts_cpu.c, OpenMP) on `st`'s chains resumed from
     the GPU's state on the GPU's stream, running continuously for `seconds` (every chain starts
-    its next transition at once: a fixed batch); the CPU baseline record."""
+    its next transition at once: a fixed batch; stopped at the deadline, every evaluated leapfrog
+    counted); the CPU baseline record."""
     out = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, it0,
-                 1 << 14, chain_offset=chain_offset, min_transitions=1, seconds=seconds, keep_z=False)
+                 1 << 14, chain_offset=chain_offset, min_transitions=0, seconds=seconds, keep_z=False)
     leap, wall, pot = out["leapfrogs"], out["wall_s"], out["potential_s"]
     rec = {"value": leap / wall, "unit": "leapfrog/s", "cores": cn.threads(), "kind": "port",
            "potential_only": {"value": leap / pot, "unit": "leapfrog/s",
@@ -269,10 +270,10 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
     Parity over the first T timed transitions (T = min(steps, sp["parity_transitions"])): the
     reference is the NumPy oracle (oracle/hmc_ref.py) with the potential in rounded float64
     (oracle/batched.py, float64) from the same states; the device's transitions (decision trace
-    dev_trace) and the C restatement's (float32 potentials in C, its own decision trace: the
-    rounding calibration) are each compared with it (oracle/parity.py): partings located at their
-    leaf, draws with every decision equal bounded by the calibration's drift there, the records
-    compared by like_calibration."""
+    dev_trace), the NumPy oracle with the float32 batched potential (the rounding calibration) and
+    the C restatement (its own decision trace) are each compared with it (oracle/parity.py):
+    partings located at their leaf, draws with every decision equal bounded by the calibration's
+    drift there, the device's record compared with the calibration's by like_calibration."""
     import numpy as np
 
     from oracle import batched as OB
@@ -311,14 +312,31 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
     t64 = time.perf_counter()
     _, hist64, _, _ = CB.run_chains(f64, states, oracles, T, record=True)
     t64 = time.perf_counter() - t64
-    c = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, eng.iteration,
-               T, chain_offset=eng.chain_offset, trace=True)
-    cz = c["z"].astype(np.float64)
+    # rounding calibration: the NumPy oracle with the float32 batched potential (oracle/batched.py),
+    # the same chains and transitions -- the plain float32 implementation the tests calibrate with
+    f32 = sp["cpu"]()
+    if eng.dense:
+        f32 = OB.Whitened(f32, *whiten)
+    states, oracles = CB.chains_from_state(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"],
+                                           st["mass_sqrt"], eng.iteration, seed, eng.num_warmup,
+                                           chain_offset=eng.chain_offset)
+    _, hist32, _, _ = CB.run_chains(f32, states, oracles, T, record=True)
+    L = dev_trace.shape[2]
+    ctr, cns, cz = _oracle_trace(hist32, L)
     if to_model is not None:
         cz = np.stack([[to_model(w) for w in cc] for cc in cz])
-    L = dev_trace.shape[2]
-    cal = PR.compare_traced(hist64, c["trace"][:, :, :L], c["num_steps"], cz, atol=1e-3, rtol=1e-3, to_model=to_model)
+    cal = PR.compare_traced(hist64, ctr, cns, cz, atol=1e-3, rtol=1e-3, to_model=to_model)
     PR.bound_draws(cal, cal)
+    # the C restatement over the same transitions (float32 potentials in C, double reductions in the
+    # sampler): a third implementation, reported beside the calibration
+    c = cn.run(st["z"], st["zgrad"], st["pe"], st["step_size"], st["inv_mass"], st["mass_sqrt"], seed, eng.iteration,
+               T, chain_offset=eng.chain_offset, trace=True)
+    ccz = c["z"].astype(np.float64)
+    if to_model is not None:
+        ccz = np.stack([[to_model(w) for w in cc] for cc in ccz])
+    crec = PR.compare_traced(hist64, c["trace"][:, :, :L], c["num_steps"], ccz, atol=1e-3, rtol=1e-3,
+                             to_model=to_model)
+    PR.bound_draws(crec, cal)
     par = _located_parity(hist64, dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3, rtol=1e-3,
                           to_model=to_model, label=label)
     dev_full = PR.compare_traced(hist64, dev_trace, dev_ns[:k, :T], dev_z[:k, :T], atol=1e-3, rtol=1e-3,
@@ -333,10 +351,14 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
                     f"reference), same chains from the same state on the same Philox stream, first {T} transitions "
                     "per chain; partings located at their leaf; draws with every decision equal bounded by the "
                     f"calibration's drift (DRAW_MULT = {PR.DRAW_MULT})")
-    par["calibration"] = {"basis": "the C restatement (oracle/c/nuts_cpu.c, float32 potentials in C) vs the same "
-                                   "reference, with its own decision trace", **PR.counts(cal),
+    par["calibration"] = {"basis": "the NumPy oracle with the float32 batched potential (oracle/batched.py) vs the "
+                                   "same reference", **PR.counts(cal),
                           "max_dE_err": cal["max_dE_err"], "max_dE_rel": cal["max_dE_rel"],
                           "device_like_calibration": ok}
+    par["c_restatement"] = {"basis": "oracle/c/nuts_cpu.c (float32 potentials in C, its own decision trace) vs the "
+                                     "same reference, its draws bounded by the same calibration", **PR.counts(crec),
+                            "max_dE_rel": crec["max_dE_rel"],
+                            "geo_mean_drift_ratio": crec["draw_drift"]["geo_mean_ratio"]}
     par["draw_drift"] = dev_full["draw_drift"]
     par["max_dE_rel"], par["worst_dE"] = dev_full["max_dE_rel"], dev_full["worst_dE"]
     par["transitions_per_chain"] = T

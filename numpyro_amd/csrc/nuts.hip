@@ -1978,16 +1978,6 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
   return ke0;
 }
 
-// NMX_PX_PROF (kernel experiments, scripts/px_profile.py): thread 0 of every block adds the
-// shader-clock cycles of each phase of its leaves to g_px_prof (nmx_debug_px_profile reads them)
-#ifdef NMX_PX_PROF
-__device__ unsigned long long g_px_prof[16];
-#define PX_T(i) const long long px_t##i = clock64()
-#define PX_ADD(k, a, b) if (threadIdx.x == 0) atomicAdd(&g_px_prof[k], (unsigned long long)(px_t##b - px_t##a))
-#else
-#define PX_T(i)
-#define PX_ADD(k, a, b)
-#endif
 
 // wave-uniform copies of values every lane holds alike (LDS reads look divergent to the
 // compiler; as scalars they stay out of the vector registers)
@@ -2160,7 +2150,6 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     }
     // every wave has read the state before wave 0's scalar logic rewrites it (a leaf's
     // reduction barrier orders this too)
-    PX_T(0);
     if (!A.leaf) __syncthreads();
     if (A.leaf) {
       const float seff = uni_f(Ssh.step_eff);
@@ -2193,11 +2182,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
       }
       if (is_nuts && A.imax > A.imin) persist_ckpt_levels<NW, NT, CARRY>(v, A, m, base, lds, fr);
       if (!CARRY && pl) lds_pre[lane] = pv;
-      PX_T(1);
-      PX_ADD(0, 0, 1);
       __syncthreads();
-      PX_T(2);
-      PX_ADD(1, 1, 2);
       if (wv == 0) {
         // lane e: entry e's total over the waves (in wave order)
         float tot = 0.0f;
@@ -2251,8 +2236,6 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
-    PX_T(3);
-    PX_ADD(2, 0, 3);
     // scalar logic: wave 0 on the LDS state (lane 0 writes back)
     if (wv == 0) {
       ChainScalars S = Ssh;
@@ -2269,10 +2252,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         if (A.fin_done) atomicAdd(&a.counters[0], 1);
       }
     }
-    PX_T(4);
-    PX_ADD(3, 3, 4);
     __syncthreads();  // decisions published
-    PX_T(5);
     const int act = uni_i(sh.act);
     {
       Act D2{};
@@ -2302,16 +2282,8 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         const float t = wave_sum(ke0);
         if (lane == 0) lds_ke[wv] = t;
       }
-      PX_T(6);
-      PX_ADD(4, 5, 6);
       __syncthreads();  // this leaf's rows are written: the next leaf reads its neighbours' positions
-      PX_T(7);
-      PX_ADD(5, 6, 7);
-      PX_ADD(6, 0, 7);
       if (threadIdx.x == 0) {
-#ifdef NMX_PX_PROF
-        atomicAdd(&g_px_prof[7], 1ull);
-#endif
       }
       if (D2.start_iter && tid == 0) {
         float t = 0.0f;
@@ -3156,15 +3128,3 @@ extern "C" int nmx_nuts_run_wide(const nmx_nuts_config* cfg, void* arena, float*
   }
 }
 
-#ifdef NMX_PX_PROF
-// kernel experiments only: the per-phase cycle sums of k_wide_persistent (thread 0 of each block;
-// [0] leaf rows, [1] reduction barrier wait, [2] = leaf rows .. end of the potential's finish,
-// [3] scalar logic, [4] apply rows, [5] end barrier wait, [6] whole leaf, [7] leaves), then reset
-extern "C" int nmx_debug_px_profile(unsigned long long* host16) {
-  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_px_prof), sizeof(unsigned long long) * 16) != hipSuccess)
-    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
-  unsigned long long z[16] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_px_prof), z, sizeof(z)) != hipSuccess) return nmx_fail(NMX_ERR_HIP, "reset");
-  return NMX_OK;
-}
-#endif

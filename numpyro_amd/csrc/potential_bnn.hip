@@ -28,25 +28,6 @@ namespace {
 
 constexpr int THREADS = 512;
 constexpr int NWAVES = THREADS / 64;
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// One 32 x 32 output tile: acc[r] = sum_k A(row, k) B(k, col) over k < K (K steps of 2), with
-// lane l supplying A(l & 31, 2s + (l >> 5)) and B(2s + (l >> 5), l & 31); register r of lane l
-// holds row (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31.
-template <class FA, class FB>
-__device__ __forceinline__ f32x16 mfma_tile(int K, FA fa, FB fb) {
-  const int lane = threadIdx.x & 63, l31 = lane & 31, kh = lane >> 5;
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll 4
-  for (int k0 = 0; k0 < K; k0 += 2) {
-    const int k = k0 + kh;
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa(l31, k), fb(k, l31), acc, 0, 0, 0);
-  }
-  return acc;
-}
-__device__ __forceinline__ int tile_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 
 // One 16 x 16 output tile of v_mfma_f32_16x16x4_f32: lane l supplies A(l & 15, 4s + (l >> 4)) and
 // B(4s + (l >> 4), l & 15); register r of lane l holds row 4 (l >> 4) + r, column l & 15.  The
@@ -66,9 +47,18 @@ __device__ __forceinline__ f32x4 mfma_tile16(int K, FA fa, FB fb) {
   return acc;
 }
 __device__ __forceinline__ int tile_row16(int r) { return 4 * ((threadIdx.x & 63) >> 4) + r; }
-#ifndef NMX_BNN_TILE
-#define NMX_BNN_TILE 16  // 16: v_mfma_f32_16x16x4_f32 tiles; 32: the 32 x 32 x 2 form (A/B)
-#endif
+
+// LDS layout of the H-wide row-major tiles (h1, h2 [N][H], W2 [H][H]; H = 69 for config 3):
+// element (r, c) lives at r H + (c ^ 32 (r & 1)) for c < 64 (columns >= 64 unswizzled).  The MFMA
+// operand reads take two patterns -- 16 rows x 4 consecutive columns (A of h1 W2 and ga2 W2^T,
+// B of ga2 W2^T) and 4 rows x 16 consecutive columns (B of h1 W2, both operands of h1^T ga2) --
+// and no row stride serves both (== 4 or 16 mod 64 banks respectively); at H = 69 (5 mod 64) the
+// second hit up to four lanes per bank.  Flipping column bit 5 on odd rows moves half the rows
+// to the other half of the banks: mean lanes per bank over every operand read of the three
+// products 2.56 -> 1.78, worst 4 -> 2 (exhaustive search over periodic XOR masks of the column,
+// scripts/bnn_swizzle_search.py), no LDS growth (two workgroups per CU kept), results bitwise
+// unchanged (addresses only).
+__device__ __forceinline__ int sw(int r, int c, int H) { return r * H + (c < 64 ? c ^ ((r & 1) << 5) : c); }
 
 struct BnnDims {
   int N, Dx, H;
@@ -133,23 +123,6 @@ __global__ __launch_bounds__(256) void k_rows_to_cols(const float* __restrict__ 
   }
 }
 
-// NMX_BNN_PROF (kernel experiments, scripts/bnn_profile.py): thread 0 of every workgroup adds the
-// shader-clock cycles of each phase to g_bnn_prof (read and reset by nmx_debug_bnn_profile)
-#ifdef NMX_BNN_PROF
-__device__ unsigned long long g_bnn_prof[16];
-#define BNN_T0() long long bnn_t = clock64()
-#define BNN_T(i)                                                                        \
-  do {                                                                                  \
-    if (threadIdx.x == 0) {                                                             \
-      const long long bnn_n = clock64();                                                \
-      atomicAdd(&g_bnn_prof[i], (unsigned long long)(bnn_n - bnn_t));                   \
-      bnn_t = bnn_n;                                                                    \
-    }                                                                                   \
-  } while (0)
-#else
-#define BNN_T0()
-#define BNN_T(i)
-#endif
 
 // zr / gr: the evaluated chains' positions and gradients as rows [position][D].
 __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, const float* __restrict__ Y, BnnDims dm,
@@ -165,9 +138,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   if (pos >= nb) return;
   const int c = nmx_eval_chain(ev, pos);
   if (c < 0) return;
-  const int ldc = ev.ldc;
   const int t = threadIdx.x;
-  BNN_T0();
 
   float* W1 = sm;                  // Dx*H
   float* W2 = W1 + Dx * H;         // H*H
@@ -194,7 +165,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
 #pragma unroll 20
   for (int i = t; i < H * H; i += THREADS) {
     const float v = z[dm.o_w2 + i];
-    W2[i] = v;
+    W2[sw(i / H, i % H, H)] = v;
     wsq += v * v;
   }
   for (int i = t; i < H; i += THREADS) {
@@ -206,52 +177,33 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int i = t; i < N * Dx; i += THREADS) Xs[i] = X[i];
   for (int i = t; i < N; i += THREADS) Ys[i] = Y[i];
   __syncthreads();
-  BNN_T(0);
 
   // h1 = tanh(X W1)
   for (int e = t; e < N * H; e += THREADS) {
     const int n = e / H, j = e % H;
     float a = 0.0f;
     for (int k = 0; k < Dx; ++k) a += Xs[n * Dx + k] * W1[k * H + j];
-    h1[e] = tanhf(a);
+    h1[sw(n, j, H)] = tanhf(a);
   }
   __syncthreads();
-  BNN_T(1);
 
   // h2 = tanh(h1 W2): tiles over (n, j), K = i
-  const int wv = t >> 6, l31 = t & 31;
-#if NMX_BNN_TILE == 16
+  const int wv = t >> 6;
   const int l15 = t & 15;
   const int mtn = (N + 15) / 16, mth = (H + 15) / 16;
   for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
     const int n0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[(n0 + m) * H + k] : 0.0f; },
-        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[k * H + j0 + c] : 0.0f; });
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[sw(n0 + m, k, H)] : 0.0f; },
+        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[sw(k, j0 + c, H)] : 0.0f; });
     const int j = j0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + tile_row16(r);
-      if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
+      if (n < N && j < H) h2[sw(n, j, H)] = tanhf(acc[r]);
     }
   }
-#else
-  const int ntn = (N + 31) / 32, nth = (H + 31) / 32;
-  for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
-    const int n0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
-    const f32x16 acc = mfma_tile(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[(n0 + m) * H + k] : 0.0f; },
-        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[k * H + j0 + c] : 0.0f; });
-    const int j = j0 + l31;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = n0 + tile_row(r);
-      if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
-    }
-  }
-#endif
   __syncthreads();
-  BNN_T(2);
 
   // yhat = h2 w3; residual; dU/dyhat = -p (Y - yhat)
   float esq = 0.0f;
@@ -259,113 +211,72 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     float yh = 0.0f;
     // sequential in j (the sum's order), unrolled so the LDS reads are issued ahead of the FMA chain
 #pragma unroll 16
-    for (int j = 0; j < H; ++j) yh += h2[n * H + j] * w3[j];
+    for (int j = 0; j < H; ++j) yh += h2[sw(n, j, H)] * w3[j];
     const float e = Ys[n] - yh;
     esq += e * e;
     gy[n] = -p * e;
   }
   __syncthreads();
-  BNN_T(3);
 
   // grad w3 = w3 + h2^T gy
   for (int j = t; j < H; j += THREADS) {
     float s = 0.0f;
 #pragma unroll 16
-    for (int n = 0; n < N; ++n) s += h2[n * H + j] * gy[n];
+    for (int n = 0; n < N; ++n) s += h2[sw(n, j, H)] * gy[n];
     g[dm.o_w3 + j] = w3[j] + s;
   }
   __syncthreads();
-  BNN_T(4);
   // ga2 = (gy w3^T) * (1 - h2^2)   (in place of h2)
   for (int e = t; e < N * H; e += THREADS) {
     const int n = e / H, j = e % H;
-    const float v = h2[e];
-    h2[e] = gy[n] * w3[j] * (1.0f - v * v);
+    const float v = h2[sw(n, j, H)];
+    h2[sw(n, j, H)] = gy[n] * w3[j] * (1.0f - v * v);
   }
   __syncthreads();
-  BNN_T(5);
 
   // grad W2 = W2 + h1^T ga2: tiles over (i, j), K = n
-#if NMX_BNN_TILE == 16
   for (int tile = wv; tile < mth * mth; tile += NWAVES) {
     const int i0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[k * H + i0 + m] : 0.0f; },
-        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[k * H + j0 + c] : 0.0f; });
+        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[sw(k, i0 + m, H)] : 0.0f; },
+        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[sw(k, j0 + c, H)] : 0.0f; });
     const int j = j0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + tile_row16(r);
-      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
+      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[sw(i, j, H)] + acc[r];
     }
   }
-#else
-  for (int tile = wv; tile < nth * nth; tile += NWAVES) {
-    const int i0 = (tile / nth) * 32, j0 = (tile % nth) * 32;
-    const f32x16 acc = mfma_tile(
-        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[k * H + i0 + m] : 0.0f; },
-        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[k * H + j0 + c] : 0.0f; });
-    const int j = j0 + l31;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = i0 + tile_row(r);
-      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
-    }
-  }
-#endif
   __syncthreads();
-  BNN_T(6);
 
   // ga1 = (ga2 W2^T) * (1 - h1^2): tiles over (n, i), K = j, in place of h1 (a tile reads h1
   // only at its own elements; grad W2 above finished reading h1 at the barrier)
-#if NMX_BNN_TILE == 16
   for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
     const int n0 = (tile / mth) * 16, i0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[(n0 + m) * H + k] : 0.0f; },
-        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[(i0 + c) * H + k] : 0.0f; });
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[sw(n0 + m, k, H)] : 0.0f; },
+        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[sw(i0 + c, k, H)] : 0.0f; });
     const int i = i0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + tile_row16(r);
       if (n < N && i < H) {
-        float* hp = &h1[n * H + i];
+        float* hp = &h1[sw(n, i, H)];
         const float hv = *hp;
         *hp = acc[r] * (1.0f - hv * hv);
       }
     }
   }
-#else
-  for (int tile = wv; tile < ntn * nth; tile += NWAVES) {
-    const int n0 = (tile / nth) * 32, i0 = (tile % nth) * 32;
-    const f32x16 acc = mfma_tile(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[(n0 + m) * H + k] : 0.0f; },
-        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[(i0 + c) * H + k] : 0.0f; });
-    const int i = i0 + l31;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = n0 + tile_row(r);
-      if (n < N && i < H) {
-        float* hp = &h1[n * H + i];
-        const float hv = *hp;
-        *hp = acc[r] * (1.0f - hv * hv);
-      }
-    }
-  }
-#endif
   __syncthreads();
-  BNN_T(7);
 
   // grad W1 = W1 + X^T ga1
   for (int e = t; e < Dx * H; e += THREADS) {
     const int k = e / H, j = e % H;
     float s = 0.0f;
 #pragma unroll 16
-    for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[n * H + j];
+    for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[sw(n, j, H)];
     g[dm.o_w1 + e] = W1[e] + s;
   }
-
-  BNN_T(9);
   const float esq_t = block_sum256(esq, red);
   const float wsq_t = block_sum256(wsq, red);
   if (t == 0) {
@@ -378,7 +289,6 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     ev.pe[c] = -lp;
     g[0] = -(3.0f - p + 0.5f * Nf - 0.5f * p * esq_t);
   }
-  BNN_T(10);
 }
 
 size_t lds_bytes(int N, int Dx, int H) {
@@ -387,15 +297,6 @@ size_t lds_bytes(int N, int Dx, int H) {
 
 }  // namespace
 
-#ifdef NMX_BNN_PROF
-extern "C" int nmx_debug_bnn_profile(unsigned long long* host16) {
-  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_bnn_prof), sizeof(unsigned long long) * 16) != hipSuccess)
-    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
-  unsigned long long z[16] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_bnn_prof), z, sizeof(z)) != hipSuccess) return nmx_fail(NMX_ERR_HIP, "reset");
-  return NMX_OK;
-}
-#endif
 
 extern "C" size_t nmx_pe_bnn_workspace_bytes(int Dx, int H, int num_chains) {
   const size_t D = 1 + (size_t)Dx * H + (size_t)H * H + H;

@@ -95,26 +95,11 @@ constexpr float LN2 = 0.6931471805599453f;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// One 32x32x16 bf16 product.  NMX_X3_SHAPE16_PROBE (timing experiment only, wrong results): each
-// is replaced by two v_mfma_f32_16x16x32_bf16 on the same operand registers into two 4-register
-// slices of the accumulator -- the same matrix-pipe cycles (2 x 16 vs 32), VALU and LDS traffic --
-// to measure what the 16x16 shape's clock gives this kernel before rewriting its layouts
-// (MI355X_MICROARCH.md 'DVFS give-back' item 7, cdna_hip_programming.md rule 28).
+// One 32x32x16 bf16 product (the 16x16x32 shape's clock / issue trade was measured in round 4 by
+// a timing probe, DESIGN.md "headline kernel clock"; the probe is not in the product sources).
 template <int S = 0>
 __device__ __forceinline__ f32x16 x3_mma(const bf16x8& a, const bf16x8& b, f32x16 acc) {
-#ifdef NMX_X3_SHAPE16_PROBE
-  // slices (0-3, 8-11) for S = 0, (4-7, 12-15) for S = 1: calls alternate S, every register lives
-  constexpr int o = 4 * S;
-  f32x4 lo = {acc[o], acc[o + 1], acc[o + 2], acc[o + 3]};
-  f32x4 hi = {acc[8 + o], acc[9 + o], acc[10 + o], acc[11 + o]};
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, lo, 0, 0, 0);
-  hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, hi, 0, 0, 0);
-  acc[o] = lo[0]; acc[o + 1] = lo[1]; acc[o + 2] = lo[2]; acc[o + 3] = lo[3];
-  acc[8 + o] = hi[0]; acc[9 + o] = hi[1]; acc[10 + o] = hi[2]; acc[11 + o] = hi[3];
-  return acc;
-#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-#endif
 }
 
 // VALU instructions the scheduling hints place after each GEMM1(k+1) / GEMM2(k) MFMA (x3_item)
@@ -566,27 +551,6 @@ inline size_t x3_lds_bytes() {
   return x3_tr<KB, DT>() ? (size_t)(3 * NA + 2) * 1024 : (size_t)2 * (x3_nal<KB, DT, H>() + NP - NA) * 1024;
 }
 
-#ifdef NMX_X3_CLOCK
-// diagnostic build only (scripts/x3_clock.py, cdna_hip_programming.md rule 28 / DVFS give-back
-// item 6): per workgroup of the last all-active launch, the shader-clock and 100 MHz real-time
-// ticks spent in the tile loop; the in-kernel clock is their ratio x 100 MHz.  Written only here
-// and read only by nmx_debug_x3_clock: no output depends on it.
-__device__ unsigned long long g_x3_clock[16384 * 2];
-__device__ __forceinline__ unsigned long long x3_memtime() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-__device__ __forceinline__ unsigned long long x3_memrealtime() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#endif
 
 template <int KB, int DT, int H, int SCHED>
 __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split, int ct,
@@ -670,9 +634,6 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         }
       }
     };
-#ifdef NMX_X3_CLOCK
-    const unsigned long long ck_t0 = x3_memtime(), ck_r0 = x3_memrealtime();
-#endif
     if (nt > 0) {
       issue_a(0);
       x3_wait_vm<0>();
@@ -726,13 +687,6 @@ __device__ __forceinline__ void x3_item(const char* __restrict__ Xq, int64_t nti
         if (k + 1 < nt) step(k + 1, accB, accA);
       }
     }
-#ifdef NMX_X3_CLOCK
-    const unsigned long long ck_t1 = x3_memtime(), ck_r1 = x3_memrealtime();
-    if (threadIdx.x == 0 && blockIdx.x < 16384) {
-      g_x3_clock[2 * blockIdx.x + (threadIdx.x & 1)] = ck_t1 - ck_t0;
-      g_x3_clock[2 * blockIdx.x + 1 + (threadIdx.x & 1)] = ck_r1 - ck_r0;
-    }
-#endif
   }
   if (!active || pos >= ldc) return;
 #pragma unroll
@@ -833,47 +787,6 @@ __device__ __forceinline__ void x3_roles_barrier_rt(int n) {  // n wave-uniform
     default: x3_roles_barrier_n<12>(); break;  // (n > 12: waits for more than needed)
   }
 }
-
-// NMX_ROLES_EXP (timing experiments only, wrong results): bit 1 = the B waves skip the residual's
-// three-term split (its raw bits as the three bf16 operands), bit 2 = the A waves skip the
-// epilogue (the accumulator as the residual)
-#ifndef NMX_ROLES_EXP
-#define NMX_ROLES_EXP 0
-#endif
-#if NMX_ROLES_EXP
-template <int DT>
-__device__ __forceinline__ void x3_gemm2_regs_nosplit(const bf16x8 (&fb)[3][DT][2], const float (&res)[16],
-                                                      f32x16 (&g)[DT]) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    u32x4 w;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) w[p] = __float_as_uint(res[8 * s + 2 * p]) ^ (__float_as_uint(res[8 * s + 2 * p + 1]) >> 16);
-    const bf16x8 r1 = __builtin_bit_cast(bf16x8, w), r2 = r1, r3 = r1;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const bf16x8 b1 = fb[0][dt][s], b2 = fb[1][dt][s], b3 = fb[2][dt][s];
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g[dt], 0, 0, 0);
-      g[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g[dt], 0, 0, 0);
-    }
-  }
-}
-#define X3_ROLES_EPI(acc, y4, p, res, lin, prod) \
-  do {                                           \
-    if (NMX_ROLES_EXP & 2) {                     \
-      res[2 * (p)] = acc[2 * (p)];               \
-      res[2 * (p) + 1] = acc[2 * (p) + 1];       \
-    } else {                                     \
-      x3_epi_pair(acc, y4, p, res, lin, prod);   \
-    }                                            \
-  } while (0)
-#else
-#define X3_ROLES_EPI(acc, y4, p, res, lin, prod) x3_epi_pair(acc, y4, p, res, lin, prod)
-#endif
 
 constexpr int X3_ROLE_WAVES = 8;
 // Prefetch depth: tile k + PA is issued in iteration k, and the barrier of iteration k waits
@@ -1033,12 +946,12 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
             n2 = fa[x3_ci<KB, CMP>(1) * 64];
           }
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
-          X3_ROLES_EPI(acc, y4, 2 * kb, res, lin, prod);
+          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
-          X3_ROLES_EPI(acc, y4, 2 * kb + 1, res, lin, prod);
+          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
@@ -1058,10 +971,10 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         if constexpr (H) {  // x3_gemm1's combined products (a1 = (a1 | a2), a2 = (a3 | a1) here)
           constexpr int kb = KB - 1;
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z3[kb], nxt, 0, 0, 0);
-          X3_ROLES_EPI(acc, y4, 2 * kb, res, lin, prod);
+          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
-          X3_ROLES_EPI(acc, y4, 2 * kb + 1, res, lin, prod);
+          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
           __builtin_amdgcn_sched_barrier(0);
           nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
@@ -1091,11 +1004,7 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
       float res[16];
       x3_res_load(rmine + (k & 1) * 4 * 4096, res);  // (waits for every LDS read, the above too)
       x3_tr_wait<DT>(fb);
-#if NMX_ROLES_EXP & 1
-      x3_gemm2_regs_nosplit<DT>(fb, res, g);
-#else
       x3_gemm2_regs<DT>(fb, res, g);
-#endif
     };
     if (nt > 0) {
       issue_a(0);
@@ -1218,13 +1127,6 @@ int check_ev(const nmx_eval_batch* ev) {
 
 extern "C" int nmx_logreg_num_splits(int64_t n_rows) { return x3_num_splits(n_rows); }
 
-#ifdef NMX_X3_CLOCK
-extern "C" int nmx_debug_x3_clock(unsigned long long* host) {  // [16384][2] (shader ticks, 100 MHz ticks)
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_clock), sizeof(unsigned long long) * 16384 * 2) != hipSuccess)
-    return nmx_fail(NMX_ERR_HIP, "hipMemcpyFromSymbol failed");
-  return NMX_OK;
-}
-#endif
 
 // packed buffer: w[64] (k_logreg_colsums) | split-bf16 tiles (k_logreg_pack_x3)
 inline size_t x3_offset() { return (COLTERM_BYTES + 255) / 256 * 256; }

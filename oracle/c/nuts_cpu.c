@@ -111,6 +111,7 @@ static void pe_funnel(int D, const float* z, float* pe, float* g) {
   const int K = D - 1;
   const float y = z[K], e = expf(-y);
   double xx = 0.0;
+#pragma omp simd reduction(+ : xx)
   for (int i = 0; i < K; ++i) xx += (double)z[i] * z[i];
   for (int i = 0; i < K; ++i) g[i] = z[i] * e;
   g[K] = (float)(y / 9.0 + 0.5 * K - 0.5 * e * xx);
@@ -308,13 +309,11 @@ typedef struct {
   int trace_T, trace_L;
 } Chain;
 
-static inline double dotd(const float* a, const float* b, int D) {
-  double s = 0.0;
-  for (int i = 0; i < D; ++i) s += (double)a[i] * b[i];
-  return s;
-}
+/* Reductions in double, vectorised (omp simd reduction: the partial sums' order is the compiler's,
+ * as in any float32 implementation of a dot product) */
 static inline float kinetic(const float* im, const float* r, int D) { /* 0.5 (M^-1 r) . r */
   double s = 0.0;
+#pragma omp simd reduction(+ : s)
   for (int i = 0; i < D; ++i) s += (double)(im[i] * r[i]) * r[i];
   return (float)(0.5 * s);
 }
@@ -322,22 +321,29 @@ static int is_turning(const float* im, const float* rl, const float* rr, const f
                       const float* ck_r_or_null, int D) {
   /* _is_turning(im, r_left, r_right, r_sum'), r_sum' = r_sum (- ck_rs + ck_r for a checkpoint) */
   double la = 0.0, ra = 0.0;
-  for (int i = 0; i < D; ++i) {
-    float s = rs[i];
-    if (ck_rs_or_null) s = s - ck_rs_or_null[i] + ck_r_or_null[i];
-    s = s - (rl[i] + rr[i]) / 2.0f;
-    la += (double)(im[i] * rl[i]) * s;
-    ra += (double)(im[i] * rr[i]) * s;
+  if (ck_rs_or_null) {
+#pragma omp simd reduction(+ : la, ra)
+    for (int i = 0; i < D; ++i) {
+      const float s = (rs[i] - ck_rs_or_null[i] + ck_r_or_null[i]) - (rl[i] + rr[i]) / 2.0f;
+      la += (double)(im[i] * rl[i]) * s;
+      ra += (double)(im[i] * rr[i]) * s;
+    }
+  } else {
+#pragma omp simd reduction(+ : la, ra)
+    for (int i = 0; i < D; ++i) {
+      const float s = rs[i] - (rl[i] + rr[i]) / 2.0f;
+      la += (double)(im[i] * rl[i]) * s;
+      ra += (double)(im[i] * rr[i]) * s;
+    }
   }
   return (la <= 0.0) || (ra <= 0.0);
 }
 static float turn_dots_min(const float* im, const float* rl, const float* rr, const float* rs, const float* ck_rs,
                            const float* ck_r, int D) { /* min(left, right) angle: the trace's U-turn dot */
   double la = 0.0, ra = 0.0;
+#pragma omp simd reduction(+ : la, ra)
   for (int i = 0; i < D; ++i) {
-    float s = rs[i];
-    if (ck_rs) s = s - ck_rs[i] + ck_r[i];
-    s = s - (rl[i] + rr[i]) / 2.0f;
+    const float s = (ck_rs ? rs[i] - ck_rs[i] + ck_r[i] : rs[i]) - (rl[i] + rr[i]) / 2.0f;
     la += (double)(im[i] * rl[i]) * s;
     ra += (double)(im[i] * rr[i]) * s;
   }
@@ -632,6 +638,7 @@ int nmx_cpu_nuts_run(const nmx_cpu_model* m, int C, const float* z0, const float
     leap += B;
     calls += 1;
     const double elapsed = now_s() - t0;
+    if (min_transitions == 0 && elapsed >= seconds) break; /* a timing run: stop mid-transition */
 #pragma omp parallel for schedule(dynamic, 4)
     for (int b = 0; b < B; ++b) {
       Chain* h = ch + idx[b];

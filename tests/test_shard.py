@@ -44,7 +44,7 @@ def test_shard_chains_partition():
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
 
 
-def _worker(rank, world, port, path, x, samples_z):
+def _worker(rank, world, port, path, x, samples_z, x3d):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -58,6 +58,10 @@ def _worker(rank, world, port, path, x, samples_z):
         }
         s = shard.summary({"a": xl})["a"]
         out.update({f"sum_{k}": np.asarray(v) for k, v in s.items()})
+        # config-4 scale path: chunks of a few coordinates, quantiles gathered to rank 0 in float32
+        w = torch.from_numpy(x3d[lo:hi]).to(torch.float32)
+        s3 = shard.summary({"w": w}, max_chunk_bytes=20000)["w"]
+        out.update({f"chk_{k}": np.asarray(v) for k, v in s3.items()})
         # pooled dense-mass covariance over ranks (dense.PooledCovariance.all_reduce)
         lo2, hi2 = shard.shard_chains(samples_z.shape[1], rank, world)
         pool = PooledCovariance(samples_z.shape[0], "cpu", torch.zeros(samples_z.shape[0]))
@@ -74,11 +78,18 @@ def _worker(rank, world, port, path, x, samples_z):
 def test_gloo_two_ranks_reproduce_single_process():
     x = _ar1(7, 120, 2, seed=3)  # 7 chains: uneven 4 / 3 shards
     zs = np.random.RandomState(1).randn(5, 301)
+    x3d = _ar1(7, 60, 12, seed=5).reshape(7, 60, 3, 4).astype(np.float32)  # a [3, 4] site
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.npz")
         port = 29500 + (os.getpid() % 1000)
-        mp.spawn(_worker, args=(2, port, path, x, zs), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, port, path, x, zs, x3d), nprocs=2, join=True)
         r = np.load(path)
+        # the chunked summary over uneven shards vs the host diagnostics (numpyro/diagnostics.py
+        # restated) of all chains in one process
+        ref3 = diagnostics.summary({"w": x3d.astype(np.float64)})["w"]
+        for k in ("mean", "std", "median", "5.0%", "95.0%", "n_eff", "r_hat"):
+            assert r[f"chk_{k}"].shape == (3, 4), k
+            np.testing.assert_allclose(r[f"chk_{k}"], np.asarray(ref3[k]), rtol=1e-6, err_msg=k)
         xt = torch.from_numpy(x)
         np.testing.assert_allclose(r["rhat"], shard.split_gelman_rubin(xt).numpy(), rtol=1e-10)
         np.testing.assert_allclose(r["ess"], shard.effective_sample_size(xt).numpy(), rtol=1e-10)
