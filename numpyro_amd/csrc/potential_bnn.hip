@@ -48,17 +48,6 @@ __device__ __forceinline__ f32x4 mfma_tile16(int K, FA fa, FB fb) {
 }
 __device__ __forceinline__ int tile_row16(int r) { return 4 * ((threadIdx.x & 63) >> 4) + r; }
 
-// LDS layout of the H-wide row-major tiles (h1, h2 [N][H], W2 [H][H]; H = 69 for config 3):
-// element (r, c) lives at r H + (c ^ 32 (r & 1)) for c < 64 (columns >= 64 unswizzled).  The MFMA
-// operand reads take two patterns -- 16 rows x 4 consecutive columns (A of h1 W2 and ga2 W2^T,
-// B of ga2 W2^T) and 4 rows x 16 consecutive columns (B of h1 W2, both operands of h1^T ga2) --
-// and no row stride serves both (== 4 or 16 mod 64 banks respectively); at H = 69 (5 mod 64) the
-// second hit up to four lanes per bank.  Flipping column bit 5 on odd rows moves half the rows
-// to the other half of the banks: mean lanes per bank over every operand read of the three
-// products 2.56 -> 1.78, worst 4 -> 2 (exhaustive search over periodic XOR masks of the column,
-// scripts/bnn_swizzle_search.py), no LDS growth (two workgroups per CU kept), results bitwise
-// unchanged (addresses only).
-__device__ __forceinline__ int sw(int r, int c, int H) { return r * H + (c < 64 ? c ^ ((r & 1) << 5) : c); }
 
 struct BnnDims {
   int N, Dx, H;
@@ -165,7 +154,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
 #pragma unroll 20
   for (int i = t; i < H * H; i += THREADS) {
     const float v = z[dm.o_w2 + i];
-    W2[sw(i / H, i % H, H)] = v;
+    W2[i] = v;
     wsq += v * v;
   }
   for (int i = t; i < H; i += THREADS) {
@@ -183,7 +172,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     const int n = e / H, j = e % H;
     float a = 0.0f;
     for (int k = 0; k < Dx; ++k) a += Xs[n * Dx + k] * W1[k * H + j];
-    h1[sw(n, j, H)] = tanhf(a);
+    h1[e] = tanhf(a);
   }
   __syncthreads();
 
@@ -194,13 +183,13 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
     const int n0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[sw(n0 + m, k, H)] : 0.0f; },
-        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[sw(k, j0 + c, H)] : 0.0f; });
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h1[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && j0 + c < H) ? W2[k * H + j0 + c] : 0.0f; });
     const int j = j0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + tile_row16(r);
-      if (n < N && j < H) h2[sw(n, j, H)] = tanhf(acc[r]);
+      if (n < N && j < H) h2[n * H + j] = tanhf(acc[r]);
     }
   }
   __syncthreads();
@@ -211,7 +200,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     float yh = 0.0f;
     // sequential in j (the sum's order), unrolled so the LDS reads are issued ahead of the FMA chain
 #pragma unroll 16
-    for (int j = 0; j < H; ++j) yh += h2[sw(n, j, H)] * w3[j];
+    for (int j = 0; j < H; ++j) yh += h2[n * H + j] * w3[j];
     const float e = Ys[n] - yh;
     esq += e * e;
     gy[n] = -p * e;
@@ -222,15 +211,15 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int j = t; j < H; j += THREADS) {
     float s = 0.0f;
 #pragma unroll 16
-    for (int n = 0; n < N; ++n) s += h2[sw(n, j, H)] * gy[n];
+    for (int n = 0; n < N; ++n) s += h2[n * H + j] * gy[n];
     g[dm.o_w3 + j] = w3[j] + s;
   }
   __syncthreads();
   // ga2 = (gy w3^T) * (1 - h2^2)   (in place of h2)
   for (int e = t; e < N * H; e += THREADS) {
     const int n = e / H, j = e % H;
-    const float v = h2[sw(n, j, H)];
-    h2[sw(n, j, H)] = gy[n] * w3[j] * (1.0f - v * v);
+    const float v = h2[e];
+    h2[e] = gy[n] * w3[j] * (1.0f - v * v);
   }
   __syncthreads();
 
@@ -238,13 +227,13 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int tile = wv; tile < mth * mth; tile += NWAVES) {
     const int i0 = (tile / mth) * 16, j0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[sw(k, i0 + m, H)] : 0.0f; },
-        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[sw(k, j0 + c, H)] : 0.0f; });
+        N, [&](int m, int k) { return (k < N && i0 + m < H) ? h1[k * H + i0 + m] : 0.0f; },
+        [&](int k, int c) { return (k < N && j0 + c < H) ? h2[k * H + j0 + c] : 0.0f; });
     const int j = j0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + tile_row16(r);
-      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[sw(i, j, H)] + acc[r];
+      if (i < H && j < H) g[dm.o_w2 + i * H + j] = W2[i * H + j] + acc[r];
     }
   }
   __syncthreads();
@@ -254,14 +243,14 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
   for (int tile = wv; tile < mtn * mth; tile += NWAVES) {
     const int n0 = (tile / mth) * 16, i0 = (tile % mth) * 16;
     const f32x4 acc = mfma_tile16(
-        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[sw(n0 + m, k, H)] : 0.0f; },
-        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[sw(i0 + c, k, H)] : 0.0f; });
+        H, [&](int m, int k) { return (n0 + m < N && k < H) ? h2[(n0 + m) * H + k] : 0.0f; },
+        [&](int k, int c) { return (k < H && i0 + c < H) ? W2[(i0 + c) * H + k] : 0.0f; });
     const int i = i0 + l15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + tile_row16(r);
       if (n < N && i < H) {
-        float* hp = &h1[sw(n, i, H)];
+        float* hp = &h1[n * H + i];
         const float hv = *hp;
         *hp = acc[r] * (1.0f - hv * hv);
       }
@@ -274,7 +263,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
     const int k = e / H, j = e % H;
     float s = 0.0f;
 #pragma unroll 16
-    for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[sw(n, j, H)];
+    for (int n = 0; n < N; ++n) s += Xs[n * Dx + k] * h1[n * H + j];
     g[dm.o_w1 + e] = W1[e] + s;
   }
   const float esq_t = block_sum256(esq, red);
