@@ -41,10 +41,15 @@ DENSE, UPPER, LOWER = 0, 1, 2  # nmx_gemm_chains `triangle` (shape of A in Out =
 class Whitening:
     """z = mu + T w, T T^T = M^-1.  Holds the two padded At operands of nmx_gemm_chains."""
 
-    def __init__(self, dim: int, device, x3: bool = True):
+    def __init__(self, dim: int, device, x3: bool = True, blocks=None):
         """x3: split-bf16 products (nmx_gemm_chains_x3, the default) or the f32-MFMA kernel
-        (nmx_gemm_chains, kept for comparison in tests)."""
+        (nmx_gemm_chains, kept for comparison in tests).  blocks (MassBlocks): a structured mass
+        (dense_mass=pooled([...])): M^-1 masked to the blocks, T factored block by block in each
+        block's own coordinate order -- triangular only when every block's coordinates are
+        contiguous and in ravel order, else the products run on the full matrix."""
         self.D = int(dim)
+        self.blocks = blocks
+        self.upper = True
         self.device = torch.device(device)
         self.lda = int(lib().nmx_dense_padded_dim(self.D))
         self.fwd_t = torch.zeros(self.lda, self.lda, dtype=torch.float32, device=self.device)  # T^T
@@ -77,8 +82,8 @@ class Whitening:
     def product(self, forward, x, out, bias, phase, count, num_chains, ldc, stream):
         """Out = T In (+ bias) if forward else T^T In, on raw device pointers (x, out, bias,
         phase, count: ints or None): the nmx_gemm_chains(_x3) call of every dense product."""
-        at, ap, tri = (self.fwd_t, getattr(self, "fwd_p", None), UPPER) if forward else \
-            (self.bwd_t, getattr(self, "bwd_p", None), LOWER)
+        at, ap, tri = (self.fwd_t, getattr(self, "fwd_p", None), self._tri(True)) if forward else \
+            (self.bwd_t, getattr(self, "bwd_p", None), self._tri(False))
         ws = ptr(self.workspace(ldc))
         if self.x3:
             check(lib().nmx_gemm_chains_x3(ptr(ap), self.lda, self.D, x, out, bias, tri, ldc, phase, count,
@@ -91,14 +96,16 @@ class Whitening:
     def product_rows(self, rows, list_, count, out, num_chains, ldc, stream):
         """Out = T In + mu on the listed chains' rows gathered in place (In column p = rows[list[p]]):
         nmx_gemm_chains_x3_rows, the pack + forward product in one call (x3 only)."""
-        check(lib().nmx_gemm_chains_x3_rows(ptr(self.fwd_p), self.lda, self.D, rows, list_, out, ptr(self.mu), UPPER,
+        check(lib().nmx_gemm_chains_x3_rows(ptr(self.fwd_p), self.lda, self.D, rows, list_, out, ptr(self.mu),
+                                            self._tri(True),
                                             ldc, count, int(num_chains), ptr(self.split_buffer(ldc)),
                                             ptr(self.workspace(ldc)), stream), "nmx_gemm_chains_x3_rows")
 
     def product_to_rows(self, x, list_, count, rows, pe_in, pe_out, num_chains, ldc, stream):
         """rows[list[p]] = (T^T In)[:, p] for p < count, pe_out[list[p]] = pe_in[p]:
         nmx_gemm_chains_x3_to_rows, the backward product + unpack in one call (x3 only)."""
-        check(lib().nmx_gemm_chains_x3_to_rows(ptr(self.bwd_p), self.lda, self.D, x, list_, rows, None, LOWER, ldc,
+        check(lib().nmx_gemm_chains_x3_to_rows(ptr(self.bwd_p), self.lda, self.D, x, list_, rows, None,
+                                               self._tri(False), ldc,
                                                count, int(num_chains), ptr(self.split_buffer(ldc)), pe_in, pe_out,
                                                stream), "nmx_gemm_chains_x3_to_rows")
 
@@ -106,10 +113,14 @@ class Whitening:
                       pe_out=None):
         """nmx_gemm_chains_x3_lists: In gathered from rows through in_list (or columns), Out stored to
         rows through out_list (or columns), positions < count (x3 only)."""
-        ap, tri = (self.fwd_p, UPPER) if forward else (self.bwd_p, LOWER)
+        ap, tri = (self.fwd_p, self._tri(True)) if forward else (self.bwd_p, self._tri(False))
         check(lib().nmx_gemm_chains_x3_lists(ptr(ap), self.lda, self.D, x, in_list, out, out_list, bias, tri, ldc,
                                              count, int(num_chains), ptr(self.split_buffer(ldc)), pe_in, pe_out,
                                              stream), "nmx_gemm_chains_x3_lists")
+
+    def _tri(self, forward):
+        """The products' triangle flag: T upper (T^T lower) triangular, or the full matrix (0)."""
+        return (UPPER if forward else LOWER) if self.upper else 0
 
     def set(self, inverse_mass_matrix, mu=None):
         """inverse_mass_matrix [D, D] (or diagonal [D]); mu [D] or None (keep)."""
@@ -118,8 +129,15 @@ class Whitening:
             imm = torch.diag(imm)
         if imm.shape != (self.D, self.D):
             raise ValueError(f"inverse_mass_matrix must be [{self.D}, {self.D}]")
-        # tril_inv = swap(chol(cov[::-1, ::-1])[::-1, ::-1])  (hmc_util.py:228-231); T = tril_inv^T
-        T = torch.linalg.cholesky(imm.flip(0, 1)).flip(0, 1)
+        if self.blocks is not None:
+            # per block the flipped Cholesky in the block's order (hmc_util.py:224-231 per
+            # welford_covariance block, :439-515 structure), the diagonal block's square roots
+            imm = self.blocks.mask(imm[None])[0]
+            T = self.blocks.factor(imm[None])[0]
+            self.upper = bool(torch.equal(torch.triu(T), T))
+        else:
+            # tril_inv = swap(chol(cov[::-1, ::-1])[::-1, ::-1])  (hmc_util.py:228-231); T = tril_inv^T
+            T = torch.linalg.cholesky(imm.flip(0, 1)).flip(0, 1)
         self.inverse_mass_matrix = imm.clone()  # never the caller's tensor: snapshots share it
         self.version += 1
         self.T = T
@@ -141,6 +159,16 @@ class Whitening:
         """T^-1 (upper triangular, float64), by column chunks: hipBLAS trsm refuses very large
         right-hand sides (D = 10000 x 4096 fails to allocate its workspace)."""
         if self._tinv is None:
+            if self.blocks is not None:  # block by block: T is block-diagonal up to the blocks' order
+                inv = torch.zeros_like(self.T)
+                for _, idx, dense in self.blocks.blocks:
+                    idx = idx.to(self.device)
+                    if dense:
+                        inv[idx[:, None], idx[None, :]] = torch.linalg.inv(self.T[idx[:, None], idx[None, :]])
+                    else:
+                        inv[idx, idx] = 1.0 / self.T[idx, idx]
+                self._tinv = inv
+                return inv
             eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
             cols = [torch.linalg.solve_triangular(self.T, eye[:, a:a + 1024], upper=True)
                     for a in range(0, self.D, 1024)]
@@ -172,10 +200,12 @@ class Whitening:
 
 
 class WhitenedPotential(Potential):
-    """U_w(w) = U(mu + T w), grad_w = T^T grad U (see module docstring)."""
+    """U_w(w) = U(mu + T w), grad_w = T^T grad U (see module docstring); with `blocks` the T of a
+    pooled structured mass (Whitening)."""
 
-    def __init__(self, base: Potential):
+    def __init__(self, base: Potential, blocks=None):
         self.base = base
+        self.blocks = blocks
         self.dim = base.dim
         self.sites = [(n, s, REAL) for n, s, _ in base.sites]
         self.whitening = None
@@ -188,7 +218,7 @@ class WhitenedPotential(Potential):
     def _bind(self, C, ldc, device):
         self.base.bind(C, ldc, device)
         if self.whitening is None or self.whitening.device != device:
-            self.whitening = Whitening(self.dim, device)
+            self.whitening = Whitening(self.dim, device, blocks=getattr(self, "blocks", None))
         self._rows_zg = None
         self.zb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
         self.gb = torch.zeros(self.dim, ldc, dtype=torch.float32, device=device)
@@ -271,8 +301,10 @@ class WhitenedPotential(Potential):
 
     def flops_per_eval(self, num_chains):
         """Algorithmic FLOPs of the two triangular products (D^2 each per chain) -- the
-        dense-matrix count 4 D^2 of SURVEY.md §8d halves because T is triangular."""
-        return 2.0 * self.dim * self.dim * num_chains
+        dense-matrix count 4 D^2 of SURVEY.md §8d halves because T is triangular (a structured
+        T in a non-triangular coordinate order runs the full products)."""
+        full = self.whitening is not None and not self.whitening.upper
+        return (4.0 if full else 2.0) * self.dim * self.dim * num_chains
 
 
 class PooledCovariance:

@@ -133,9 +133,9 @@ class Engine:
                                                                            or bool(opts.dense_blocks))
         self.blocks = None
         if opts.dense_blocks:
+            # structured mass: per chain (the reference's semantics), or pooled over chains
+            # (dense_mass=pooled([...]): one block-structured matrix, WhitenedPotential below)
             from .dense import MassBlocks
-            if not self.chain_dense:
-                raise NotImplementedError("structured dense_mass with dense_mass='pooled'")
             self.blocks = MassBlocks(potential.sites, opts.dense_blocks)
         if self.chain_dense:
             from .dense import CHAIN_DENSE_MAX_D, ChainWhitenedPotential, chain_dense_bytes
@@ -144,11 +144,13 @@ class Engine:
                 raise ValueError(
                     f"per-chain dense mass matrices for {num_chains} chains of dimension {potential.dim} need "
                     f"{need / 2**30:.1f} GiB (limit {opts.chain_dense_bytes / 2**30:.0f} GiB, dim <= "
-                    f"{CHAIN_DENSE_MAX_D}); use dense_mass='pooled' for one matrix adapted over all chains")
+                    f"{CHAIN_DENSE_MAX_D}); use " + ("numpyro_amd.infer.pooled(dense_mass)" if self.blocks is not None
+                                                     else "dense_mass='pooled'") +
+                    " for one matrix adapted over all chains")
             potential = ChainWhitenedPotential(potential, self.blocks)
         elif self.dense:
             from .dense import WhitenedPotential
-            potential = WhitenedPotential(potential)
+            potential = WhitenedPotential(potential, self.blocks)
         self.potential = potential
         self.C = int(num_chains)
         self.D = int(potential.dim)
@@ -800,7 +802,8 @@ class Engine:
                 mats = (wt.inverse_mass_matrix.to(torch.float32), wt.mass_matrix_sqrt().to(torch.float32),
                         wt.mass_matrix_sqrt_inv().to(torch.float32).clone())
                 if self.blocks is not None:  # {site group: block} dicts, as HMCAdaptState holds them
-                    mats = tuple(self.blocks.split(m) for m in mats)
+                    mats = tuple(self.blocks.split(m) if self.chain_dense else
+                                 {k: v[0] for k, v in self.blocks.split(m[None]).items()} for m in mats)
                 self._mass_cache = (key, mats)
             return self._mass_cache[1]
         ms = self.chain_state("mass_sqrt").clone()

@@ -130,6 +130,19 @@ def restore_state(eng, state):
     state._engine = eng
 
 
+class PooledGroups(list):
+    """dense_mass=pooled([("x", "y"), ...]): the structured mass of the listed site groups
+    (hmc.py:239-252: dense blocks, one diagonal block over the other sites) adapted ONCE from the
+    draws of all chains -- the labelled opt-in for groups whose per-chain blocks do not fit (the
+    reference adapts one matrix per chain; dense_mass='pooled' is the same for one dense block over
+    every site)."""
+
+
+def pooled(groups):
+    """Mark a structured dense_mass as pooled over chains (PooledGroups)."""
+    return PooledGroups(tuple(g) for g in groups)
+
+
 class MCMCKernel:
     """Interface of numpyro/infer/mcmc.py:32-158."""
 
@@ -194,11 +207,16 @@ class HMC(MCMCKernel):
         if find_heuristic_step_size and dense_mass:
             raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
                                       "coordinates, the dense engine in whitened ones")
+        self._pooled = isinstance(dense_mass, PooledGroups)
         if isinstance(dense_mass, str):
             if dense_mass != "pooled":
                 raise ValueError("dense_mass must be a bool, 'pooled' or a list of site groups")
             warnings.warn("dense_mass='pooled': one dense mass matrix is adapted from the draws of all chains "
                           "(not per chain as in numpyro); chains share it", stacklevel=2)
+        if self._pooled:
+            warnings.warn("dense_mass=pooled([...]): one structured mass matrix (dense blocks over the listed "
+                          "site groups, diagonal elsewhere) is adapted from the draws of all chains (not per chain "
+                          "as in numpyro); chains share it", stacklevel=2)
         if isinstance(dense_mass, (list, tuple)):
             # structured mass (hmc.py:239-252): dense blocks over the listed site groups, one
             # diagonal block over the remaining sites; adapted per chain (dense.MassBlocks)
@@ -251,7 +269,8 @@ class HMC(MCMCKernel):
         return SamplerOptions(
             algo=self._algo, step_size=self._step_size, adapt_step_size=self._adapt_step_size,
             adapt_mass_matrix=self._adapt_mass_matrix,
-            dense_mass=self._dense_mass if self._dense_mass == "pooled" else bool(self._dense_mass),
+            dense_mass="pooled" if (self._dense_mass == "pooled" or getattr(self, "_pooled", False))
+            else bool(self._dense_mass),
             dense_blocks=list(self._dense_mass) if isinstance(self._dense_mass, list) and self._dense_mass else None,
             target_accept_prob=self._target_accept_prob, max_tree_depth=md,
             trajectory_length=self._trajectory_length, num_steps=self._num_steps,

@@ -848,3 +848,82 @@ def test_inverse_mass_matrix_dict_of_blocks_matches_oracle(device):
         hist.append(PC.traced(o, s, T))
     par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
     PC.report(par, "inverse_mass_matrix dict", frac=0.9)
+
+
+def test_pooled_structured_mass_matches_oracle(device):
+    """dense_mass=pooled([("w3", "prec_obs")]) on the BNN at H = 16 (D = 321: the chain-row dense
+    step): one structured mass for all chains -- a dense block over (w3, prec_obs) in that group's
+    order, a diagonal block over w1 and w2 (hmc.py:239-252, hmc_util.py:439-515) -- adapted from the
+    pooled draws of the middle window.  (1) teacher-forced: the window's draws of every chain, pooled
+    (mean and covariance over chains and draws), regularized as welford_covariance's final_fn
+    (hmc_util.py:212-226) and cut to the blocks, reproduce the state's {group: block} matrices; the
+    group order makes T non-triangular in ravel order, so the whitening runs the full products.
+    (2) from the post-warmup state the oracle's dense-mass NUTS with the block matrices scattered into
+    full ones (each block's own flipped Cholesky: mass_matrix_sqrt block by block) takes the device's
+    trees and draws, leaf-located against the device's decision trace."""
+    import warnings
+
+    from numpyro_amd import datasets
+    from numpyro_amd.infer import pooled
+
+    Hh, C, W, T, seed = 16, 64, 150, 3, 41
+    X, Y = datasets.bnn_data(N=30, D_X=3)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        kern = NUTS(P.bnn, dense_mass=pooled([("w3", "prec_obs")]), max_tree_depth=6)
+    mcmc = MCMC(kern, num_warmup=W, num_samples=T, num_chains=C, postprocess_fn=lambda z: z)
+    mcmc.warmup(seed, X, Y, Hh, collect_warmup=True)
+    eng = mcmc._engine
+    assert eng.dense and not eng.chain_dense and eng.blocks is not None and eng.crow
+    wt = eng.potential.whitening
+    assert not wt.upper  # (w3, prec_obs) is not in ravel order
+    ws = mcmc.get_samples(group_by_chain=True)
+    D = eng.D
+    flat = lambda d: np.concatenate([d["prec_obs"].cpu().numpy()[..., None],  # noqa: E731
+                                     d["w1"].cpu().numpy().reshape(*d["w1"].shape[:2], -1),
+                                     d["w2"].cpu().numpy().reshape(*d["w2"].shape[:2], -1),
+                                     d["w3"].cpu().numpy().reshape(*d["w3"].shape[:2], -1)], axis=-1)
+    draws = flat(ws).astype(np.float64)  # [C, W, D] ravel order
+    assert draws.shape == (C, W, D)
+    win = draws[:, 75:100].reshape(-1, D)  # the middle window [75, 99], all chains pooled
+    n = win.shape[0]
+    cov = np.cov(win.T) * n / (n + 5.0) + 1e-3 * 5.0 / (n + 5.0) * np.eye(D)
+    o = 1 + 3 * Hh + Hh * Hh
+    grp = list(range(o, o + Hh)) + [0]
+    rest = list(range(1, o))
+    st = mcmc.post_warmup_state
+    imm = st.adapt_state.inverse_mass_matrix
+    assert set(imm) == {("w3", "prec_obs"), ("w1", "w2")}
+    np.testing.assert_allclose(imm[("w3", "prec_obs")].cpu().numpy(), cov[np.ix_(grp, grp)], rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(imm[("w1", "w2")].cpu().numpy(), cov[rest, rest], rtol=2e-4, atol=1e-6)
+    # (2) sampling from the post-warmup state, traced
+    eng.set_trace(C, W, T)
+    mcmc.run(seed + 1, X, Y, Hh, extra_fields=("num_steps",))
+    tr = eng.trace_records()
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"].cpu().numpy()
+    zs = flat(mcmc.get_samples(True))
+    z0 = flat({k: v[:, None] for k, v in st.z.items()})[:, 0]
+    g0, pe0 = st.z_grad.cpu().numpy(), st.potential_energy.cpu().numpy()
+    ss = st.adapt_state.step_size.cpu().numpy()
+    dense_b = imm[("w3", "prec_obs")].cpu().numpy().astype(np.float32)
+    diag_b = imm[("w1", "w2")].cpu().numpy().astype(np.float32)
+    imm_f = np.zeros((D, D), np.float32)
+    msq_f = np.zeros((D, D), np.float32)
+    i_b, sq_b, _ = H._initialize_mass_matrix(len(grp), dense_b, True)
+    imm_f[np.ix_(grp, grp)], msq_f[np.ix_(grp, grp)] = i_b, sq_b
+    i_d, sq_d, _ = H._initialize_mass_matrix(len(rest), diag_b, False)
+    imm_f[rest, rest], msq_f[rest, rest] = i_d, sq_d
+    ref = OP.BNN(X, Y, Hh, dtype=np.float32)
+    hist = []
+    for c in range(C):
+        o_ = H.NUTSOracle(PC.f32(ref.pe_grad), D, W, step_size=float(ss[c]), adapt_step_size=False,
+                          adapt_mass_matrix=False, dense_mass=True, inverse_mass_matrix=np.eye(D, dtype=np.float32),
+                          max_tree_depth=6)
+        wa = o_.wa_init((z0[c].astype(np.float32),), None, np.float32(ss[c]),
+                        inverse_mass_matrix=np.eye(D, dtype=np.float32), mass_matrix_size=D)._replace(
+            inverse_mass_matrix=imm_f, mass_matrix_sqrt=msq_f)
+        s0 = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
+                        0, np.float32(0), np.float32(0), False, wa, (seed + 1, c))
+        hist.append(PC.traced(o_, s0, T))
+    par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
+    PC.report(par, "pooled structured mass BNN D=321", frac=0.8)
