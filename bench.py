@@ -247,6 +247,7 @@ def _config_specs():
                    model=P.stochastic_volatility, args=(r,), chains=8192, warmup=CONFIG_WARMUP["c4"],
                    steps=10, dense=False, one_gpu=False, bytes=7 * 4 * 2519,
                    basis="7 D x 4 B per chain-leapfrog (z, r, g read + write, inverse mass read; SURVEY §8d)",
+                   valu_profile="profiles/r05/sv_valu.json",
                    cpu=lambda dt=np.float32: OB.SVBatch(r, dtype=dt), cpu_chains=32,
                    c_model="sv", c_args=(r,)),
     }
@@ -402,6 +403,27 @@ def _oracle_trace(hist, L):
     return tr, ns, z
 
 
+def _valu_roofline(path, rank_rate):
+    """VALU issue fraction of a kernel that the HBM basis does not bound: the profiled VALU
+    wave-instructions per chain-leapfrog (rocprofv3 SQ_INSTS_VALU over the kernel's dispatches,
+    committed under profiles/) x this rank's leapfrog rate, against the SIMDs' issue peak of
+    one wave64 VALU instruction per 2 cycles (256 CUs x 4 SIMDs, MI355X_MICROARCH.md) at the
+    effective clock profiled with it (GRBM_GUI_ACTIVE / 8 / kernel time)."""
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), path)) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return None
+    per, clk = prof["valu_wave_insts_per_leapfrog"], prof["effective_clock_ghz"]
+    achieved = per * rank_rate / 1e9
+    peak = 256 * 4 * 0.5 * clk
+    return {"achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s", "frac": achieved / peak,
+            "insts_per_leapfrog": per, "salu_per_leapfrog": prof.get("salu_per_leapfrog"), "clock_ghz": clk,
+            "profile_frac": prof.get("valu_issue_frac"), "source": path,
+            "basis": "profiled VALU wave-instructions per chain-leapfrog x this rank's leapfrog rate / (1024 SIMDs "
+                     "x 0.5 instr/cycle x profiled clock)"}
+
+
 def secondary_configs(which, rank, world, device, cpu_seconds):
     """Leapfrogs/s of the BASELINE.json secondary configs on synthetic data of their shape:
     adaptation (untimed; its tree sizes and divergences reported), then `steps` transitions
@@ -501,6 +523,8 @@ def secondary_configs(which, rank, world, device, cpu_seconds):
             gbs = sp["bytes"] * leap / wall / 1e9
             r["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": gbs / MI355X_HBM_PEAK_GBS, "basis": sp["basis"] + " over the sampling wall time"}
+            if sp.get("valu_profile"):
+                r["roofline"]["valu"] = _valu_roofline(sp["valu_profile"], st[0].item() / wall)
         # end-of-run exchange: cross-chain split R-hat over ranks (+ sample
         # gather for the sharded config); R-hat of the timed draws is the regime check
         torch.cuda.synchronize()

@@ -222,6 +222,13 @@ int nmx_nuts_resume(const nmx_nuts_config* cfg, void* arena, void* stream);
 int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void* stream);
 int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream);
 int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, void* stream);
+/* Dense mass (whitened arena, unit_mass): noise writes each searching chain's normals eps
+ * [D][ldc] (the draw propose would make; 0 for the others), the caller maps them to the
+ * whitened momentum p = T^T M^-1 eps (z = mu + T w: the reference's r = M^-1 eps,
+ * hmc_util.py:359, with kinetic 0.5 r^T M^-1 r = 0.5 |p|^2), and propose_with runs propose
+ * with that momentum ([D][ldc]; NULL = propose). */
+int nmx_heuristic_noise(const nmx_nuts_config* cfg, void* arena, float* eps, void* stream);
+int nmx_heuristic_propose_with(const nmx_nuts_config* cfg, void* arena, const float* momentum, void* stream);
 /* One lockstep step of the per-chain NUTS/HMC state machine (sample_kernel hmc.py:459-530
  * with build_tree hmc_util.py:1088-1180 unrolled into leaves): consumes the potential at
  * z_eval for LEAF chains, advances trees / transitions / adaptation / collection, and

@@ -2605,8 +2605,31 @@ __global__ void k_heur_begin(Arena a, nmx_nuts_config cfg) {
   AF(NMX_F_HS_STEP)[c] = AF(NMX_F_STEP_SIZE)[c];
 }
 
-// step update, momentum, first half step and z_eval; lists the searching chains (list 0)
-__global__ void k_heur_propose(Arena a, nmx_nuts_config cfg) {
+// the search's normals of every searching chain's attempt, eps[D][ldc] (0 for the others):
+// the momentum draw of k_heur_propose, exported for a caller that maps it through a dense mass
+__global__ void k_heur_noise(Arena a, nmx_nuts_config cfg, float* eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cfg.ldc) return;
+  const int k = c < cfg.num_chains ? AI(NMX_F_HS_K)[c] : -1;
+  const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
+  const int it = k >= 0 ? AI(NMX_F_ITER)[c] : 0;
+  for (int blk = 0; 4 * blk < cfg.dim; ++blk) {
+    float n[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (k >= 0) {
+      const nmx_u4 x = nmx_rng(cfg.seed, gch, (uint32_t)it, NMX_EV_HEURISTIC, blk, (uint32_t)k);
+      nmx_box_muller(x.x, x.y, n[0], n[1]);
+      nmx_box_muller(x.z, x.w, n[2], n[3]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * blk + q < cfg.dim) eps[(size_t)(4 * blk + q) * cfg.ldc + c] = n[q];
+  }
+}
+
+// step update, momentum, first half step and z_eval; lists the searching chains (list 0).
+// mom != NULL: the momentum is given ([D][ldc], unit mass: a whitened dense mass's
+// T^T M^-1 eps), else drawn as im * eps (hmc_util.py:359 momentum_generator)
+__global__ void k_heur_propose(Arena a, nmx_nuts_config cfg, const float* mom) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = c < cfg.num_chains ? AI(NMX_F_HS_K)[c] : -1;
   const bool act = k >= 0;
@@ -2619,17 +2642,19 @@ __global__ void k_heur_propose(Arena a, nmx_nuts_config cfg) {
     const int ldc = cfg.ldc;
     float ke = 0.0f;
     for (int blk = 0; 4 * blk < cfg.dim; ++blk) {
-      const nmx_u4 x = nmx_rng(cfg.seed, gch, (uint32_t)it, NMX_EV_HEURISTIC, blk, (uint32_t)k);
-      float n[4];
-      nmx_box_muller(x.x, x.y, n[0], n[1]);
-      nmx_box_muller(x.z, x.w, n[2], n[3]);
+      float n[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (!mom) {
+        const nmx_u4 x = nmx_rng(cfg.seed, gch, (uint32_t)it, NMX_EV_HEURISTIC, blk, (uint32_t)k);
+        nmx_box_muller(x.x, x.y, n[0], n[1]);
+        nmx_box_muller(x.z, x.w, n[2], n[3]);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int d = 4 * blk + q;
         if (d < cfg.dim) {
           const size_t idx = (size_t)d * ldc + c;
           const float im = cfg.unit_mass ? 1.0f : AV(NMX_F_INV_MASS)[idx];
-          const float r = im * n[q];
+          const float r = mom ? mom[idx] : im * n[q];
           ke += (im * r) * r;
           const float rh = r - (0.5f * step) * AV(NMX_F_ZGRAD)[idx];
           AV(NMX_F_RL)[idx] = rh;
@@ -2804,17 +2829,34 @@ extern "C" int nmx_heuristic_begin(const nmx_nuts_config* cfg, void* arena, void
   return nmx_check_launch("k_heur_begin");
 }
 
-extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream) {
+extern "C" int nmx_heuristic_propose_with(const nmx_nuts_config* cfg, void* arena, const float* momentum,
+                                          void* stream) {
   int st = validate(cfg);
   if (st) return st;
   if ((st = need_chain_minor(cfg, "nmx_heuristic_propose"))) return st;
   if (group_count(*cfg) > 1) return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_propose: one chain group only");
+  if (momentum && !cfg->unit_mass)
+    return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_propose_with: a given momentum needs unit_mass");
   Arena a = arena_of(cfg, arena);
   if (hipMemsetAsync(a.counters + 2, 0, 4, (hipStream_t)stream) != hipSuccess)
     return nmx_fail(NMX_ERR_HIP, "hipMemsetAsync failed");
   hipLaunchKernelGGL(k_heur_propose, dim3((cfg->num_chains + 63) / 64), dim3(64), 0, (hipStream_t)stream, a,
-                     *cfg);
+                     *cfg, momentum);
   return nmx_check_launch("k_heur_propose");
+}
+
+extern "C" int nmx_heuristic_propose(const nmx_nuts_config* cfg, void* arena, void* stream) {
+  return nmx_heuristic_propose_with(cfg, arena, nullptr, stream);
+}
+
+extern "C" int nmx_heuristic_noise(const nmx_nuts_config* cfg, void* arena, float* eps, void* stream) {
+  int st = validate(cfg);
+  if (st) return st;
+  if ((st = need_chain_minor(cfg, "nmx_heuristic_noise"))) return st;
+  if (!eps) return nmx_fail(NMX_ERR_INVALID, "nmx_heuristic_noise: eps is NULL");
+  Arena a = arena_of(cfg, arena);
+  hipLaunchKernelGGL(k_heur_noise, dim3(cfg->ldc / 64), dim3(64), 0, (hipStream_t)stream, a, *cfg, eps);
+  return nmx_check_launch("k_heur_noise");
 }
 
 extern "C" int nmx_heuristic_finish(const nmx_nuts_config* cfg, void* arena, int at_init, void* stream) {

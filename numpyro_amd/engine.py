@@ -105,11 +105,6 @@ class Engine:
     def __init__(self, potential, num_chains: int, opts: SamplerOptions, device=None,
                  chain_offset: int = 0, sync_chains: bool = False):
         self.dense = bool(opts.dense_mass)
-        if self.dense and opts.find_heuristic_step_size:
-            # the search would run in whitened coordinates and never again after a window-end
-            # re-expression: not the reference's find_reasonable_step_size (hmc.py:320-331)
-            raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
-                                      "coordinates, the dense engine in whitened ones")
         self.model_potential = potential
         # the initial inverse mass matrix in ravel coordinates: a dict of site-group blocks, a
         # structured dense_mass's array, or a matrix for a diagonal mass take the reference's
@@ -379,13 +374,49 @@ class Engine:
         ev = self.eval_lists[0]
         ev.num_chains = self.C
         check(L.nmx_heuristic_begin(cfgp, arena, s), "nmx_heuristic_begin")
+        eps = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device) if self.dense else None
         for _ in range(600):  # the step doubles or halves each round: <= 2 x 254 rounds to an extreme
-            check(L.nmx_heuristic_propose(cfgp, arena, s), "nmx_heuristic_propose")
+            if self.dense:
+                check(L.nmx_heuristic_noise(cfgp, arena, ptr(eps), s), "nmx_heuristic_noise")
+                check(L.nmx_heuristic_propose_with(cfgp, arena, ptr(self._dense_momentum(eps, s)), s),
+                      "nmx_heuristic_propose_with")
+            else:
+                check(L.nmx_heuristic_propose(cfgp, arena, s), "nmx_heuristic_propose")
             self.potential.evaluate(ev, s)
             check(L.nmx_heuristic_finish(cfgp, arena, int(at_init), s), "nmx_heuristic_finish")
             if int(self.view("counters")[1].item()) == 0:
                 return
         raise RuntimeError("find_reasonable_step_size did not terminate")
+
+    def _dense_momentum(self, eps, s):
+        """The search's momentum in whitened coordinates, p = T^T M^-1 eps = T^T T T^T eps:
+        the reference draws r = M^-1 eps (hmc_util.py:359, momentum_generator called with the
+        inverse mass matrix) and moves z by M^-1 r; with z = mu + T w that is w' = p = T^T r
+        and kinetic 0.5 r^T M^-1 r = 0.5 |p|^2.  Three device products (the pooled GEMMs or
+        the per-chain matvecs) on [D, ldc]."""
+        wt = self.potential.whitening
+        a, b = torch.empty_like(eps), torch.empty_like(eps)
+        if self.chain_dense:
+            for m, x, o in ((wt.bwd, eps, a), (wt.fwd, a, b), (wt.bwd, b, a)):
+                check(lib().nmx_chain_matvec(ptr(m), self.D, ptr(x), ptr(o), self.ldc, None, None, None, self.C, s),
+                      "nmx_chain_matvec")
+        else:
+            for fwd, x, o in ((False, eps, a), (True, a, b), (False, b, a)):
+                wt.product(fwd, ptr(x), ptr(o), None, None, None, self.C, self.ldc, s)
+        return a
+
+    def _search_at_window_end(self, e, cstart, thinning, S, fields, s):
+        """find_reasonable_step_size at the end of a middle window (hmc_util.py:619-626); the
+        transition that ended the window reports the searched step size, as its adapt_state
+        does in the reference (update_fn returns it, :700-705)."""
+        self._find_step_size(False, s)
+        slot = self._slot_of(e - 1, cstart, thinning, S)
+        if slot >= 0:
+            fields[slot, native.COLLECT.index("step_size"), :self.C] = self.view("step_size")[:self.C]
+
+    def _search_cuts(self, a, b):
+        """Window ends e in (a, b] at which the step-size search runs (sorted)."""
+        return [e for e in self._window_ends() if a < e <= b] if self._heuristic() else []
 
     def _window_ends(self):
         """First transition index after each middle adaptation window (hmc_util.py:596-635)."""
@@ -483,19 +514,14 @@ class Engine:
         cstart = it0 + start_idx
         if not self.dense:
             # with the step-size search, stop at every middle-window end it runs at
-            cuts = [e for e in self._window_ends() if it0 < e <= it0 + num_iters] if self._heuristic() else []
+            cuts = self._search_cuts(it0, it0 + num_iters)
             launches, a = 0, it0
-            for b in cuts + [it0 + num_iters]:
+            for b in sorted(set(cuts + [it0 + num_iters])):
                 if b > a:
                     launches += self._run_segment(a, b, seed, cstart, thinning, S, samples, fields, poll_every, s,
                                                   max_launches)
                 if b in cuts:
-                    self._find_step_size(False, s)
-                    # the transition that ended the window reports the searched step size, as
-                    # its adapt_state does in the reference (update_fn returns it, :700-705)
-                    slot = self._slot_of(b - 1, cstart, thinning, S)
-                    if slot >= 0:
-                        fields[slot, native.COLLECT.index("step_size"), :self.C] = self.view("step_size")[:self.C]
+                    self._search_at_window_end(b, cstart, thinning, S, fields, s)
                 a = b
         else:
             launches = self._run_dense(it0, it0 + num_iters, seed, cstart, thinning, S, samples, fields,
@@ -529,9 +555,16 @@ class Engine:
         launches = 0
         for a, b, win in self._dense_segments(it0, it1):
             if win is None:
-                launches += self._run_segment(a, b, seed, cstart, thinning, S, samples, fields, poll_every, s,
-                                              max_launches)
-                self._convert_slots(samples, self._slots_in(a, b, cstart, thinning, S), s)
+                # without mass adaptation the window ends still run the step-size search
+                cuts = self._search_cuts(a, b)
+                ends = sorted(set(cuts + [b]))
+                for p, q in zip([a] + ends[:-1], ends):
+                    if q > p:
+                        launches += self._run_segment(p, q, seed, cstart, thinning, S, samples, fields, poll_every,
+                                                      s, max_launches)
+                        self._convert_slots(samples, self._slots_in(p, q, cstart, thinning, S), s)
+                    if q in cuts:
+                        self._search_at_window_end(q, cstart, thinning, S, fields, s)
                 continue
             if self._pool is None or self._pool[0] != win:
                 self._pool = (win, ChainWelford(self.D, self.C, self.device) if self.chain_dense
@@ -566,6 +599,8 @@ class Engine:
                     cov, mean = pool.finalize(self.opts.regularize_mass_matrix)
                 self._pool = None
                 self._reexpress(cov, mean, s)
+                if self._heuristic():
+                    self._search_at_window_end(b, cstart, thinning, S, fields, s)
         return launches
 
     def _persistent_model(self):

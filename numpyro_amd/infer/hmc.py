@@ -204,9 +204,6 @@ class HMC(MCMCKernel):
                               "can't be adapted", stacklevel=2)
         if kinetic_fn is not None:
             raise NotImplementedError("custom kinetic_fn: the engine uses the Euclidean kinetic energy")
-        if find_heuristic_step_size and dense_mass:
-            raise NotImplementedError("find_heuristic_step_size with dense_mass: the search runs in model "
-                                      "coordinates, the dense engine in whitened ones")
         self._pooled = isinstance(dense_mass, PooledGroups)
         if isinstance(dense_mass, str):
             if dense_mass != "pooled":

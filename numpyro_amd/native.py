@@ -129,6 +129,8 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_heuristic_begin": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_heuristic_propose": (c_int, [_cfgp, c_vp, c_vp]),
     "nmx_heuristic_finish": (c_int, [_cfgp, c_vp, c_int, c_vp]),
+    "nmx_heuristic_noise": (c_int, [_cfgp, c_vp, c_vp, c_vp]),
+    "nmx_heuristic_propose_with": (c_int, [_cfgp, c_vp, c_vp, c_vp]),
     "nmx_nuts_run_small": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
     "nmx_nuts_run_wide": (c_int, [_cfgp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp]),
     "nmx_predict_logreg": (c_int, [c_vp, ctypes.c_int64, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp]),

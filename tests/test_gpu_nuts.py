@@ -661,6 +661,50 @@ def test_find_heuristic_step_size_matches_oracle(device, model, dim):
     assert moved > 0  # the search changed the initial step size of at least some chains
 
 
+@pytest.mark.parametrize("mass", ["adapted", "given"])
+@pytest.mark.parametrize("model,dim", [("diag_normal", 40), ("logreg", 55)])
+def test_find_heuristic_step_size_dense_matches_oracle(device, model, dim, mass):
+    """find_heuristic_step_size with dense_mass=True: the search runs in the engine's whitened
+    coordinates with momentum p = T^T M^-1 eps (the reference's r = M^-1 eps,
+    hmc_util.py:359) at init and after the window-end re-expression.  "adapted": per-chain
+    matrices from the window [75, 99] (searched at the new matrix, hmc_util.py:609-626);
+    "given": a fixed non-diagonal inverse_mass_matrix, adapt_mass_matrix=False (one shared
+    whitening; the window end still searches).  Oracle: the reference adapter with dense_mass,
+    fed the device's accept probabilities and draws, reproduces every transition's step size
+    (rtol 1e-5: a search mismatch would be a whole factor 2)."""
+    seed, C, W = 31, 64, 150
+    rs = np.random.RandomState(dim)
+    args, fm, ref, *_ = _fixed_step_case(model, dim, rs)
+    kw = {}
+    if mass == "given":
+        q = rs.randn(dim, dim) / np.sqrt(dim)
+        kw = dict(inverse_mass_matrix=(q @ q.T + 0.5 * np.eye(dim)).astype(np.float32), adapt_mass_matrix=False)
+    eng = NUTS(fm, find_heuristic_step_size=True, dense_mass=True, **kw).make_engine(C, args)
+    assert eng.chain_dense == (mass == "adapted")
+    eng.initialize(seed, W)
+    ss0 = eng.chain_state("step_size").cpu().numpy().copy()
+    z0 = eng.model_state()[0].cpu().numpy()
+    samples, fields, _ = eng.run(W, seed)
+    acc = fields[:, native.COLLECT.index("accept_prob"), :C].cpu().numpy().T
+    ss = fields[:, native.COLLECT.index("step_size"), :C].cpu().numpy().T
+    draws = samples[:, :, :C].cpu().numpy().transpose(2, 0, 1)
+    pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
+                              for v in ref.pe_grad(z))
+    changed = 0
+    for c in range(C):
+        o = H.NUTSOracle(pe_grad, dim, W, find_heuristic_step_size=True, dense_mass=True, **kw)
+        st = o.init(z0[c], seed, c)
+        np.testing.assert_allclose(ss0[c], st.adapt_state.step_size, rtol=1e-5, err_msg=f"chain {c} initial search")
+        wa = st.adapt_state
+        for t in range(W):
+            z = draws[c, t].astype(np.float32)
+            pe, g = pe_grad(z)
+            wa = o.wa_update(t, np.float32(acc[c, t]), H.IntegratorState(z, None, pe, g), wa)
+            np.testing.assert_allclose(ss[c, t], wa.step_size, rtol=1e-5, err_msg=f"chain {c} after transition {t}")
+        changed += int(ss[c, 99] != ss[c, 98])
+    assert np.any(ss0 != 1.0) and changed > 0
+
+
 @pytest.mark.parametrize("model,dim", [("diag_normal", 40), ("logreg", 55)])
 def test_find_heuristic_step_size_without_warmup(device, model, dim):
     """num_warmup = 0: wa_init still runs find_reasonable_step_size whenever adapt_step_size is
