@@ -362,8 +362,12 @@ __device__ __forceinline__ void x3_epi_pair(const f32x16& acc, const f32x4 (&yh4
   x3_epi_one(acc[r1], yh4[r1 >> 2][r1 & 3], res[r1], lin, prod[1]);
 }
 
+// a tile's U term (per lane, double); x3_epi_finish adds it to the running sum
+__device__ __forceinline__ double x3_epi_term(float lin, const float (&prod)[2]) {
+  return (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod[0] * prod[1]) * (double)LN2;
+}
 __device__ __forceinline__ void x3_epi_finish(float lin, const float (&prod)[2], double& pe) {
-  pe += (double)(0.5f * lin) * (double)LN2 + (double)__builtin_amdgcn_logf(prod[0] * prod[1]) * (double)LN2;
+  pe += x3_epi_term(lin, prod);
 }
 
 __device__ __forceinline__ void x3_epilogue(const f32x16& acc, const f32x4 (&yh4)[4], float (&res)[16], double& pe) {
@@ -417,8 +421,8 @@ __device__ __forceinline__ void x3_gemm2(const bf16x8* fr, const float (&res)[16
 // c1 and plane 1 from the h = 1 half of c0 (32 lanes = 512 bytes further).  Those reads'
 // columns 56..63 (zero in the plane pieces) then read the neighbouring half instead: they only
 // feed GEMM2 output rows >= 56 > D, which are never stored.  Columns < D read the same bytes.
-template <int KB, int DT, bool COMPACT = false>
-__device__ __forceinline__ void x3_gemm2_tr_load(const char* aslot, bf16x8 (&fb)[3][DT][2]) {
+template <int KB, int DT, bool COMPACT, int DTI>
+__device__ __forceinline__ void x3_tr_load_dt(const char* aslot, bf16x8 (&fb)[3][2]) {
   static_assert(KB >= 2 * DT, "the GEMM1 image must cover GEMM2's 32 DT columns");
   static_assert(!COMPACT || KB == 2 * DT, "compact slot: the last k-block is GEMM2's last column half");
   const int L = threadIdx.x & 63;
@@ -426,34 +430,50 @@ __device__ __forceinline__ void x3_gemm2_tr_load(const char* aslot, bf16x8 (&fb)
   const unsigned base0 = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)aslot) +
                          (q + 32 * (p >> 1) + 4 * h) * 16 + 8 * (p & 1);
 #pragma unroll
+  for (int plane = 0; plane < 3; ++plane) {
+    // byte offsets of the k-blocks 2 dt (g1 = 0) and 2 dt + 1 (g1 = 1) in the slot
+    constexpr int dt = DTI, kb0 = 2 * dt, kb1 = 2 * dt + 1;
+    int o0, o1;
+    if constexpr (COMPACT) {
+      o0 = x3_ai<KB, true>(plane, kb0) * 1024;
+      o1 = kb1 < KB - 1 ? x3_ai<KB, true>(plane, kb1) * 1024
+                        : (plane == 2 ? x3_ci<KB, true>(1) * 1024 : x3_ci<KB, true>(0) * 1024 + (plane == 1 ? 512 : 0));
+    } else {
+      o0 = (plane * KB + kb0) * 1024;
+      o1 = (plane * KB + kb1) * 1024;
+    }
+    const unsigned base = base0 + (g1 ? o1 : o0);
+#pragma unroll
+    for (int sidx = 0; sidx < 2; ++sidx) {
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      s4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                   : "=&v"(lo), "=&v"(hi)
+                   : "v"(base), "i"((16 * sidx) * 16), "i"((16 * sidx + 8) * 16));
+      const s4 lh[2] = {lo, hi};
+      bf16x8 f;
+      __builtin_memcpy(&f, lh, 16);
+      fb[plane][sidx] = f;
+    }
+  }
+}
+template <int KB, int DT, bool COMPACT = false>
+__device__ __forceinline__ void x3_gemm2_tr_load(const char* aslot, bf16x8 (&fb)[3][DT][2]) {
+  bf16x8 f0[3][2];
+  x3_tr_load_dt<KB, DT, COMPACT, 0>(aslot, f0);
+#pragma unroll
   for (int plane = 0; plane < 3; ++plane)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      // byte offsets of the k-blocks 2 dt (g1 = 0) and 2 dt + 1 (g1 = 1) in the slot
-      const int kb0 = 2 * dt, kb1 = 2 * dt + 1;
-      int o0, o1;
-      if constexpr (COMPACT) {
-        o0 = x3_ai<KB, true>(plane, kb0) * 1024;
-        o1 = kb1 < KB - 1 ? x3_ai<KB, true>(plane, kb1) * 1024
-                          : (plane == 2 ? x3_ci<KB, true>(1) * 1024 : x3_ci<KB, true>(0) * 1024 + (plane == 1 ? 512 : 0));
-      } else {
-        o0 = (plane * KB + kb0) * 1024;
-        o1 = (plane * KB + kb1) * 1024;
-      }
-      const unsigned base = base0 + (g1 ? o1 : o0);
+    for (int sidx = 0; sidx < 2; ++sidx) fb[plane][0][sidx] = f0[plane][sidx];
+  if constexpr (DT > 1) {
+    bf16x8 f1[3][2];
+    x3_tr_load_dt<KB, DT, COMPACT, (DT > 1 ? 1 : 0)>(aslot, f1);
 #pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        typedef short s4 __attribute__((ext_vector_type(4)));
-        s4 lo, hi;
-        asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
-                     : "=&v"(lo), "=&v"(hi)
-                     : "v"(base), "i"((16 * sidx) * 16), "i"((16 * sidx + 8) * 16));
-        const s4 lh[2] = {lo, hi};
-        bf16x8 f;
-        __builtin_memcpy(&f, lh, 16);
-        fb[plane][dt][sidx] = f;
-      }
-    }
+    for (int plane = 0; plane < 3; ++plane)
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) fb[plane][1][sidx] = f1[plane][sidx];
+  }
+  static_assert(DT <= 2, "x3_gemm2_tr_load: DT <= 2");
 }
 template <int DT>
 __device__ __forceinline__ void x3_tr_wait(bf16x8 (&fb)[3][DT][2]) {
@@ -788,6 +808,66 @@ __device__ __forceinline__ void x3_roles_barrier_rt(int n) {  // n wave-uniform
   }
 }
 
+// Role A's tile: GEMM1 of the next tile (fa, into nxt) hand-interleaved with the epilogue of
+// the current one (acc -> res, lin, prod)
+template <int KB, int H, bool CMP>
+__device__ __forceinline__ void x3_a_tile(const bf16x8* fa, const bf16x8 (&z1)[KB], const bf16x8 (&z2)[KB],
+                                          const bf16x8 (&z3)[KB], const f32x16& acc, const f32x4 (&y4)[4],
+                                          f32x16& nxt, float (&res)[16], float& lin, float (&prod)[2]) {
+  // hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with row
+  // pairs of tile k's epilogue; sched_barrier(0) pins the order; the operations and their
+  // per-value order equal x3_gemm1 / x3_epilogue (bitwise equal results)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
+  bf16x8 a1 = fa[x3_ai<KB, CMP>(0, 0) * 64], a2 = fa[x3_ai<KB, CMP>(1, 0) * 64],
+         a3 = fa[x3_ai<KB, CMP>(2, 0) * 64];
+#pragma unroll
+  for (int kb = 0; kb < KB - H; ++kb) {
+    bf16x8 n1, n2, n3;
+    if (kb + 1 < KB - H) {
+      n1 = fa[x3_ai<KB, CMP>(0, kb + 1) * 64];
+      n2 = fa[x3_ai<KB, CMP>(1, kb + 1) * 64];
+      n3 = fa[x3_ai<KB, CMP>(2, kb + 1) * 64];
+    } else if (H && kb + 1 == KB - 1) {  // the combined pieces (a1 | a2), (a3 | a1)
+      n1 = fa[x3_ci<KB, CMP>(0) * 64];
+      n2 = fa[x3_ci<KB, CMP>(1) * 64];
+    }
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
+    x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
+    x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kb + 1 < KB - H) {
+      a1 = n1;
+      a2 = n2;
+      a3 = n3;
+    } else if (H && kb + 1 == KB - 1) {
+      a1 = n1;
+      a2 = n2;
+    }
+  }
+  if constexpr (H) {  // x3_gemm1's combined products (a1 = (a1 | a2), a2 = (a3 | a1) here)
+    constexpr int kb = KB - 1;
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z3[kb], nxt, 0, 0, 0);
+    x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
+    x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
+    __builtin_amdgcn_sched_barrier(0);
+    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 constexpr int X3_ROLE_WAVES = 8;
 // Prefetch depth: tile k + PA is issued in iteration k, and the barrier of iteration k waits
 // only for the DMAs of the tile pair it needs (A(k+1), labels(k)), leaving the later PA - 2
@@ -824,6 +904,265 @@ inline size_t x3_roles_lds_bytes() {
   return (size_t)(x3_roles_aslots<PA>() * NA + (PA + 1)) * 1024 + (size_t)2 * 4 * 4096;
 }
 
+// ---- narrow tail: launches over at most 32 listed chains ----------------------------------
+// The common case of a NUTS run's straggler phase is one chain tile (<= 32 chains).  The role
+// split above then keeps two SIMDs busy (the tile's A and B waves), its per-tile critical path
+// GEMM1 + epilogue on one wave and both GEMM2 column halves plus the residual split on another,
+// one barrier per tile (0.78 us a tile).  Here the one chain tile runs as a three-stage pipeline
+// over tile pairs, one barrier per pair:
+//   role A, waves 2 and 3 (SIMDs 2, 3): the tiles of a split alternately -- GEMM1 of tile
+//     2k+2+a hand-interleaved with the epilogue of tile 2k+a, exactly x3_a_tile -- residual R and
+//     U term to LDS (iteration k);
+//   split, waves 4 and 5 (SIMDs 0, 1): the residual of tile 2(k-1)+j split into its three bf16
+//     terms (iteration k), beside the role-B wave of their SIMD, which is MFMA-bound;
+//   role B, waves 0 and 1 (SIMDs 0, 1): GEMM2 for one 32-column half dt each, over every tile in
+//     tile order (pair k-2 in iteration k), wave 0 also adds the tiles' U terms in tile order;
+//   every LDS-DMA on waves 4-7 (s_memtime stamps of an experiment build: a 1-KB piece costs its
+//     issuing wave ~160 cycles, on the A / B waves the critical path).
+// Every accumulator sees x3_item's products in x3_item's order, the split is split3 of the same
+// values: bitwise the results of the other forms.  Compact image (H) only.  LDS (159 KB): images
+// of five tile pairs (k-2 in GEMM2, k-1 and k kept for it, k+1 in GEMM1, k+2 landing), labels of
+// two, residuals + terms and split residuals + terms of two pairs each.
+template <int KB, int H>
+inline size_t x3_narrow_lds_bytes() {
+  constexpr int NA = x3_roles_na<KB, H>();
+  return (size_t)(10 * NA + 4) * 1024 + 2 * 2 * (4096 + 512) + 2 * 2 * (6144 + 512);
+}
+
+// role B's operands of one tile, issued without a wait: the transposed X^T reads of column half
+// DTI, the split residual (terms t of k-steps s at (3 s + t) KB) and (TERM) the tile's U term
+template <int KB, int DT, bool CMP, int DTI, bool TERM>
+__device__ __forceinline__ void x3_narrow_b_issue(const char* slot, const char* sbase, const char* tbase,
+                                                  bf16x8 (&fb)[3][2], bf16x8 (&r)[2][3], double& term) {
+  x3_tr_load_dt<KB, DT, CMP, DTI>(slot, fb);
+  const unsigned sa = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)sbase);
+  asm volatile(
+      "ds_read_b128 %0, %6\n\t"
+      "ds_read_b128 %1, %6 offset:1024\n\t"
+      "ds_read_b128 %2, %6 offset:2048\n\t"
+      "ds_read_b128 %3, %6 offset:3072\n\t"
+      "ds_read_b128 %4, %6 offset:4096\n\t"
+      "ds_read_b128 %5, %6 offset:5120"
+      : "=&v"(r[0][0]), "=&v"(r[0][1]), "=&v"(r[0][2]), "=&v"(r[1][0]), "=&v"(r[1][1]), "=&v"(r[1][2])
+      : "v"(sa)
+      : "memory");
+  if constexpr (TERM) {
+    const unsigned ta = (unsigned)(size_t)((__attribute__((address_space(3))) const char*)tbase);
+    asm volatile("ds_read_b64 %0, %1" : "=&v"(term) : "v"(ta) : "memory");
+  }
+}
+// wait for them; the empty asm makes every later use depend on the wait
+__device__ __forceinline__ void x3_narrow_b_wait(bf16x8 (&fb)[3][2], bf16x8 (&r)[2][3], double& term) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+    for (int sidx = 0; sidx < 2; ++sidx) asm volatile("" : "+v"(fb[pl][sidx]), "+v"(r[sidx][pl]));
+  asm volatile("" : "+v"(term));
+}
+// the tile's 12 GEMM2 MFMAs of one column half, in x3_gemm2's order
+__device__ __forceinline__ void x3_narrow_b_mma(const bf16x8 (&fb)[3][2], const bf16x8 (&r)[2][3], f32x16& g) {
+#pragma unroll
+  for (int sidx = 0; sidx < 2; ++sidx) {
+    const bf16x8 b1 = fb[0][sidx], b2 = fb[1][sidx], b3 = fb[2][sidx];
+    const bf16x8 r1 = r[sidx][0], r2 = r[sidx][1], r3 = r[sidx][2];
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b3, r1, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r2, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r3, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, r1, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r2, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, r1, g, 0, 0, 0);
+  }
+}
+
+template <int KB, int DT, int H>
+__device__ __forceinline__ void x3_narrow(const char* __restrict__ Xq, int64_t ntiles, int D, int S, int split,
+                                          const nmx_eval_batch& ev, float* __restrict__ gpart,
+                                          double* __restrict__ pepart, char* lds) {
+  constexpr int NP = 3 * KB + 2 * H + 6 * DT + 1, NA = x3_roles_na<KB, H>();
+  constexpr bool CMP = H != 0;
+  constexpr int NIMG = 10, NLAB = 4;  // tile slots: 5 image pairs, 2 label pairs
+  constexpr int NQ = 2 * NA + 2;      // DMA pieces of a pair: the images of two tiles, their labels
+  static_assert(DT == 2 && H == 1 && X3_ROLE_WAVES == 8, "narrow tail: compact image, two column halves, 8 waves");
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l31 = lane & 31;
+  const int ldc = ev.ldc;
+  const int pos = l31;  // the chain tile 0 (ldc >= 64)
+  const int c = nmx_eval_chain(ev, pos);
+  const int64_t per = (ntiles + S - 1) / S;
+  const int64_t t0 = min((int64_t)split * per, ntiles);
+  const int64_t t1 = min(t0 + per, ntiles);
+  const int nt = (int)(t1 - t0);
+  const int npairs = (nt + 1) / 2;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Xq + (size_t)t0 * NP * 1024), 0, (int)((size_t)nt * NP * 1024), 0x00020000);
+  char* iring = lds;                         // [tile % NIMG][NA KB]
+  char* lring = iring + NIMG * NA * 1024;    // [tile % NLAB][1 KB]
+  char* rring = lring + NLAB * 1024;         // [pair parity][j][4 KB] residuals
+  char* tring = rring + 2 * 2 * 4096;        // [pair parity][j][512 B] their U terms
+  char* sring = tring + 2 * 2 * 512;         // [pair parity][j][6 KB] split residuals
+  char* uring = sring + 2 * 2 * 6144;        // [pair parity][j][512 B] their U terms
+  const bool helper = w >= 4;
+  const int hw = w - 4;
+  // DMA pair p = the images of tile pair p + 1 and the labels of pair p; its piece q (images: q
+  // = j NA + il for tile j of the pair and slot position il; labels: q = 2 NA + j) is issued by
+  // helper wave q mod 4.  Iteration k needs pair k, issued in iteration k - 1 (all of it: the
+  // barrier waits vmcnt(0)).
+  auto issue_q = [&](int p, int q) {
+    if (q < 2 * NA) {
+      const int j = q / NA, il = q % NA, tile = 2 * (p + 1) + j;
+      if (tile < nt) {
+        const int i = il < 3 * (KB - 1) ? (il / (KB - 1)) * KB + il % (KB - 1) : 3 * KB + (il - 3 * (KB - 1));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xrs, (__attribute__((address_space(3))) void*)(iring + (tile % NIMG) * NA * 1024 + il * 1024), 16,
+            lane * 16, (unsigned)((tile * NP + i) * 1024), 0, 0);
+      }
+    } else {
+      const int tile = 2 * p + (q - 2 * NA);
+      if (tile < nt)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xrs, (__attribute__((address_space(3))) void*)(lring + (tile % NLAB) * 1024), 16, lane * 16,
+            (unsigned)((tile * NP + NP - 1) * 1024), 0, 0);
+    }
+  };
+  auto issue_pair = [&](int p) {
+    if (!helper) return;
+#pragma unroll
+    for (int jj = 0; jj < (NQ + 3) / 4; ++jj) {
+      const int q = hw + 4 * jj;
+      if (q < NQ) issue_q(p, q);
+    }
+  };
+  const bool roleA = w == 2 || w == 3;
+  // a tile's index within a pair is w & 1 for the A, split and B waves alike (w - 2 / w - 4 here
+  // let the compiler merge the A and split waves' LDS addresses with a form valid for one only)
+  const int a = w & 1;
+  bf16x8 z1[KB], z2[KB], z3[KB];
+  if (roleA) {
+    const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc((void*)ev.z, 0, D * ldc * 4, 0x00020000);
+    x3_load_z<KB, H>(zrs, c, h, ldc, z1, z2, z3);
+  }
+  f32x16 g;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) g[r] = 0.0f;
+  double pe = 0.0;
+  if (nt > 0) {
+    if (helper) {  // the images of pair 0
+#pragma unroll
+      for (int jj = 0; jj < (2 * NA + 3) / 4; ++jj) {
+        const int q = hw + 4 * jj;
+        if (q < 2 * NA) issue_q(-1, q);
+      }
+    }
+    x3_roles_barrier();  // the images of pair 0 are in
+    issue_pair(0);
+    f32x16 accA, accB;
+    if (roleA) accA = x3_gemm1<KB, H, CMP>(reinterpret_cast<const bf16x8*>(iring + (a % NIMG) * NA * 1024) + lane, z1,
+                                           z2, z3);
+    auto iter = [&](int k, const f32x16& acc, f32x16& nxt) {
+      x3_roles_barrier();  // DMA pair k landed; R(k - 1), SR(k - 2) written; pair k - 3's slots read
+      issue_pair(k + 1);
+      if (roleA) {
+        const int i = 2 * k + a;
+        if (k < npairs && i < nt) {
+          f32x4 y4[4];
+          x3_labels(lring + (i % NLAB) * 1024, h, y4);
+          x3_labels_wait(y4);
+          // GEMM1 of this wave's next tile i + 2 (a stale slot past the last tile: computed, never used)
+          const bf16x8* fa = reinterpret_cast<const bf16x8*>(iring + ((i + 2) % NIMG) * NA * 1024) + lane;
+          float res[16];
+          float lin = 0.0f;
+          float prod[2] = {1.0f, 1.0f};
+          x3_a_tile<KB, H, CMP>(fa, z1, z2, z3, acc, y4, nxt, res, lin, prod);
+          const double term = x3_epi_term(lin, prod);
+          x3_res_store(rring + ((k & 1) * 2 + a) * 4096 + lane * 16, res);
+          const unsigned ta =
+              (unsigned)(size_t)((__attribute__((address_space(3))) char*)(tring + ((k & 1) * 2 + a) * 512)) + lane * 8;
+          asm volatile("ds_write_b64 %0, %1" ::"v"(ta), "v"(term) : "memory");
+        }
+      } else if (w == 4 || w == 5) {
+        const int j = w & 1, i = 2 * (k - 1) + j, par = (k - 1) & 1;
+        if (k >= 1 && k <= npairs && i < nt) {  // split R(i): the residual's three bf16 terms per k-step
+          float res[16];
+          x3_res_load(rring + (par * 2 + j) * 4096 + lane * 16, res);
+          const unsigned ta =
+              (unsigned)(size_t)((__attribute__((address_space(3))) char*)(tring + (par * 2 + j) * 512)) + lane * 8;
+          double term;
+          asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(term) : "v"(ta) : "memory");
+          bf16x8 r[2][3];
+#pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) v[jj] = res[8 * sidx + jj];
+            split3(v, r[sidx][0], r[sidx][1], r[sidx][2]);
+          }
+          const unsigned sa =
+              (unsigned)(size_t)((__attribute__((address_space(3))) char*)(sring + (par * 2 + j) * 6144)) + lane * 16;
+          asm volatile(
+              "ds_write_b128 %0, %1\n\t"
+              "ds_write_b128 %0, %2 offset:1024\n\t"
+              "ds_write_b128 %0, %3 offset:2048\n\t"
+              "ds_write_b128 %0, %4 offset:3072\n\t"
+              "ds_write_b128 %0, %5 offset:4096\n\t"
+              "ds_write_b128 %0, %6 offset:5120" ::"v"(sa),
+              "v"(r[0][0]), "v"(r[0][1]), "v"(r[0][2]), "v"(r[1][0]), "v"(r[1][1]), "v"(r[1][2])
+              : "memory");
+          const unsigned ua =
+              (unsigned)(size_t)((__attribute__((address_space(3))) char*)(uring + (par * 2 + j) * 512)) + lane * 8;
+          asm volatile("ds_write_b64 %0, %1" ::"v"(ua), "v"(term) : "memory");
+        }
+      } else if (w < 2 && k >= 2) {
+        const int i0 = 2 * (k - 2), par = k & 1;  // (k - 2) & 1
+        const bool two = i0 + 1 < nt;
+        bf16x8 fb0[3][2], fb1[3][2], r0[2][3], r1[2][3];
+        double u0 = 0.0, u1 = 0.0;
+        // both tiles' operands at once (a missing second tile's slots are valid LDS: its MFMAs
+        // run on whatever they hold and are dropped)
+        if (w == 0) {
+          x3_narrow_b_issue<KB, DT, CMP, 0, true>(iring + (i0 % NIMG) * NA * 1024,
+                                                  sring + (par * 2) * 6144 + lane * 16,
+                                                  uring + (par * 2) * 512 + lane * 8, fb0, r0, u0);
+          x3_narrow_b_issue<KB, DT, CMP, 0, true>(iring + ((i0 + 1) % NIMG) * NA * 1024,
+                                                  sring + (par * 2 + 1) * 6144 + lane * 16,
+                                                  uring + (par * 2 + 1) * 512 + lane * 8, fb1, r1, u1);
+        } else {
+          x3_narrow_b_issue<KB, DT, CMP, 1, false>(iring + (i0 % NIMG) * NA * 1024,
+                                                   sring + (par * 2) * 6144 + lane * 16, nullptr, fb0, r0, u0);
+          x3_narrow_b_issue<KB, DT, CMP, 1, false>(iring + ((i0 + 1) % NIMG) * NA * 1024,
+                                                   sring + (par * 2 + 1) * 6144 + lane * 16, nullptr, fb1, r1, u1);
+        }
+        x3_narrow_b_wait(fb0, r0, u0);
+        x3_narrow_b_wait(fb1, r1, u1);
+        x3_narrow_b_mma(fb0, r0, g);
+        f32x16 g1 = g;
+        x3_narrow_b_mma(fb1, r1, g1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) g[r] = two ? g1[r] : g[r];
+        if (w == 0) {
+          pe += u0;
+          if (two) pe += u1;
+        }
+      }
+    };
+    for (int k = 0; k <= npairs + 1; k += 2) {
+      iter(k, accA, accB);
+      if (k + 1 <= npairs + 1) iter(k + 1, accB, accA);
+    }
+  }
+  if (w >= 2 || pos >= ldc) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int d = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (d < D) gpart[((size_t)split * D + d) * ldc + pos] = g[r];
+  }
+  if (w == 0) {
+    const double p = pe + __shfl_xor(pe, 32);
+    if (h == 0) pepart[(size_t)split * ldc + pos] = p;
+  }
+}
+
 template <int KB, int DT, int H, int PA>
 __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const char* __restrict__ Xq,
                                                                          int64_t ntiles, int D, int S, int Gt,
@@ -841,6 +1180,12 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
   const int npos = ev.active_idx ? *ev.active_count : ev.ldc;
   if (ct * 128 >= npos) return;
   const int split = (qb / Gt) * 8 + (b & 7);
+  if (npos <= 32) {  // one chain tile: the narrow form (ct = 0 here)
+    if constexpr (DT == 2 && H == 1) {
+      x3_narrow<KB, DT, H>(Xq, ntiles, D, S, split, ev, gpart, pepart, lds);
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool roleA = w < 4;
@@ -925,60 +1270,9 @@ __global__ __launch_bounds__(64 * X3_ROLE_WAVES, 1) void k_logreg_x3_roles(const
         x3_labels_wait(y4);
         const bf16x8* fa = reinterpret_cast<const bf16x8*>(aring + ((k + 1) % PAS) * NA * 1024) + lane;
         float res[16];
-        // hand-interleaved (in-order issue within a wave): GEMM1(k+1)'s MFMAs alternate with row
-        // pairs of tile k's epilogue; sched_barrier(0) pins the order; the operations and their
-        // per-value order equal x3_gemm1 / x3_epilogue (bitwise equal results)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) nxt[r] = 0.0f;
         float lin = 0.0f;
         float prod[2] = {1.0f, 1.0f};
-        bf16x8 a1 = fa[x3_ai<KB, CMP>(0, 0) * 64], a2 = fa[x3_ai<KB, CMP>(1, 0) * 64],
-               a3 = fa[x3_ai<KB, CMP>(2, 0) * 64];
-#pragma unroll
-        for (int kb = 0; kb < KB - H; ++kb) {
-          bf16x8 n1, n2, n3;
-          if (kb + 1 < KB - H) {
-            n1 = fa[x3_ai<KB, CMP>(0, kb + 1) * 64];
-            n2 = fa[x3_ai<KB, CMP>(1, kb + 1) * 64];
-            n3 = fa[x3_ai<KB, CMP>(2, kb + 1) * 64];
-          } else if (H && kb + 1 == KB - 1) {  // the combined pieces (a1 | a2), (a3 | a1)
-            n1 = fa[x3_ci<KB, CMP>(0) * 64];
-            n2 = fa[x3_ci<KB, CMP>(1) * 64];
-          }
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, z1[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z2[kb], nxt, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z3[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z1[kb], nxt, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (kb + 1 < KB - H) {
-            a1 = n1;
-            a2 = n2;
-            a3 = n3;
-          } else if (H && kb + 1 == KB - 1) {
-            a1 = n1;
-            a2 = n2;
-          }
-        }
-        if constexpr (H) {  // x3_gemm1's combined products (a1 = (a1 | a2), a2 = (a3 | a1) here)
-          constexpr int kb = KB - 1;
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, z3[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb, res, lin, prod);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z2[kb], nxt, 0, 0, 0);
-          x3_epi_pair(acc, y4, 2 * kb + 1, res, lin, prod);
-          __builtin_amdgcn_sched_barrier(0);
-          nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, z1[kb], nxt, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        x3_a_tile<KB, H, CMP>(fa, z1, z2, z3, acc, y4, nxt, res, lin, prod);
         x3_epi_finish(lin, prod, pe);
         x3_res_store(rmine + (k & 1) * 4 * 4096, res);
       };
@@ -1177,12 +1471,21 @@ extern "C" int nmx_logreg_pe_grad(const void* packed, int64_t n_rows, int dim, c
   const int nb = std::min(ev->num_chains, ev->ldc);  // batch positions that can hold a chain
   const int Gt = (nb + 127) / 128;
   const dim3 grid(Gt * S), blk(256);
-  if (KB == 4 && Gt <= X3_TAIL_TILES && H)
-    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 1, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
-                       (x3_roles_lds_bytes<4, 2, 1, X3_ROLE_PA>()), s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
-  else if (KB == 4 && Gt <= X3_TAIL_TILES)
-    hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 0, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES),
-                       (x3_roles_lds_bytes<4, 2, 0, X3_ROLE_PA>()), s, Xq, nt, dim, S, Gt, *ev, gpart, pepart);
+  if (KB == 4 && Gt <= X3_TAIL_TILES) {
+    // the role-split form, or (compact image) the narrow one (<= 32 listed chains, decided in the
+    // kernel): LDS for either
+    const size_t lds = H ? std::max(x3_roles_lds_bytes<4, 2, 1, X3_ROLE_PA>(), x3_narrow_lds_bytes<4, 1>())
+                         : x3_roles_lds_bytes<4, 2, 0, X3_ROLE_PA>();
+    const void* fn = H ? (const void*)k_logreg_x3_roles<4, 2, 1, X3_ROLE_PA>
+                       : (const void*)k_logreg_x3_roles<4, 2, 0, X3_ROLE_PA>;
+    if (int st = nmx_lds_limit(fn, lds, s, "k_logreg_x3_roles")) return st;
+    if (H)
+      hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 1, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES), lds, s, Xq, nt,
+                         dim, S, Gt, *ev, gpart, pepart);
+    else
+      hipLaunchKernelGGL((k_logreg_x3_roles<4, 2, 0, X3_ROLE_PA>), grid, dim3(64 * X3_ROLE_WAVES), lds, s, Xq, nt,
+                         dim, S, Gt, *ev, gpart, pepart);
+  }
   else if (KB == 4 && H)
     hipLaunchKernelGGL((k_logreg_x3<4, 2, 1, 3, 0>), grid, blk, (x3_lds_bytes<4, 2, 1>()), s, Xq, nt, dim, S, Gt,
                        *ev, gpart, pepart);

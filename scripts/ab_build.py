@@ -21,7 +21,8 @@ for spec in sys.argv[2:]:
         src_v = os.path.abspath(path)
     else:
         src_v = src
-    out = os.path.join(ROOT, "build", "ab", name)
+    # AB_DIR: a directory the GPU snapshot carries (build/ab itself is gpurun-ignored)
+    out = os.path.join(ROOT, "build", os.environ.get("AB_DIR", "ab"), name)
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, os.path.basename(src) + ".o")
     cmd = [B.HIPCC, *B.COMMON_FLAGS, *B.FILE_FLAGS.get(os.path.basename(src), ()), "-DNMX_EXPERIMENT",

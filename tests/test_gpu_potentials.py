@@ -125,6 +125,52 @@ def test_logreg_tail_forms_are_bitwise_the_full_kernel(device, n_rows):
         np.testing.assert_allclose(g_a[:8], g_r, rtol=1e-3, atol=1e-2)
 
 
+def _eval_list(pot, Z, idx, device):
+    """The potential of the chains idx (a compacted active list, count = len(idx)) inside a
+    batch of every chain of Z, as the NUTS loop evaluates them: U / dU at the chains' columns."""
+    import torch
+
+    from numpyro_amd import native
+
+    C, D = Z.shape
+    ldc = (C + 63) // 64 * 64
+    pot.bind(C, ldc, device)
+    z = torch.zeros(D, ldc, device=device)
+    z[:, :C] = torch.from_numpy(Z.T.astype(np.float32)).to(device)
+    g = torch.full((D, ldc), float("nan"), device=device)
+    pe = torch.full((ldc,), float("nan"), device=device)
+    lst = torch.zeros(ldc, dtype=torch.int32, device=device)
+    lst[:len(idx)] = torch.as_tensor(np.asarray(idx, np.int32), device=device)
+    cnt = torch.tensor([len(idx)], dtype=torch.int32, device=device)
+    ev = native.EvalBatch(z=native.ptr(z), grad=native.ptr(g), pe=native.ptr(pe), active_idx=native.ptr(lst),
+                          active_count=native.ptr(cnt), num_chains=len(idx), ldc=ldc)
+    pot.evaluate(ev, native.stream_ptr())
+    torch.cuda.synchronize()
+    return pe[idx].cpu().numpy().astype(np.float64), g[:, idx].cpu().numpy().T.astype(np.float64)
+
+
+@pytest.mark.parametrize("n_rows", [4001, 70001, 581012])
+def test_logreg_listed_tail_forms_are_bitwise_the_full_kernel(device, n_rows):
+    """Compacted lists of <= 32 chains (the narrow form: one chain tile on four waves), 33-256
+    chains (the role-split form) and a wide list (the full kernel's early-exit groups): every
+    listed chain's U / dU bitwise equal to the full kernel's over the whole batch, for scattered
+    chain indices and ragged row counts (short last split, odd tile counts)."""
+    from numpyro_amd.potentials import LogisticRegression
+
+    rs = np.random.RandomState(n_rows % 997)
+    X = rs.randn(n_rows, 55).astype(np.float32)
+    y = (rs.rand(n_rows) < 0.4).astype(np.float32)
+    Z = rs.randn(300, 55).astype(np.float32) * 0.05
+    pot = LogisticRegression(X, y)
+    pe_a, g_a = _eval(pot, Z, device)
+    perm = rs.permutation(300)
+    for n in (1, 7, 32, 33, 200, 300):
+        idx = np.sort(perm[:n]) if n % 2 else perm[:n]
+        pe_b, g_b = _eval_list(pot, Z, idx, device)
+        np.testing.assert_array_equal(pe_a[idx], pe_b, err_msg=f"{n} listed chains")
+        np.testing.assert_array_equal(g_a[idx], g_b, err_msg=f"{n} listed chains")
+
+
 def test_eight_schools_matches_oracle(device):
     from numpyro_amd.potentials import EightSchools
 
