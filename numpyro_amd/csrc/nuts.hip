@@ -144,7 +144,29 @@ struct StepArgs {
 // Must be reached by every thread of the block.
 template <int NV, int CPW, int N>
 __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, int cl) {
-  if constexpr (NV > 1) {
+  if constexpr (NV >= 8) {
+    // the block's NV x CPW threads share the N x CPW sums (each over the NV partials in slice
+    // order, as below), then every thread reads its chain's totals: NV + N LDS reads per thread
+    // instead of N x NV (the fused covtype step, NV = 32, N = 23: 55 instead of 736, which made
+    // the reduction ~25k cycles of a ~30k-cycle tail-launch block -- s_memtime stamps).  Same
+    // order, bitwise the same sums.  lds holds N x NV x CPW partials + N x CPW totals.
+    constexpr int NT = NV * CPW;
+#pragma unroll
+    for (int i = 0; i < N; ++i) lds[(i * NV + vw) * CPW + cl] = v[i];
+    __syncthreads();
+    float* const tot = lds + N * NV * CPW;
+    for (int o = threadIdx.x; o < N * CPW; o += NT) {
+      const int i = o / CPW, c = o % CPW;
+      float s = 0.0f;
+#pragma unroll 8
+      for (int w = 0; w < NV; ++w) s += lds[(i * NV + w) * CPW + c];
+      tot[o] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = tot[i * CPW + cl];
+    // the next call writes the partials only, and reads them after its first barrier
+  } else if constexpr (NV > 1) {
 #pragma unroll
     for (int i = 0; i < N; ++i) lds[(i * NV + vw) * CPW + cl] = v[i];
     __syncthreads();
@@ -1103,7 +1125,7 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
 
 template <int TPC, int CPW>
 __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
-  __shared__ float lds[TPC * 64 / CPW > 1 ? NPART * TPC * 64 : 1];
+  __shared__ float lds[TPC * 64 / CPW > 1 ? NPART * TPC * 64 + NPART * CPW : 1];
   fused_step<TPC, CPW, true, const StepArgs>(P, lds);
 }
 
