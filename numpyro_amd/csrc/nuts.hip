@@ -142,6 +142,11 @@ struct StepArgs {
 // Fixed-order sum of N partials over the NV "virtual waves" of a block that hold the same
 // chain (virtual wave vw = wave * SUBS + sub, chain slot cl = lane % CPW; all get the total).
 // Must be reached by every thread of the block.
+// workgroup barrier ordering LDS accesses only (global memory operations may stay in flight)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int NV, int CPW, int N>
 __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, int cl) {
   if constexpr (NV >= 8) {
@@ -150,10 +155,14 @@ __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, in
     // instead of N x NV (the fused covtype step, NV = 32, N = 23: 55 instead of 736, which made
     // the reduction ~25k cycles of a ~30k-cycle tail-launch block -- s_memtime stamps).  Same
     // order, bitwise the same sums.  lds holds N x NV x CPW partials + N x CPW totals.
+    // LDS-only barriers: __syncthreads' workgroup fence would first wait for every global store
+    // the leaf / apply rows issued (vmcnt(0): a store round trip per barrier); no thread of the
+    // launched step reads global data another thread wrote in the same launch (a chain's lanes
+    // own their rows in both row phases), so only the LDS partials need ordering
     constexpr int NT = NV * CPW;
 #pragma unroll
     for (int i = 0; i < N; ++i) lds[(i * NV + vw) * CPW + cl] = v[i];
-    __syncthreads();
+    lds_barrier();
     float* const tot = lds + N * NV * CPW;
     for (int o = threadIdx.x; o < N * CPW; o += NT) {
       const int i = o / CPW, c = o % CPW;
@@ -162,7 +171,7 @@ __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, in
       for (int w = 0; w < NV; ++w) s += lds[(i * NV + w) * CPW + c];
       tot[o] = s;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = tot[i * CPW + cl];
     // the next call writes the partials only, and reads them after its first barrier
@@ -1081,11 +1090,15 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
   float red[NPART];
 #pragma unroll
   for (int i = 0; i < NPART; ++i) red[i] = 0.0f;
+// two rows per load round in the leaf and apply phases (a lane holds <= 2 rows at D <= 64):
+// every row's loads go out before the first row's stores, whose completion the next row's
+// loads would otherwise wait for (vmcnt counts stores and loads in issue order); step kernel
+// p50 21.0 -> 19.9 us in the 512-chain covtype protocol, bitwise the same draws (round 5)
 #ifndef NMX_STEP_LROWS
-#define NMX_STEP_LROWS 1
+#define NMX_STEP_LROWS 2
 #endif
 #ifndef NMX_STEP_AROWS
-#define NMX_STEP_AROWS 1
+#define NMX_STEP_AROWS 2
 #endif
   constexpr int LROWS = TPC > 1 ? (NMX_STEP_LROWS == 2 ? 2 : 1) : 1;
   constexpr bool LPRE = TPC > 1 && NMX_STEP_LROWS >= 1;

@@ -1368,10 +1368,14 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void k_logreg_finalize(const float*
   const int ldc = ev.ldc;
   const int sp0 = w * S / FIN_WAVES, sp1 = (w + 1) * S / FIN_WAVES;
   // the U row's z loads (wave 0) go out before the slot sums: one dependent round less
+  // (clamped rows, masked after: a load under `k < D` compiled to 55 branches, each with its own
+  // vmcnt(0) wait -- one dependent round per coordinate, ~14 us of a tail launch's finalize)
   float zf[64];
   if (d == D && w == 0 && c >= 0) {
 #pragma unroll
-    for (int k = 0; k < 64; ++k) zf[k] = k < D ? ev.z[(size_t)k * ldc + c] : 0.0f;
+    for (int k = 0; k < 64; ++k) zf[k] = ev.z[(size_t)(k < D ? k : D - 1) * ldc + c];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) zf[k] = k < D ? zf[k] : 0.0f;
   }
   if (c >= 0) {
     if (d < D) part[w][lane] = sum_slots(gpart + (size_t)d * ldc + pos, (size_t)D * ldc, sp0, sp1);

@@ -32,10 +32,11 @@ def show(tag):
     nb = (C + 15) // 16
     st = st[:nb].astype(np.float64)
     d = np.diff(st[:, :8], axis=1)
-    leaf = (st[:, 8].astype(np.int64) & 1) == 1
+    leaf = st[:, 8] > 0  # the block evaluated a leaf in the recorded launch
     rt = (st[:, 11] - st[:, 10]) / 100.0
     clk = (st[:, 7] - st[:, 0]) / np.maximum(st[:, 11] - st[:, 10], 1) * 100e6 / 1e9
-    print(f"{tag}: blocks {nb}, chain-0 LEAF in {int(leaf.sum())}; block wall us median {np.median(rt):.1f} "
+    span = (st[leaf, 11].max() - st[leaf, 10].min()) / 100.0 if leaf.any() else 0.0
+    print(f"{tag}: blocks {nb}, with a leaf {int(leaf.sum())}; span {span:.1f} us; block wall us median {np.median(rt):.1f} "
           f"max {rt.max():.1f}; clock {np.median(clk):.2f} GHz")
     for sel, lab in ((leaf, "leaf blocks"), (~leaf, "other blocks")):
         if sel.any():
