@@ -203,7 +203,10 @@ class HMC(MCMCKernel):
                 warnings.warn("If both `num_steps` and `trajectory_length` are specified step size "
                               "can't be adapted", stacklevel=2)
         if kinetic_fn is not None:
-            raise NotImplementedError("custom kinetic_fn: the engine uses the Euclidean kinetic energy")
+            from .hmc_util import euclidean_kinetic_energy
+            if kinetic_fn is not euclidean_kinetic_energy:
+                raise NotImplementedError("custom kinetic_fn: the engine integrates the Euclidean kinetic energy "
+                                          "(numpyro_amd.infer.hmc_util.euclidean_kinetic_energy) only")
         self._pooled = isinstance(dense_mass, PooledGroups)
         if isinstance(dense_mass, str):
             if dense_mass != "pooled":

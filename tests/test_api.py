@@ -31,6 +31,8 @@ def test_kernel_argument_validation():
         NUTS(P.eight_schools, dense_mass=[("mu", 3)])  # groups of site names (hmc.py:239-252)
     with pytest.raises(NotImplementedError):
         NUTS(P.eight_schools, kinetic_fn=lambda m, r: 0.0)
+    from numpyro_amd.infer.hmc_util import euclidean_kinetic_energy
+    NUTS(P.eight_schools, kinetic_fn=euclidean_kinetic_energy)  # the energy the device integrates
     with pytest.warns(UserWarning):
         HMC(P.eight_schools, num_steps=5, trajectory_length=1.0)  # hmc.py:595-599
     k = NUTS(P.eight_schools, dense_mass=True, max_tree_depth=(8, 10), target_accept_prob=0.9)
@@ -236,3 +238,29 @@ def test_postprocess_fn_is_applied_per_draw():
         return {"s": torch.tensor(float(z["theta"].sum().item()))}
 
     torch.testing.assert_close(_postprocess_per_draw(py, sites)["s"], sites["theta"].sum(-1))
+
+
+def test_euclidean_kinetic_energy_matches_oracle():
+    """hmc_util.euclidean_kinetic_energy / its gradient (hmc_util.py:1183-1220) against the
+    oracle's restatement: diagonal, dense, dict-of-blocks structured mass, dict momenta."""
+    import numpy as np
+    import torch
+
+    import oracle.hmc_ref as H
+    from numpyro_amd.infer.hmc_util import euclidean_kinetic_energy as ke, euclidean_kinetic_grad as kg
+
+    rs = np.random.RandomState(0)
+    r = rs.randn(5)
+    diag = rs.rand(5) + 0.5
+    q = rs.randn(5, 5)
+    dense = q @ q.T + np.eye(5)
+    for imm in (diag, dense):
+        np.testing.assert_allclose(float(ke(torch.tensor(imm), torch.tensor(r))), H.euclidean_kinetic_energy(imm, r),
+                                   rtol=1e-12)
+        np.testing.assert_allclose(kg(torch.tensor(imm), torch.tensor(r)).numpy(), H.kinetic_grad(imm, r),
+                                   rtol=1e-12)
+    # structured: {("a", "b"): dense over a (2) and b (1), ("c",): diagonal (2)}; dict momenta
+    rd = {"a": torch.tensor(r[:2]), "b": torch.tensor(r[2:3]), "c": torch.tensor(r[3:])}
+    blocks = {("a", "b"): torch.tensor(dense[:3, :3]), ("c",): torch.tensor(diag[3:])}
+    want = H.euclidean_kinetic_energy(dense[:3, :3], r[:3]) + H.euclidean_kinetic_energy(diag[3:], r[3:])
+    np.testing.assert_allclose(float(ke(blocks, rd)), want, rtol=1e-12)
