@@ -917,8 +917,8 @@ inline size_t x3_roles_lds_bytes() {
 //     terms (iteration k), beside the role-B wave of their SIMD, which is MFMA-bound;
 //   role B, waves 0 and 1 (SIMDs 0, 1): GEMM2 for one 32-column half dt each, over every tile in
 //     tile order (pair k-2 in iteration k), wave 0 also adds the tiles' U terms in tile order;
-//   every LDS-DMA on waves 4-7 (s_memtime stamps of an experiment build: a 1-KB piece costs its
-//     issuing wave ~160 cycles, on the A / B waves the critical path).
+//   every LDS-DMA on waves 4-7, two thirds on 6 and 7 (s_memtime stamps of an experiment build:
+//     a 1-KB piece costs its issuing wave ~160-330 cycles, on the A / B waves the critical path).
 // Every accumulator sees x3_item's products in x3_item's order, the split is split3 of the same
 // values: bitwise the results of the other forms.  Compact image (H) only.  LDS (159 KB): images
 // of five tile pairs (k-2 in GEMM2, k-1 and k kept for it, k+1 in GEMM1, k+2 landing), labels of
@@ -951,9 +951,12 @@ __device__ __forceinline__ void x3_narrow_b_issue(const char* slot, const char* 
     asm volatile("ds_read_b64 %0, %1" : "=&v"(term) : "v"(ta) : "memory");
   }
 }
-// wait for them; the empty asm makes every later use depend on the wait
+// wait for them (N: LDS operations issued after them that may stay in flight, <= 15); the empty
+// asm makes every later use depend on the wait
+template <int N = 0>
 __device__ __forceinline__ void x3_narrow_b_wait(bf16x8 (&fb)[3][2], bf16x8 (&r)[2][3], double& term) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
 #pragma unroll
   for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
@@ -1003,12 +1006,10 @@ __device__ __forceinline__ void x3_narrow(const char* __restrict__ Xq, int64_t n
   char* tring = rring + 2 * 2 * 4096;        // [pair parity][j][512 B] their U terms
   char* sring = tring + 2 * 2 * 512;         // [pair parity][j][6 KB] split residuals
   char* uring = sring + 2 * 2 * 6144;        // [pair parity][j][512 B] their U terms
-  const bool helper = w >= 4;
-  const int hw = w - 4;
   // DMA pair p = the images of tile pair p + 1 and the labels of pair p; its piece q (images: q
   // = j NA + il for tile j of the pair and slot position il; labels: q = 2 NA + j) is issued by
-  // helper wave q mod 4.  Iteration k needs pair k, issued in iteration k - 1 (all of it: the
-  // barrier waits vmcnt(0)).
+  // wave owner(q).  Iteration k needs pair k, issued in iteration k - 1 (all of it: the barrier
+  // waits vmcnt(0)).
   auto issue_q = [&](int p, int q) {
     if (q < 2 * NA) {
       const int j = q / NA, il = q % NA, tile = 2 * (p + 1) + j;
@@ -1026,14 +1027,17 @@ __device__ __forceinline__ void x3_narrow(const char* __restrict__ Xq, int64_t n
             (unsigned)((tile * NP + NP - 1) * 1024), 0, 0);
     }
   };
+  // pieces q < 16 go to waves 6 and 7 (SIMDs 2, 3, beside the A waves), the rest to the split
+  // waves 4 and 5 (stamps: a wave issuing LDS-DMA stalls ~160-330 cycles a piece, ~1000 cycles
+  // for even one piece on the A / B waves, whose reads and MFMAs then start late: measured
+  // slower, 0.069 vs 0.058 ms per 1-32-chain evaluation)
+  auto owner = [&](int q) { return q < 16 ? 6 + (q & 1) : 4 + (q & 1); };
   auto issue_pair = [&](int p) {
-    if (!helper) return;
 #pragma unroll
-    for (int jj = 0; jj < (NQ + 3) / 4; ++jj) {
-      const int q = hw + 4 * jj;
-      if (q < NQ) issue_q(p, q);
-    }
+    for (int q = 0; q < NQ; ++q)
+      if (owner(q) == w) issue_q(p, q);
   };
+  static_assert(NQ == 24, "the owner table covers 24 pieces a pair");
   const bool roleA = w == 2 || w == 3;
   // a tile's index within a pair is w & 1 for the A, split and B waves alike (w - 2 / w - 4 here
   // let the compiler merge the A and split waves' LDS addresses with a form valid for one only)
@@ -1048,13 +1052,10 @@ __device__ __forceinline__ void x3_narrow(const char* __restrict__ Xq, int64_t n
   for (int r = 0; r < 16; ++r) g[r] = 0.0f;
   double pe = 0.0;
   if (nt > 0) {
-    if (helper) {  // the images of pair 0
+    // the images of pair 0
 #pragma unroll
-      for (int jj = 0; jj < (2 * NA + 3) / 4; ++jj) {
-        const int q = hw + 4 * jj;
-        if (q < 2 * NA) issue_q(-1, q);
-      }
-    }
+    for (int q = 0; q < 2 * NA; ++q)
+      if (owner(q) == w) issue_q(-1, q);
     x3_roles_barrier();  // the images of pair 0 are in
     issue_pair(0);
     f32x16 accA, accB;
@@ -1133,9 +1134,11 @@ __device__ __forceinline__ void x3_narrow(const char* __restrict__ Xq, int64_t n
           x3_narrow_b_issue<KB, DT, CMP, 1, false>(iring + ((i0 + 1) % NIMG) * NA * 1024,
                                                    sring + (par * 2 + 1) * 6144 + lane * 16, nullptr, fb1, r1, u1);
         }
-        x3_narrow_b_wait(fb0, r0, u0);
-        x3_narrow_b_wait(fb1, r1, u1);
+        // the first tile's operands (the oldest of the 37-38 reads), then its MFMAs while the
+        // second tile's reads land
+        x3_narrow_b_wait<15>(fb0, r0, u0);
         x3_narrow_b_mma(fb0, r0, g);
+        x3_narrow_b_wait<0>(fb1, r1, u1);
         f32x16 g1 = g;
         x3_narrow_b_mma(fb1, r1, g1);
 #pragma unroll

@@ -45,14 +45,14 @@ rep = [('''    auto iter = [&](int k, const f32x16& acc, f32x16& nxt) {
   if (w >= 2 || pos >= ldc) return;'''),
        ('''  double pe = 0.0;
   if (nt > 0) {
-    if (helper) {  // the images of pair 0''', '''  double pe = 0.0;
+    // the images of pair 0''', '''  double pe = 0.0;
   if (blockIdx.x < 8 && lane == 0) {
     unsigned long long rt = __builtin_amdgcn_s_memrealtime(), mt = __builtin_amdgcn_s_memtime();
     __builtin_nontemporal_store(rt, &g_nx_stamps[blockIdx.x][w][158][0]);
     __builtin_nontemporal_store(mt, &g_nx_stamps[blockIdx.x][w][158][1]);
   }
   if (nt > 0) {
-    if (helper) {  // the images of pair 0''')]
+    // the images of pair 0''')]
 for a, b in rep:
     assert a in src, a[:60]
     src = src.replace(a, b)

@@ -42,7 +42,7 @@ for wg in range(3):
     clk = (mt1 - mt0) / (rt1 - rt0) * 100e6
     print(f"WG {wg}: {(rt1 - rt0) / 100:.1f} us between the first and last stamps, clock {clk / 1e9:.2f} GHz")
     K = int(np.max(np.nonzero(st[wg, 0, :158, 3])[0])) + 1
-    for w, name in ((0, "B0"), (1, "B1"), (2, "A0"), (3, "A1"), (4, "helper")):
+    for w, name in ((0, "B0"), (1, "B1"), (2, "A0"), (3, "A1"), (4, "split4"), (5, "split5"), (6, "dma6"), (7, "dma7")):
         t = st[wg, w, 1:K - 1]
         bar = np.mean(t[:, 1] - t[:, 0])
         iss = np.mean(t[:, 2] - t[:, 1])
