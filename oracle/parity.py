@@ -32,9 +32,11 @@ A transition whose decisions all agree but whose draw differs is reported as `dr
 leaf was selected, but the positions drifted apart along the trajectory (leapfrog dynamics of a
 tanh network or a stiff posterior amplify rounding over hundreds of leaves).  A draw has a
 bound too: it is explained only by a rounding calibration (below) -- when the device's drift
-at that chain and transition is within DRAW_MULT x the calibration's drift there (or, where the
-calibration already parted from the reference at an earlier transition, its largest drift at
-the same tree size).  Without a calibration a draw mismatch is unexplained: a bug that corrupts
+at that chain and transition is within DRAW_MULT x the calibration's drift there, or x the
+calibration's median drift over its chains at that transition where that is larger (chaotic
+trajectories spread single-chain drifts over two orders of magnitude), or -- where the
+calibration already parted from the reference at an earlier transition -- its largest drift at
+the same tree size.  Without a calibration a draw mismatch is unexplained: a bug that corrupts
 the proposal (the whitening's to_model, the collection) while every decision stays equal
 cannot pass as drift.  Drift is measured in tolerance units, max_i |z_i - ref_i| / (atol +
 rtol |ref_i|), so a draw mismatch has drift > 1.
@@ -48,7 +50,8 @@ transition whose decisions agree, the relative leaf-energy discrepancy.  The dev
 with the same reference; `bound_draws` explains (or not) its draw mismatches by the
 calibration's drift, and `like_calibration` requires its whole record to be of the
 calibration's order: drift distributions compared pairwise on the (chain, transition) pairs both
-reached on the reference's path (geometric mean of the ratios <= DRIFT_GEO_MAX), leaf-energy
+reached on the reference's path (geometric mean of the ratios <= DRIFT_GEO_MAX, at its lower
+95% bound when the pairs are few), leaf-energy
 discrepancies relative to the energies' magnitude (tests/test_gpu_parity_trace.py, bench.py's
 config legs)."""
 from __future__ import annotations
@@ -213,17 +216,29 @@ def bound_draws(par, cal, mult=DRAW_MULT):
     cal_drift / ratio / explained on each draw and par["draw_drift"] (paired drift statistics,
     see drift_stats); returns par."""
     at = {(d["chain"], d["transition"]): d["drift"] for d in cal["drift"]}
-    by_tree = {}
+    by_tree, by_t = {}, {}
     for d in cal["drift"]:
         by_tree[d["tree"]] = max(by_tree.get(d["tree"], 0.0), d["drift"])
+        by_t.setdefault(d["transition"], []).append(d["drift"])
+    typical = {t: float(np.median(v)) for t, v in by_t.items()}
     top = max((d["drift"] for d in cal["drift"]), default=0.0)
     for m in par["mismatches"]:
         if m["kind"] != "draw":
             continue
         key = (m["chain"], m["transition"])
-        ref, how = (at[key], "same chain and transition") if key in at else (
-            (by_tree[m["tree_oracle"]], "largest at this tree size") if m["tree_oracle"] in by_tree
-            else (top, "largest of the calibration"))
+        if key in at:
+            # a chaotic trajectory's drift varies by two orders of magnitude between chains at the
+            # same transition (BNN c3: 1.05 to 198 tolerance units), so a chain whose own
+            # calibration drift happens to be small is bounded by the calibration's typical drift
+            # at that transition instead
+            ref, how = at[key], "same chain and transition"
+            med = typical.get(m["transition"], 0.0)
+            if med > ref:
+                ref, how = med, "median of the calibration's chains at this transition"
+        elif m["tree_oracle"] in by_tree:
+            ref, how = by_tree[m["tree_oracle"]], "largest at this tree size"
+        else:
+            ref, how = top, "largest of the calibration"
         m["cal_drift"], m["cal_basis"] = ref, how
         m["ratio"] = m["drift"] / ref if ref > 0 else math.inf
         m["bound"] = mult * ref
@@ -245,7 +260,16 @@ def drift_stats(par, cal):
     fl = DRIFT_FLOOR
     r = [math.log(max(a[k], fl) / max(b[k], fl)) for k in keys]
     draws = [m for m in par["mismatches"] if m["kind"] == "draw"]
+    # the geometric mean's lower 95% bound (2 standard errors of the mean log ratio): a chaotic
+    # pair's log ratio has a spread of ~1 or more, so a few pairs cannot tell 2x from 1x
+    lo = None
+    if len(r) >= 2:
+        mu, sd = sum(r) / len(r), float(np.std(r, ddof=1))
+        lo = math.exp(mu - 2.0 * sd / math.sqrt(len(r)))
+    elif r:
+        lo = math.exp(r[0])
     return {"pairs": len(keys), "geo_mean_ratio": math.exp(sum(r) / len(r)) if r else None,
+            "geo_mean_lo95": lo,
             "median_dev": float(np.median([a[k] for k in keys])) if keys else None,
             "median_cal": float(np.median([b[k] for k in keys])) if keys else None,
             "max_dev": max((a[k] for k in keys), default=None), "max_cal": max((b[k] for k in keys), default=None),
@@ -298,7 +322,8 @@ def like_calibration(dev, cal, slack=None):
     calibration `cal` (a second float32 oracle vs the same reference, same chains): its draws
     bounded by the calibration's drift (bound_draws) and every located parting explained at its
     leaf; matched chains within `slack` (default max(4, chains / 10)) of the calibration's; the
-    paired drift's geometric-mean ratio <= DRIFT_GEO_MAX; and the largest relative leaf-energy
+    paired drift's geometric-mean ratio <= DRIFT_GEO_MAX (its lower 95% bound, over few pairs);
+    and the largest relative leaf-energy
     discrepancy within DE_REL_MULT x the calibration's (floor 1e-7, a few float32 ulps)."""
     if "draw_drift" not in dev:
         bound_draws(dev, cal)
@@ -311,8 +336,10 @@ def like_calibration(dev, cal, slack=None):
     msg = (f"device {a} (max dE err {dev['max_dE_err']:.3g}, relative {dev['max_dE_rel']:.3g}) vs rounding "
            f"calibration {b} (max dE err {cal['max_dE_err']:.3g}, relative {cal['max_dE_rel']:.3g}); paired drift "
            f"{dev['draw_drift']['pairs']} transitions, geometric-mean ratio "
-           f"{'n/a' if g is None else format(g, '.3g')}, median {dev['draw_drift']['median_dev']} vs "
+           f"{'n/a' if g is None else format(g, '.3g')} (lower 95% bound "
+           f"{'n/a' if dev['draw_drift'].get('geo_mean_lo95') is None else format(dev['draw_drift']['geo_mean_lo95'], '.3g')}), median {dev['draw_drift']['median_dev']} vs "
            f"{dev['draw_drift']['median_cal']} tolerance units")
+    lo = dev["draw_drift"].get("geo_mean_lo95")
     ok = (a["unexplained"] == 0 and a["matched"] >= b["matched"] - slack and rel_ok
-          and (g is None or g <= DRIFT_GEO_MAX))
+          and (lo is None or lo <= DRIFT_GEO_MAX))
     return ok, msg

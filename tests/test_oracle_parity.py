@@ -172,3 +172,30 @@ def test_draw_mismatch_needs_a_calibration_and_is_bounded_by_it():
     assert same["draw_drift"]["geo_mean_ratio"] == 1.0
     ok, msg = PR.like_calibration(same, cal)
     assert ok, msg
+
+
+def test_draw_bound_uses_the_calibrations_typical_drift_at_that_transition():
+    """A chain whose own calibration drift is small is bounded by the calibration's median drift
+    over chains at the same transition (chaotic trajectories spread single-chain drifts over two
+    orders of magnitude); the paired geometric mean is judged at its lower 95% bound."""
+    drift = [{"chain": c, "transition": 1, "tree": 7, "drift": d, "dz": d}
+             for c, d in enumerate([1.0, 30.0, 50.0, 80.0, 200.0])]
+    cal = {"drift": drift, "mismatches": [], "matched": 0}
+    par = {"drift": [], "mismatches": [{"kind": "draw", "chain": 0, "transition": 1,
+                                        "tree_oracle": 7, "drift": 60.0, "dz": 60.0}]}
+    PR.bound_draws(par, cal)
+    m = par["mismatches"][0]
+    assert m["explained"] and m["cal_drift"] == 50.0 and "median" in m["cal_basis"], m
+    # far beyond the typical drift: still unexplained
+    par = {"drift": [], "mismatches": [dict(par["mismatches"][0], drift=1e4, dz=1e4)]}
+    PR.bound_draws(par, cal)
+    assert not par["mismatches"][0]["explained"]
+    # paired drift: 3 pairs whose geometric mean is above 2x but whose spread cannot exclude 1x
+    dev = {"drift": [dict(d, drift=d["drift"] * f) for d, f in zip(drift, [0.5, 1.0, 20.0])],
+           "mismatches": []}
+    st = PR.drift_stats(dev, cal)
+    assert st["geo_mean_ratio"] > PR.DRIFT_GEO_MAX and st["geo_mean_lo95"] <= PR.DRIFT_GEO_MAX, st
+    # the same ratio on every pair is judged at face value
+    dev = {"drift": [dict(d, drift=d["drift"] * 3.0) for d in drift], "mismatches": []}
+    st = PR.drift_stats(dev, cal)
+    assert st["geo_mean_lo95"] > PR.DRIFT_GEO_MAX, st
