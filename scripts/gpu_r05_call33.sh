@@ -14,3 +14,12 @@ d=json.loads(open('$O/bench_c3.json').readline())
 c=d['configs']['c3']; p=c.get('parity',{})
 print(json.dumps({k:p.get(k) for k in ('matched','unexplained','explained','draw_drift')})[:800]); print(p.get('calibration'))"
 grep -E "\[c3\]" $O/bench_c3.err | tail -8
+# kernel-boundary cost micro (scripts/micro/boundary_cost.hip, built into build/abx/micro)
+timeout -k 10 120 build/abx/micro/boundary_cost 2000 > $O/boundary.txt 2>&1 || exit 1
+cat $O/boundary.txt
+for c in 32 4096; do
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/bprof$c -o run -- build/abx/micro/boundary_cost 500 $c > $O/bprof$c.log 2>&1 || exit 1
+  echo "== chains $c" >> $O/boundary_hist.txt
+  python3 scripts/kernel_hist.py $O/bprof$c >> $O/boundary_hist.txt 2>&1 || exit 1
+done
+cat $O/boundary_hist.txt
