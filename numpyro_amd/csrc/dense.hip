@@ -360,8 +360,11 @@ __global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ i
 // ---------------------------------------------------------------------------------------
 // Split-bf16 chain products (f32-accurate on the bf16 matrix cores; the scheme of the covtype
 // kernel, potential_logreg.hip "Split-bf16 kernel"): every f32 operand as three bf16 terms,
-// six bf16 products (a3b1 + a2b2 + a1b3 + a2b1 + a1b2 + a1b1) per 16-deep k-step into f32
-// accumulators.  A (= T or T^T, constant between adaptation windows) is packed once into
+// six bf16 products per 16-deep k-step into f32 accumulators: a1b1 into the main accumulator,
+// the five correction products (a3b1 + a2b2 + a1b3 + a2b1 + a1b2, ~2^-8 of it) into a second
+// one, the two added once after the k loop.  One rounding of the main sum per k-step instead
+// of six: at D = 5038 the products' largest error fell from 4x to ~1x a float32 GEMM's
+// (scripts/bnn_accuracy.py), which is what the BNN parity leg's draw drift was made of.  A (= T or T^T, constant between adaptation windows) is packed once into
 // MFMA-fragment order (nmx_gemm_x3_pack_a); each call splits In into fragment order first
 // (k_x3_split_b, ~6 B written per f32 read), then k_gemm_x3 streams both through a 2-slot
 // LDS ring by buffer LDS-DMA.  Tiles, triangle skipping, split-K boundaries, the XCD-aware
@@ -587,11 +590,11 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
     }
   };
 
-  f32x16 acc[CT];
+  f32x16 acc[CT], cor[CT];  // a1b1 / the five correction products
 #pragma unroll
   for (int cl = 0; cl < CT; ++cl)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[cl][r] = 0.0f;
+    for (int r = 0; r < 16; ++r) acc[cl][r] = cor[cl][r] = 0.0f;
   if (kt_begin < nk) issue(kt_begin, 0);
   if (NBUF == 3 && kt_begin + 1 < nk) issue(kt_begin + 1, 1);
   int buf = 0;
@@ -615,16 +618,20 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
       for (int cl = 0; cl < CT; ++cl) {
         const bf16x8 b1 = fr[(NPA + s * 3 * CT + cl * 3 + 0) * 64], b2 = fr[(NPA + s * 3 * CT + cl * 3 + 1) * 64],
                      b3 = fr[(NPA + s * 3 * CT + cl * 3 + 2) * 64];
-        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[cl], 0, 0, 0);
-        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[cl], 0, 0, 0);
-        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[cl], 0, 0, 0);
-        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc[cl], 0, 0, 0);
-        acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc[cl], 0, 0, 0);
+        cor[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, cor[cl], 0, 0, 0);
+        cor[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, cor[cl], 0, 0, 0);
+        cor[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, cor[cl], 0, 0, 0);
+        cor[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, cor[cl], 0, 0, 0);
+        cor[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, cor[cl], 0, 0, 0);
         acc[cl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[cl], 0, 0, 0);
       }
     }
     buf = buf + 1 == NBUF ? 0 : buf + 1;
   }
+#pragma unroll
+  for (int cl = 0; cl < CT; ++cl)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[cl][r] += cor[cl][r];
   if (out_list) {
     // scattered to the listed chains' rows (Out [.][D], NMX_LAYOUT_CHAIN_ROWS; one K-split): a
     // lane holds 4 consecutive coordinates per register group -- 16-byte stores when D % 4 == 0
