@@ -11,6 +11,7 @@ numpyro/infer/hmc.py:459-530) with ``progress_bar=False``.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import uuid
@@ -429,9 +430,12 @@ class Engine:
         wt = self.potential.whitening
         z = torch.empty(self.D, self.ldc, dtype=torch.float32, device=self.device)
         wt.to_model(self.view("z").contiguous(), z, stream=s)
-        wt.set(inverse_mass_matrix, mu)
         w = torch.zeros(self.D, self.ldc, dtype=torch.float32, device=self.device)
-        w[:, :self.C] = wt.to_whitened(z[:, :self.C])
+        lock = self.device_group[0].linalg_lock if self.device_group is not None else contextlib.nullcontext()
+        with lock:
+            wt.set(inverse_mass_matrix, mu)
+            w[:, :self.C] = wt.to_whitened(z[:, :self.C])
+            torch.cuda.current_stream(self.device).synchronize()
         check(lib().nmx_nuts_init_from(ctypes.byref(self.cfg), ptr(self.arena), ptr(w), s))
         self._evaluate_all(s)
         check(lib().nmx_nuts_init_check(ctypes.byref(self.cfg), ptr(self.arena), s))

@@ -46,6 +46,11 @@ class DeviceGroup:
         self.size = int(size)
         self.barrier = threading.Barrier(self.size)
         self.slots = [None] * self.size
+        # the window-end factorizations of the ranks' threads run one at a time: the linear
+        # algebra libraries behind torch.linalg keep per-device state that concurrent host
+        # threads on one device must not share (a rank's factorization then equals the torchrun
+        # rank's, which has a process of its own)
+        self.linalg_lock = threading.Lock()
 
     def all_reduce_sum(self, rank, tensors):
         """Every rank passes the same list of tensors; each gets back their sums over ranks (in
