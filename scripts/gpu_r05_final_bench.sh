@@ -12,7 +12,7 @@ rm -rf $O/t/f $O/t/w
 cat $O/traffic.json | cut -c1-400
 timeout -k 10 1100 python -u bench.py --traffic-json $O/traffic.json > $O/bench.json 2> $O/bench.err || exit 1
 head -c 600 $O/bench.json; echo
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --configs none --no-cpu-baseline --traffic-json $O/traffic.json > $O/prof.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --configs none --no-cpu-baseline --traffic-json $O/traffic.json > $O/prof.log 2>&1 || exit 1
 python3 scripts/kernel_hist.py $O/prof > $O/headline_kernel_hist.txt && cat $O/headline_kernel_hist.txt
 find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/headline_kernel_stats.csv \;
 python3 scripts/bench_timed_kernel_avg.py $O/prof $O/prof.log > $O/timed_kernel_avg.json && cat $O/timed_kernel_avg.json
