@@ -337,10 +337,13 @@ def velocity_verlet(pe_grad, kinetic_fn=euclidean_kinetic_energy, kinetic_grad_f
 
 
 def find_reasonable_step_size(pe_grad, kinetic_fn, momentum_generator, init_step_size,
-                              inverse_mass_matrix, z_info, rng_key):
+                              inverse_mass_matrix, z_info, rng_key, margins=None):
     """hmc_util.py:314-384; `momentum_generator(z, inverse_mass_matrix, k)` draws the k-th
     attempt's momentum (the reference passes the inverse mass matrix where
-    momentum_generator expects its square root, hmc_util.py:359; kept)."""
+    momentum_generator expects its square root, hmc_util.py:359; kept).  `margins` (a list, test
+    instrumentation) receives each attempt's (decision margin -dE - log 0.8, energy scale
+    |E_current| + |E_new|): a margin within rounding of zero is a tie another float32
+    implementation may decide the other way."""
     target_accept_prob = np.float32(np.log(np.float32(0.8)))  # jnp.log(0.8) in float32
     _, vv_update = velocity_verlet(pe_grad, kinetic_fn)
     z, _, potential_energy, z_grad = z_info
@@ -366,6 +369,8 @@ def find_reasonable_step_size(pe_grad, kinetic_fn, momentum_generator, init_step
         energy_new = kinetic_fn(inverse_mass_matrix, r_new) + potential_energy_new
         delta_energy = energy_new - energy_current
         direction_new = 1 if target_accept_prob < -delta_energy else -1
+        if margins is not None:
+            margins.append((float(-delta_energy - target_accept_prob), float(abs(energy_current) + abs(energy_new))))
         last_direction, direction = direction, direction_new
     return step_size
 
@@ -622,8 +627,13 @@ class NUTSOracle:
                     eps = philox.heuristic_normals(seed, chain, it, k, self.dim).astype(dtype)
                     return momentum_generator(np.asarray(imm, dtype), eps).astype(dtype)
 
-                return dtype(find_reasonable_step_size(self.pe_grad, euclidean_kinetic_energy, momentum,
-                                                       dtype(step_size), inverse_mass_matrix, z_info, None))
+                self.search_margins = []
+                out = dtype(find_reasonable_step_size(self.pe_grad, euclidean_kinetic_energy, momentum,
+                                                      dtype(step_size), inverse_mass_matrix, z_info, None,
+                                                      margins=self.search_margins))
+                if self.force_search is not None:  # test: teacher-force a search decided at a tie
+                    out, self.force_search = dtype(self.force_search), None
+                return out
         self.wa_init, self.wa_update = warmup_adapter(
             num_warmup, find_reasonable_step_size=frs, adapt_step_size=adapt_step_size,
             adapt_mass_matrix=adapt_mass_matrix, dense_mass=dense_mass,
@@ -631,6 +641,7 @@ class NUTSOracle:
             dtype=dtype)
         self.step_size = step_size
         self.inverse_mass_matrix = inverse_mass_matrix
+        self.search_margins, self.force_search = [], None
         self.vv_init, self.vv_update = velocity_verlet(pe_grad)
 
     def init(self, z, seed, chain):

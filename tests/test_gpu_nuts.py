@@ -661,6 +661,12 @@ def test_find_heuristic_step_size_matches_oracle(device, model, dim):
     assert moved > 0  # the search changed the initial step size of at least some chains
 
 
+# a step-size search attempt decided within this fraction of its energies' magnitude (|E_current| +
+# |E_new|) of the threshold is a rounding tie: two float32 implementations (the device's whitened
+# products, the oracle's mass_matrix_sqrt @ eps) may decide it either way
+SEARCH_TIE = 1e-5
+
+
 @pytest.mark.parametrize("mass", ["adapted", "given"])
 @pytest.mark.parametrize("model,dim", [("diag_normal", 40), ("logreg", 55)])
 def test_find_heuristic_step_size_dense_matches_oracle(device, model, dim, mass):
@@ -671,7 +677,9 @@ def test_find_heuristic_step_size_dense_matches_oracle(device, model, dim, mass)
     "given": a fixed non-diagonal inverse_mass_matrix, adapt_mass_matrix=False (one shared
     whitening; the window end still searches).  Oracle: the reference adapter with dense_mass,
     fed the device's accept probabilities and draws, reproduces every transition's step size
-    (rtol 1e-5: a search mismatch would be a whole factor 2)."""
+    (rtol 1e-5: a search mismatch would be a whole factor 2), except where a search attempt's
+    decision margin (-dE - log 0.8) is within rounding of zero (SEARCH_TIE x the energies'
+    magnitude): there the device's result is teacher-forced and the count of such ties printed."""
     seed, C, W = 31, 64, 150
     rs = np.random.RandomState(dim)
     args, fm, ref, *_ = _fixed_step_case(model, dim, rs)
@@ -690,18 +698,35 @@ def test_find_heuristic_step_size_dense_matches_oracle(device, model, dim, mass)
     draws = samples[:, :, :C].cpu().numpy().transpose(2, 0, 1)
     pe_grad = lambda z: tuple(np.asarray(v, np.float32) if np.ndim(v) else np.float32(v)  # noqa: E731
                               for v in ref.pe_grad(z))
-    changed = 0
+    changed, ties = 0, []
+
+    def at_tie(o):
+        return any(abs(m) <= SEARCH_TIE * sc for m, sc in o.search_margins)
+
     for c in range(C):
         o = H.NUTSOracle(pe_grad, dim, W, find_heuristic_step_size=True, dense_mass=True, **kw)
         st = o.init(z0[c], seed, c)
-        np.testing.assert_allclose(ss0[c], st.adapt_state.step_size, rtol=1e-5, err_msg=f"chain {c} initial search")
+        if not np.isclose(ss0[c], st.adapt_state.step_size, rtol=1e-5):
+            assert at_tie(o), (c, ss0[c], st.adapt_state.step_size, o.search_margins)
+            ties.append((c, "init"))
+            o.force_search = ss0[c]
+            st = o.init(z0[c], seed, c)
         wa = st.adapt_state
         for t in range(W):
             z = draws[c, t].astype(np.float32)
             pe, g = pe_grad(z)
-            wa = o.wa_update(t, np.float32(acc[c, t]), H.IntegratorState(z, None, pe, g), wa)
+            zi = H.IntegratorState(z, None, pe, g)
+            wa_new = o.wa_update(t, np.float32(acc[c, t]), zi, wa)
+            if not np.isclose(ss[c, t], wa_new.step_size, rtol=1e-5) and o.search_margins and at_tie(o):
+                ties.append((c, t))
+                o.force_search = ss[c, t]
+                wa_new = o.wa_update(t, np.float32(acc[c, t]), zi, wa)
+            o.search_margins = []
+            wa = wa_new
             np.testing.assert_allclose(ss[c, t], wa.step_size, rtol=1e-5, err_msg=f"chain {c} after transition {t}")
         changed += int(ss[c, 99] != ss[c, 98])
+    print(f"[heuristic dense {model} {mass}] {len(ties)} searches decided at a rounding tie (teacher-forced): {ties}")
+    assert len(ties) <= C // 8
     assert np.any(ss0 != 1.0) and changed > 0
 
 
