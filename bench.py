@@ -241,7 +241,7 @@ def _config_specs():
                    args=(X, Y, H), chains=2048, warmup=CONFIG_WARMUP["c3"], steps=5, dense="pooled", one_gpu=True,
                    flop=2.0 * D_bnn * D_bnn + 6.0 * 100 * H * H + 6.0 * 100 * 3 * H,
                    basis="2 D^2 (whitening) + 6 N H^2 + 6 N Dx H (network) FLOP per chain-leapfrog",
-                   cpu=lambda dt=np.float32: OB.BNNBatch(X, Y, H, dtype=dt), cpu_chains=8, parity_transitions=2,
+                   cpu=lambda dt=np.float32: OB.BNNBatch(X, Y, H, dtype=dt), cpu_chains=16, parity_transitions=2,
                    c_model="bnn", c_args=(X, Y, H)),
         "c4": dict(name="stochastic volatility T=2517 (D=2519), diag mass, examples/stochastic_volatility.py",
                    model=P.stochastic_volatility, args=(r,), chains=8192, warmup=CONFIG_WARMUP["c4"],
