@@ -146,6 +146,37 @@ def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
                                   None, C, None, None, None) != 0  # no split buffer
 
 
+def test_gemm_chains_x3_error_is_a_float32_gemms(device):
+    """The split-bf16 product's rounding is that of a float32 GEMM (BLAS sgemm in NumPy) on the
+    same float32 operands, both against float64: at D = 5038 (BASELINE config 3's whitening) the
+    median over chains of the largest relative error is within 2.5x sgemm's (1.7x measured; 4x
+    when the five correction products shared the main accumulator, which is what the c3 parity
+    leg's draw drift was made of -- scripts/bnn_accuracy.py)."""
+    D, C, tri = 5038, 128, 1
+    rs = np.random.RandomState(11)
+    lib = native.lib()
+    lda = lib.nmx_dense_padded_dim(D)
+    A32 = np.triu(rs.randn(D, D) / np.sqrt(D)).astype(np.float32)
+    x32 = rs.randn(D, C).astype(np.float32)
+    At = torch.zeros(lda, lda, device=device)
+    At[:D, :D] = torch.from_numpy(A32.T.copy()).to(device)
+    xd = torch.from_numpy(x32).to(device)
+    out = torch.empty(D, C, device=device)
+    Ap = torch.empty(lib.nmx_gemm_x3_packed_a_bytes(lda), dtype=torch.uint8, device=device)
+    sp = torch.empty(lib.nmx_gemm_x3_split_bytes(lda, C), dtype=torch.uint8, device=device)
+    s = native.stream_ptr()
+    native.check(lib.nmx_gemm_x3_pack_a(native.ptr(At), lda, native.ptr(Ap), s))
+    native.check(lib.nmx_gemm_chains_x3(native.ptr(Ap), lda, D, native.ptr(xd), native.ptr(out), None, tri, C, None,
+                                        None, C, native.ptr(sp), None, s))
+    torch.cuda.synchronize()
+    y64 = A32.astype(np.float64) @ x32.astype(np.float64)
+    sc = np.abs(y64).max(0)
+    dev = np.median(np.abs(out.cpu().numpy().astype(np.float64) - y64).max(0) / sc)
+    ref = np.median(np.abs((A32 @ x32).astype(np.float64) - y64).max(0) / sc)
+    print(f"[x3 accuracy D={D}] device {dev:.3g} vs sgemm {ref:.3g} ({dev / ref:.2f}x)")
+    assert dev <= 2.5 * ref, (dev, ref)
+
+
 @pytest.mark.parametrize("tri", [0, 1, 2])
 def test_gemm_chains_x3_tiles_agree(device, tri):
     """nmx_gemm_chains_x3 picks its workgroup tile from the grid size (256 x 128 when the launch
