@@ -102,3 +102,16 @@ def test_fixed_batch_mode_and_path_comparison():
     par = PR.compare_traced(hist, tr, ns, zs_bad, atol=0.0)
     assert par["matched"] == n - 1 and (par["mismatches"][0]["chain"], par["mismatches"][0]["transition"]) == (1, 1)
     assert par["mismatches"][0]["kind"] == "draw" and not par["mismatches"][0]["explained"]
+
+
+def test_bench_valu_roofline_from_the_committed_profile():
+    """bench.py's c4 VALU fraction: profiled VALU wave-instructions per chain-leapfrog x rate over
+    1024 SIMDs x 0.5 instructions per cycle at the profiled clock (profiles/r05/sv_valu.json)."""
+    import bench
+
+    r = bench._valu_roofline("profiles/r05/sv_valu.json", 33.0e6)
+    assert r is not None and r["unit"] == "G VALU wave-instr/s"
+    assert np.isclose(r["achieved"], r["insts_per_leapfrog"] * 33.0e6 / 1e9)
+    assert np.isclose(r["peak"], 1024 * 0.5 * r["clock_ghz"])
+    assert 0.05 < r["frac"] < 1.0
+    assert bench._valu_roofline("profiles/r05/no_such_profile.json", 1.0) is None

@@ -130,3 +130,27 @@ def test_device_group_all_reduce_sum_in_rank_order():
     ref = (vals[0] + vals[1]) + vals[2]
     for r in range(3):
         assert torch.equal(out[r][0], ref) and float(out[r][1]) == 3.0
+
+
+def test_device_group_serializes_window_end_factorizations():
+    """MCMC(devices=...) runs one host thread per device; their window-end factorizations
+    (torch.linalg) take DeviceGroup.linalg_lock one at a time (Engine._reexpress)."""
+    import threading
+    import time
+
+    g = shard.DeviceGroup(2)
+    inside, peak = [0], [0]
+
+    def work():
+        with g.linalg_lock:
+            inside[0] += 1
+            peak[0] = max(peak[0], inside[0])
+            time.sleep(0.02)
+            inside[0] -= 1
+
+    ts = [threading.Thread(target=work) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert peak[0] == 1
