@@ -639,7 +639,9 @@ int nmx_cpu_nuts_run(const nmx_cpu_model* m, int C, const float* z0, const float
     calls += 1;
     const double elapsed = now_s() - t0;
     if (min_transitions == 0 && elapsed >= seconds) break; /* a timing run: stop mid-transition */
-#pragma omp parallel for schedule(dynamic, 4)
+    /* one chain per chunk: with 32 chains on 16 threads, chunks of 4 left half the threads idle in
+     * the tree logic (SV, scripts/sv_cpu_share.py on the GPU box: 1.37-1.42x leapfrog/s) */
+#pragma omp parallel for schedule(dynamic, 1)
     for (int b = 0; b < B; ++b) {
       Chain* h = ch + idx[b];
       copyv(h->ng, Gb + (size_t)b * vec, D);
