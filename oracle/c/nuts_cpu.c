@@ -625,6 +625,56 @@ int nmx_cpu_nuts_run(const nmx_cpu_model* m, int C, const float* z0, const float
   const double t0 = now_s();
   double pot = 0.0, leap = 0.0, calls = 0.0;
   int running = C;
+  if (m->model != 1 && !m->wT) {
+    /* per-chain potentials (funnel, SV, BNN with a diagonal mass): no batch to form, so each thread
+     * runs its own chains (c = tid, tid + nthreads, ...) leaf by leaf, round robin, with no
+     * barrier per leaf -- the batched loop below paid three fork / joins and waited for the slowest
+     * chain every round.  Each chain's arithmetic is the same (bitwise the same draws); the
+     * potential seconds are the threads' mean. */
+    const int nth = omp_get_max_threads();
+#pragma omp parallel reduction(+ : pot, leap, calls)
+    {
+      const int tid = omp_get_thread_num(), nt = omp_get_num_threads();
+      float* work = sc.work ? sc.work + (size_t)tid * sc.work_per : NULL;
+      int live = 1;
+      while (live) {
+        live = 0;
+        for (int c = tid; c < C; c += nt) {
+          Chain* h = ch + c;
+          if (!h->active) continue;
+          const double p0 = now_s();
+          float pe_new;
+          if (m->model == 2) pe_funnel(D, h->nz, &pe_new, h->ng);
+          else if (m->model == 3) pe_sv(m->r2, D - 2, h->nz, &pe_new, h->ng);
+          else pe_bnn(m, h->nz, &pe_new, h->ng, work);
+          const double p1 = now_s();
+          pot += p1 - p0;
+          leap += 1.0;
+          calls += 1.0;
+          if (min_transitions == 0 && p1 - t0 >= seconds) { /* a timing run: stop mid-transition */
+            h->active = 0;
+            continue;
+          }
+          live = 1;
+          if (!leaf_end(h, pe_new, max_delta_energy, seed)) continue;
+          copyv(h->z, h->tpz, D);
+          copyv(h->g, h->tpg, D);
+          h->pe = h->tp_pe;
+          const int t = h->done_t;
+          out_num_steps[(size_t)h->c * num_transitions + t] = h->tn;
+          if (out_z) copyv(out_z + ((size_t)h->c * num_transitions + t) * vec, h->z, D);
+          h->done_t = t + 1;
+          h->it += 1;
+          if (h->done_t < num_transitions && (h->done_t < min_transitions || p1 - t0 < seconds)) {
+            h->active = 1;
+            start_transition(h, seed);
+          }
+        }
+      }
+    }
+    pot /= nth;
+    running = 0;
+  }
   while (running > 0) {
     int B = 0;
     for (int c = 0; c < C; ++c)
