@@ -29,9 +29,23 @@ int nmx_check_launch(const char* what) {
 // hipFuncSetAttribute holds per device: a kernel launched on several GPUs of one process needs
 // its dynamic-LDS limit raised on each.  Remembered per (kernel, device) so the host call is
 // made once; the device is the launch stream's (the calling thread's current device may be
-// another one).
+// another one).  Called on every launch of the hot kernels: a per-thread cache of the last
+// (kernel, stream) answered is checked first, so the launch path takes no lock and makes no
+// HIP call once a (kernel, stream) pair has been served (host threads of an in-process
+// multi-device run never meet here after their first launches).
 int nmx_lds_limit(const void* fn, size_t bytes, hipStream_t stream, const char* what) {
   if (bytes <= 64 * 1024) return NMX_OK;
+  struct Hit {
+    const void* fn;
+    hipStream_t stream;
+    size_t bytes;
+  };
+  static thread_local Hit hits[8] = {};
+  static thread_local unsigned next_hit = 0;
+  // (the null stream is the calling thread's current device, which may change: not cached)
+  if (stream)
+    for (const Hit& h : hits)
+      if (h.fn == fn && h.stream == stream && h.bytes >= bytes) return NMX_OK;
   int dev = 0;
   hipError_t e = stream ? hipStreamGetDevice(stream, &dev) : hipGetDevice(&dev);
   if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "%s: device of the stream: %s", what, hipGetErrorString(e));
@@ -39,7 +53,10 @@ int nmx_lds_limit(const void* fn, size_t bytes, hipStream_t stream, const char* 
   static std::map<std::pair<const void*, int>, size_t> done;
   std::lock_guard<std::mutex> lock(mu);
   auto it = done.find({fn, dev});
-  if (it != done.end() && it->second >= bytes) return NMX_OK;
+  if (it != done.end() && it->second >= bytes) {
+    if (stream) hits[next_hit++ % 8] = Hit{fn, stream, it->second};
+    return NMX_OK;
+  }
   int cur = dev;
   (void)hipGetDevice(&cur);
   if (cur != dev) (void)hipSetDevice(dev);
@@ -47,6 +64,7 @@ int nmx_lds_limit(const void* fn, size_t bytes, hipStream_t stream, const char* 
   if (cur != dev) (void)hipSetDevice(cur);
   if (e != hipSuccess) return nmx_fail(NMX_ERR_HIP, "%s: hipFuncSetAttribute: %s", what, hipGetErrorString(e));
   done[{fn, dev}] = bytes;
+  if (stream) hits[next_hit++ % 8] = Hit{fn, stream, bytes};
   return NMX_OK;
 }
 

@@ -147,6 +147,18 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// LDS floats vblock_sum<NV, CPW, N> uses: every caller sizes its array with this (the NV >= 8
+// form also keeps the N x CPW totals behind the partials)
+template <int NV, int CPW, int N>
+constexpr int vblock_lds_floats() {
+  return NV >= 8 ? N * NV * CPW + N * CPW : (NV > 1 ? N * NV * CPW : 1);
+}
+// floats of the fused step's reduction array (its largest vblock_sum: N = NPART)
+template <int TPC, int CPW>
+constexpr int step_lds_floats() {
+  return vblock_lds_floats<TPC * (64 / CPW), CPW, NPART>();
+}
+
 template <int NV, int CPW, int N>
 __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, int cl) {
   if constexpr (NV >= 8) {
@@ -158,7 +170,9 @@ __device__ __forceinline__ void vblock_sum(float (&v)[N], float* lds, int vw, in
     // LDS-only barriers: __syncthreads' workgroup fence would first wait for every global store
     // the leaf / apply rows issued (vmcnt(0): a store round trip per barrier); no thread of the
     // launched step reads global data another thread wrote in the same launch (a chain's lanes
-    // own their rows in both row phases), so only the LDS partials need ordering
+    // own their rows in both row phases: leaf_rows / apply_rows give row d of chain c to one
+    // lane in both, and that rule must hold for any change there), so only the LDS partials
+    // need ordering
     constexpr int NT = NV * CPW;
 #pragma unroll
     for (int i = 0; i < N; ++i) lds[(i * NV + vw) * CPW + cl] = v[i];
@@ -351,9 +365,27 @@ __device__ __forceinline__ void begin_act(const nmx_nuts_config& cfg, const Chai
   NMX_DCHECK(!(A.leaf && is_nuts) || (A.imax < cfg.max_depth_alloc && A.j < cfg.max_depth_alloc));
 }
 
-// Resolve WAIT (sync_chains) and set up the step's inputs.
+// Whether a chain waiting at the end of its transition (sync_chains) may start the next one:
+// every chain of the job has finished that transition.  The count is written by other blocks
+// (and, with chain groups, other streams) while this launch runs, so two loads of it can
+// disagree: a chain whose threads span several waves must take this decision ONCE and share
+// it (fused_step: through LDS, k_chain_step: one thread), or some of its waves start the
+// transition (momentum, first half step) while others keep waiting -- the round-5 lockstep
+// chain-group failure, one 16-chain block of k_nuts_step<8,16> drawing differently.
+__device__ __forceinline__ bool wait_released(const nmx_nuts_config& cfg, const Arena& a, int it) {
+  const int slot_w = it - 1 - cfg.iter_begin;
+  const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
+                      ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : cfg.num_chains;
+  return fin >= cfg.num_chains;
+}
+
+// Resolve WAIT (sync_chains) and set up the step's inputs.  resolve_wait = false leaves a
+// waiting chain in WAIT (begin_act: no work); the caller then decides for the chain as a whole
+// (wait_released above).  Only schedules with one lane per chain, or all of a chain's lanes in
+// one wave (one load instruction serves them all), resolve here.
 __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Arena& a, int c, bool valid,
-                                          ChainScalars& S, Act& A) {
+                                          ChainScalars& S, Act& A, bool resolve_wait = true) {
   // the leaf's potential is loaded with the scalars, whatever the phase (a load behind the
   // phase test would be one more dependent memory round per step)
   float pe_ev = 0.0f;
@@ -364,13 +396,7 @@ __device__ __forceinline__ int begin_step(const nmx_nuts_config& cfg, const Aren
     S.phase = NMX_PH_DONE;
   }
   int ph = S.phase;
-  if (ph == NMX_PH_WAIT) {
-    const int slot_w = S.it - 1 - cfg.iter_begin;
-    const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
-                        ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : cfg.num_chains;
-    if (fin >= cfg.num_chains) ph = NMX_PH_START;
-  }
+  if (ph == NMX_PH_WAIT && resolve_wait && wait_released(cfg, a, S.it)) ph = NMX_PH_START;
   begin_act(cfg, S, ph, A);
   A.pe_eval = A.leaf ? pe_ev : 0.0f;
   return ph;
@@ -766,7 +792,10 @@ __device__ __forceinline__ void leaf_store(const VecCtx& v, const Act& A, float 
   }
 }
 
-// rows d0, d0 + step, ... < d1 of chain column c, ROWS rows per iteration
+// rows d0, d0 + step, ... < d1 of chain column c, ROWS rows per iteration.  Row ownership rule
+// (the fused step's LDS-only barriers depend on it, vblock_sum): the lane that runs row d of
+// chain c here is the one that runs it in apply_rows (same d0 / step), so no lane ever reads a
+// global value another lane of the launch wrote.
 template <bool NUTS, int ROWS, bool PRE1 = (ROWS == 2)>
 __device__ __forceinline__ void leaf_rows(const VecCtx& v, const Act& A, float seff, int d0, int d1, int step, int c,
                                           float* red) {
@@ -1060,7 +1089,7 @@ __device__ __forceinline__ float apply_rows(const VecCtx& v, const Act& A, float
 // made the compiler copy all of it to scratch), a reference to an LDS copy in the persistent
 // loop (by value there, the loop-invariant arguments were hoisted into registers and spilled).
 template <int TPC, int CPW, bool LIST, class PA>
-__device__ __forceinline__ void fused_step(PA P, float* lds) {
+__device__ __forceinline__ void fused_step(PA P, float* lds, int* wait_go = nullptr) {
   constexpr int SUBS = 64 / CPW;
   constexpr int NV = TPC * SUBS;
   const nmx_nuts_config& cfg = P.cfg;
@@ -1082,7 +1111,13 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
 
   ChainScalars S;
   Act A;
-  begin_step(cfg, a, c, valid, S, A);
+  // TPC > 1: a chain's lanes span TPC waves; a waiting chain's release is read once, by its
+  // virtual wave 0, and published through LDS (read after vblock_sum's barriers; a waiting
+  // chain has no leaf, so the rows phase does not depend on it)
+  begin_step(cfg, a, c, valid, S, A, TPC == 1);
+  if constexpr (TPC > 1) {
+    if (vw == 0 && valid && S.phase == NMX_PH_WAIT) wait_go[cl] = wait_released(cfg, a, S.it) ? 1 : 0;
+  }
   const int ph_in = S.phase;  // the stored phase (begin_step's return resolves WAIT)
   const VecCtx v{&a, ldc, D, (size_t)D * ldc, cfg.unit_mass != 0};
   const float seff = valid ? S.step_eff : 0.0f;
@@ -1107,6 +1142,9 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
     else leaf_rows<false, LROWS, LPRE>(v, A, seff, vw, D, NV, c, red);
   }
   vblock_sum<NV, CPW, NPART>(red, lds, vw, cl);
+  if constexpr (TPC > 1) {
+    if (valid && S.phase == NMX_PH_WAIT && wait_go[cl]) begin_act(cfg, S, NMX_PH_START, A);
+  }
   leaf_phase(cfg, S, A, 0.5f * red[0], seed, gch);
   tree_phase(
       cfg, S, A, [&](int i, int side) { return red[1 + 2 * i + side]; },
@@ -1138,8 +1176,9 @@ __device__ __forceinline__ void fused_step(PA P, float* lds) {
 
 template <int TPC, int CPW>
 __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
-  __shared__ float lds[TPC * 64 / CPW > 1 ? NPART * TPC * 64 + NPART * CPW : 1];
-  fused_step<TPC, CPW, true, const StepArgs>(P, lds);
+  __shared__ float lds[step_lds_floats<TPC, CPW>()];
+  __shared__ int wait_go[CPW];  // sync_chains: the release of each waiting chain (fused_step)
+  fused_step<TPC, CPW, true, const StepArgs>(P, lds, wait_go);
 }
 
 // ---- persistent schedule for tiny models ----------------------------
@@ -1150,7 +1189,7 @@ __global__ __launch_bounds__(64 * TPC) void k_nuts_step(StepArgs P) {
 // draws are bitwise those of the launched schedule.  Async schedule only (no sync_chains).
 template <class Pot>
 __global__ __launch_bounds__(64) void k_nuts_persistent(StepArgs P, Pot pot, int max_steps) {
-  __shared__ float lds[64 / SMALL_CPW > 1 ? NPART * 64 : 1];
+  __shared__ float lds[step_lds_floats<1, SMALL_CPW>()];
   __shared__ StepArgs sP;
   if (threadIdx.x == 0) sP = P;
   __syncthreads();
@@ -2387,14 +2426,15 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_chain_step(StepArgs Pk) {
   const bool is_nuts = cfg.algo == NMX_ALGO_NUTS;
   const uint32_t gch = (uint32_t)(cfg.chain_offset + c);
   const uint64_t seed = cfg.seed;
-  int ph = uni_i(AI(NMX_F_PHASE)[c]);
+  int ph = uni_i(AI(NMX_F_PHASE)[c]);  // the same for every wave: only this workgroup writes it
   if (ph == NMX_PH_DONE) return;
   if (ph == NMX_PH_WAIT) {  // sync_chains: start once every chain finished the transition
-    const int slot_w = uni_i(AI(NMX_F_ITER)[c]) - 1 - cfg.iter_begin;
-    const int fin = (slot_w >= 0 && slot_w < cfg.iter_capacity)
-                        ? __hip_atomic_load(&a.finished[slot_w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : cfg.num_chains;
-    if (uni_i(fin) < cfg.num_chains) return;
+    // one thread reads the count for the whole workgroup (wait_released: waves reading it
+    // separately could disagree while other workgroups are still adding to it)
+    __shared__ int sh_go;
+    if (tid == 0) sh_go = wait_released(cfg, a, AI(NMX_F_ITER)[c]) ? 1 : 0;
+    __syncthreads();
+    if (!uni_i(sh_go)) return;
     ph = NMX_PH_START;
   }
   Act A;

@@ -702,12 +702,12 @@ class Engine:
 
     def _groups(self):
         """Chain groups of the launched fused step (1: none): dim <= 256 models whose potential
-        keeps a workspace per concurrently evaluated group, at >= 128 chains per group.  Not with
-        the lockstep schedule (sync_chains): there a group's WAIT phase reads the transition
-        counts the other groups' streams are still writing, and a round-5 GPU suite caught one
-        16-chain block of a two-group lockstep run drawing differently from the one-stream loop."""
+        keeps a workspace per concurrently evaluated group, at >= 128 chains per group.  Also
+        under the lockstep schedule (sync_chains): a waiting chain's release is decided once per
+        chain inside the step (nuts.hip wait_released), so other streams' writes to the
+        transition counts only decide WHEN a chain starts, never what it computes."""
         G = int(self.chain_groups)
-        if G <= 1 or self.dense or self.crow or self.sync_chains or lib().nmx_nuts_num_slices(self.D) > 0:
+        if G <= 1 or self.dense or self.crow or lib().nmx_nuts_num_slices(self.D) > 0:
             return 1
         if getattr(self.potential, "slots", 1) < G or self.C < 128 * G:
             return 1

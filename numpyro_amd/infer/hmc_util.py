@@ -9,12 +9,37 @@ __all__ = ["euclidean_kinetic_energy", "euclidean_kinetic_grad"]
 
 
 def _ravel(r):
-    """ravel_pytree order: dict sites by sorted name, tuples / lists in order, then flattened."""
+    """ravel_pytree (jax.flatten_util): the flat vector and the function mapping a flat vector back
+    to r's structure.  A plain dict flattens by sorted key, an OrderedDict in insertion order (as
+    jax's pytree registry does), tuples / lists in order."""
+    from collections import OrderedDict
+
     if isinstance(r, dict):
-        return torch.cat([torch.as_tensor(r[k]).reshape(-1) for k in sorted(r)])
+        keys = list(r) if isinstance(r, OrderedDict) else sorted(r)
+        leaves = [torch.as_tensor(r[k]) for k in keys]
+        flat = torch.cat([v.reshape(-1) for v in leaves])
+
+        def unravel(v):
+            out, o = OrderedDict() if isinstance(r, OrderedDict) else {}, 0
+            for k, leaf in zip(keys, leaves):
+                n = leaf.numel()
+                out[k] = v[o:o + n].reshape(leaf.shape)
+                o += n
+            return out
+        return flat, unravel
     if isinstance(r, (tuple, list)):
-        return torch.cat([torch.as_tensor(v).reshape(-1) for v in r])
-    return torch.as_tensor(r).reshape(-1)
+        leaves = [torch.as_tensor(v) for v in r]
+        flat = torch.cat([v.reshape(-1) for v in leaves])
+
+        def unravel(v):
+            out, o = [], 0
+            for leaf in leaves:
+                out.append(v[o:o + leaf.numel()].reshape(leaf.shape))
+                o += leaf.numel()
+            return type(r)(out)
+        return flat, unravel
+    t = torch.as_tensor(r)
+    return t.reshape(-1), lambda v: v.reshape(t.shape)
 
 
 def euclidean_kinetic_energy(inverse_mass_matrix, r):
@@ -25,20 +50,30 @@ def euclidean_kinetic_energy(inverse_mass_matrix, r):
         for names, block in inverse_mass_matrix.items():
             ke = ke + euclidean_kinetic_energy(block, tuple(r[k] for k in names))
         return ke
-    r = _ravel(r)
+    r, _ = _ravel(r)
     imm = torch.as_tensor(inverse_mass_matrix, dtype=r.dtype, device=r.device)
+    if imm.dim() not in (1, 2):
+        raise ValueError("inverse_mass_matrix should have 1 or 2 dimensions.")
     v = imm @ r if imm.dim() == 2 else imm * r
     return 0.5 * torch.dot(v, r)
 
 
 def euclidean_kinetic_grad(inverse_mass_matrix, r):
-    """dK/dr = M^-1 r (hmc_util.py:1203-1220), raveled."""
+    """dK/dr = M^-1 r in r's own structure (hmc_util.py:1203-1223): the flat product unraveled
+    like r (ravel_pytree / unravel_fn); for a dict of site-group blocks a {site: grad} dict, each
+    block's momenta taken in the group's order (the reference's OrderedDict r_block)."""
+    from collections import OrderedDict
+
     if isinstance(inverse_mass_matrix, dict):
-        return torch.cat([euclidean_kinetic_grad(b, tuple(r[k] for k in names))
-                          for names, b in inverse_mass_matrix.items()])
-    r = _ravel(r)
-    imm = torch.as_tensor(inverse_mass_matrix, dtype=r.dtype, device=r.device)
-    return imm @ r if imm.dim() == 2 else imm * r
+        r_grad = {}
+        for names, block in inverse_mass_matrix.items():
+            r_grad.update(euclidean_kinetic_grad(block, OrderedDict((k, r[k]) for k in names)))
+        return r_grad
+    flat, unravel = _ravel(r)
+    imm = torch.as_tensor(inverse_mass_matrix, dtype=flat.dtype, device=flat.device)
+    if imm.dim() not in (1, 2):
+        raise ValueError("inverse_mass_matrix should have 1 or 2 dimensions.")
+    return unravel(imm @ flat if imm.dim() == 2 else imm * flat)
 
 
 euclidean_kinetic_energy._kinetic_grad = euclidean_kinetic_grad

@@ -137,6 +137,16 @@ class MCMC:
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             return None  # one process per GPU: this rank's shard lives on its device
         if self.devices is None:
+            if self.chain_method == "parallel" and self.local_chains > 1 and not getattr(MCMC, "_warned_devices", False):
+                n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+                if n > 1:
+                    # the reference's "parallel" pmaps over every local device (mcmc.py:700-715);
+                    # here that is opt-in, so a multi-GPU script would silently use one device
+                    MCMC._warned_devices = True
+                    warnings.warn(f"chain_method='parallel' runs on one GPU unless devices= is given; {n} GPUs "
+                                  "are visible: pass devices='all' to shard the chains over them as the reference's "
+                                  "pmap does (or launch one process per GPU with torch.distributed)",
+                                  UserWarning, stacklevel=4)
             return None
         devs = self.devices
         devs = devs[:max(1, self.local_chains)]

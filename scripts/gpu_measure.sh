@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 5 end-of-round measurement: in-run HBM traffic of the headline (FETCH_SIZE and
+# end-of-round measurement (usage: bash scripts/gpu_measure.sh [OUT_DIR]): in-run HBM traffic of the headline (FETCH_SIZE and
 # WRITE_SIZE in separate passes), the default bench line, and the headline's rocprof kernel stats
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r05/final_bench
+O=${1:-gpurun_out/measure}
 mkdir -p $O/t
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/t/f -o p -- python3 bench.py --steps 20 --warmup 5 --configs none --no-cpu-baseline > $O/t/f.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/t/w -o p -- python3 bench.py --steps 20 --warmup 5 --configs none --no-cpu-baseline > $O/t/w.log 2>&1 || exit 1

@@ -264,3 +264,37 @@ def test_euclidean_kinetic_energy_matches_oracle():
     blocks = {("a", "b"): torch.tensor(dense[:3, :3]), ("c",): torch.tensor(diag[3:])}
     want = H.euclidean_kinetic_energy(dense[:3, :3], r[:3]) + H.euclidean_kinetic_energy(diag[3:], r[3:])
     np.testing.assert_allclose(float(ke(blocks, rd)), want, rtol=1e-12)
+
+
+def test_euclidean_kinetic_grad_keeps_the_momentum_structure():
+    """_euclidean_kinetic_energy_grad (hmc_util.py:1203-1223) returns M^-1 r in r's pytree shape:
+    a dict momentum with a structured (dict-of-blocks) mass gives a {site: grad} dict whose block
+    momenta are taken in the group's order (r_block = OrderedDict over site_names), not in sorted
+    order; a dict momentum with one dense matrix is unraveled by sorted key (ravel_pytree)."""
+    import numpy as np
+    import torch
+
+    from numpyro_amd.infer.hmc_util import euclidean_kinetic_grad as kg
+
+    rs = np.random.RandomState(1)
+    rd = {"b": torch.tensor(rs.randn(2, 1)), "a": torch.tensor(rs.randn(3)), "c": torch.tensor(rs.randn(2))}
+    q = rs.randn(5, 5)
+    dense5 = torch.tensor(q @ q.T + np.eye(5))
+    # group ("b", "a"): the block's coordinates are b (2) then a (3), against the block as given
+    blocks = {("b", "a"): dense5, ("c",): torch.tensor(rs.rand(2) + 0.5)}
+    g = kg(blocks, rd)
+    assert set(g) == {"a", "b", "c"} and g["b"].shape == (2, 1) and g["a"].shape == (3,)
+    v = dense5 @ torch.cat([rd["b"].reshape(-1), rd["a"]])
+    torch.testing.assert_close(g["b"].reshape(-1), v[:2])
+    torch.testing.assert_close(g["a"], v[2:])
+    torch.testing.assert_close(g["c"], blocks[("c",)] * rd["c"])
+    # one dense matrix over a dict momentum: sorted-key ravel (a, b, c), unraveled back
+    d7 = torch.tensor(np.eye(7) * 2.0 + 0.1)
+    g2 = kg(d7, rd)
+    flat = torch.cat([rd["a"], rd["b"].reshape(-1), rd["c"]])
+    v2 = d7 @ flat
+    torch.testing.assert_close(torch.cat([g2["a"], g2["b"].reshape(-1), g2["c"]]), v2)
+    assert g2["b"].shape == (2, 1)
+    # tuple momentum stays a tuple
+    gt = kg(torch.tensor([1.0, 2.0, 3.0]), (torch.tensor([1.0]), torch.tensor([1.0, 1.0])))
+    assert isinstance(gt, tuple) and gt[1].tolist() == [2.0, 3.0]

@@ -785,13 +785,15 @@ def test_frontend_models_run_like_fused_models(device, which):
     np.testing.assert_array_equal(na.cpu().numpy(), nb.cpu().numpy())
 
 
-@pytest.mark.parametrize("groups,C,sync", [(2, 256, False), (4, 512, False), (2, 256, True)])
+@pytest.mark.parametrize("groups,C,sync", [(2, 256, False), (4, 512, False), (2, 256, True), (4, 512, True)])
 def test_chain_groups_are_bitwise_the_one_stream_loop(device, groups, C, sync, monkeypatch):
     """Chain groups (nmx_nuts_config.num_groups): the launched fused step and the covtype
     potential per group on its own stream, each group with its own compacted lists and DONE
     count.  A chain's computation does not depend on its group or on how the streams
-    interleave: draws, tree sizes and energies equal the one-stream loop bitwise.  The lockstep
-    schedule (sync) runs one group whatever is asked (Engine._groups)."""
+    interleave: draws, tree sizes and energies equal the one-stream loop bitwise -- also under
+    the lockstep schedule (sync), where a waiting chain's release is read while other groups'
+    streams are still adding to the transition counts (decided once per chain: nuts.hip
+    wait_released; round 5 caught a 16-chain block whose waves disagreed)."""
     from numpyro_amd.engine import Engine
 
     X, y = datasets.covtype_synthetic(n_rows=4000, seed=1)
@@ -799,7 +801,7 @@ def test_chain_groups_are_bitwise_the_one_stream_loop(device, groups, C, sync, m
     for G in (1, groups):
         monkeypatch.setattr(Engine, "chain_groups", G)
         mcmc, _ = _run_engine((X, y), P.logistic_regression, C, 30, 12, 3, sync=sync)
-        assert mcmc._engine._groups() == (1 if sync else G)
+        assert mcmc._engine._groups() == G
         ef = mcmc.get_extra_fields(True)
         out[G] = (mcmc.get_samples(True)["coefs"].cpu().numpy(), ef["num_steps"].cpu().numpy(),
                   ef["potential_energy"].cpu().numpy())
