@@ -433,7 +433,7 @@ int nmx_pack_rows(const float* in, int ldc, int dim, const int32_t* list, const 
 int nmx_unpack_rows(const float* in, int ldi, int dim, const int32_t* list, const int32_t* count, float* out,
                     int ldc, const float* pe_in, float* pe_out, void* stream);
 /* Per-chain dense mass matrices (the reference's per-chain adaptation, hmc.py:790-798 vmapped
- * init_kernel; hmc_util.py:133-239 welford_covariance(diagonal=False)), dim <= 256.
+ * init_kernel; hmc_util.py:133-239 welford_covariance(diagonal=False)); these two: dim <= 256.
  * nmx_chain_matvec: out[a][c] = sum_b M[c][b][a] in[b][c] for the listed chains (list/count),
  * or the chains with phase >= LEAF (list NULL; phase NULL = every chain < num_chains);
  * M [C][dim][dim] f32: T_c^T row-major gives z = T_c w, T_c row-major gives g_w = T_c^T g_z.
@@ -444,6 +444,16 @@ int nmx_chain_matvec(const float* M, int dim, const float* in, float* out, int l
                      const int32_t* count, const int32_t* phase, int num_chains, void* stream);
 int nmx_chain_welford(const float* z, int dim, int ldc, int num_chains, int n, float* mean, float* m2,
                       void* stream);
+/* The same for dim <= 4096 (the same hmc.py:790-798 / hmc_util.py:133-239 semantics; above dim
+ * 256 a workgroup per (chain, 256 outputs) and a two-launch Welford).  tri: 0 full M, 1 forward
+ * with T_c upper triangular (M = T_c^T: rows b < a are zero), 2 backward (M = T_c: rows b > a
+ * are zero) -- the zero rows are skipped.  nmx_chain_welford_ws needs `work` of
+ * nmx_chain_welford_work_bytes(dim, num_chains) bytes (0 up to dim 256). */
+int nmx_chain_matvec_tri(const float* M, int dim, const float* in, float* out, int ldc, const int32_t* list,
+                         const int32_t* count, const int32_t* phase, int num_chains, int tri, void* stream);
+size_t nmx_chain_welford_work_bytes(int dim, int num_chains);
+int nmx_chain_welford_ws(const float* z, int dim, int ldc, int num_chains, int n, float* mean, float* m2,
+                         float* work, void* stream);
 /* Multivariate normal, U = 0.5 (z-mu)^T P (z-mu), grad = P z - P mu (one nmx_gemm_chains
  * with At = P^T, bias = -P mu) then the per-chain quadratic form: the dense-mass test
  * targets of test/infer/test_mcmc.py:73-100 and :313-343. */

@@ -501,6 +501,8 @@ template <int CT, int RW = 4>
 constexpr int x3_pieces() { return 2 * (RW * 3 + CT * 3); }  // per 32-deep stage: A 2 x 3 RW, B 2 x 3 CT pieces of 1 KB
 constexpr int X3_PIECES = x3_pieces<2>();
 
+constexpr int X3_BLK = 8;  // stages (of 32 k) per block sum in k_gemm_x3
+
 template <int CT, int NBUF, int RW>
 __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_x3(const char* __restrict__ Ap, int lda, int D,
                                                     const char* __restrict__ Bp, float* __restrict__ Out,
@@ -597,7 +599,14 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
   // item 7).  The staged pieces keep the 32 x 16 fragment order of k_x3_pack_a / k_x3_split_b:
   // lane (r16, q) of a sub-tile reads row / chain 16 m + r16, k-group q of the stage, i.e.
   // k-step q >> 1, half q & 1 of the piece: lane index (q & 1) * 32 + 16 m + r16.
-  f32x4 acc[CT][2][2], cor[CT][2][2];  // a1b1 / the five correction products
+  // a1b1 of the current block of X3_BLK stages / the running total of the finished blocks / the
+  // five correction products.  The MFMA rounds its running sum into the accumulator every few
+  // products (the measured error of one accumulator over K = 5038 was 1.7x a float32 sgemm's,
+  // which a model rounding every 8 products reproduces); summing each 256-deep block in a fresh
+  // accumulator and the blocks in a second one rounds at the block sum's scale instead: 0.4x
+  // sgemm's in that model.  Block boundaries are absolute stage indices (multiples of
+  // X3_BLK), so skipped all-zero triangle stages and the tile shape leave the sums unchanged.
+  f32x4 acc[CT][2][2], tot[CT][2][2], cor[CT][2][2];
 #pragma unroll
   for (int cl = 0; cl < CT; ++cl)
 #pragma unroll
@@ -605,7 +614,20 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[cl][m][n][r] = cor[cl][m][n][r] = 0.0f;
+        for (int r = 0; r < 4; ++r) acc[cl][m][n][r] = tot[cl][m][n][r] = cor[cl][m][n][r] = 0.0f;
+  auto flush = [&]() {
+#pragma unroll
+    for (int cl = 0; cl < CT; ++cl)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            tot[cl][m][n][r] += acc[cl][m][n][r];
+            acc[cl][m][n][r] = 0.0f;
+          }
+  };
   const int r16 = lane & 15, q = lane >> 4;
   const int qs = q >> 1, ql = (q & 1) * 32 + r16;  // k-step and lane index within the piece
   if (kt_begin < nk) issue(kt_begin, 0);
@@ -649,7 +671,9 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
         }
     }
     buf = buf + 1 == NBUF ? 0 : buf + 1;
+    if ((kt + 1) % X3_BLK == 0) flush();
   }
+  flush();
 #pragma unroll
   for (int cl = 0; cl < CT; ++cl)
 #pragma unroll
@@ -657,7 +681,7 @@ __global__ __launch_bounds__(64 * RW, (RW == 4 && CT == 2) ? 2 : 1) void k_gemm_
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[cl][m][n][r] += cor[cl][m][n][r];
+        for (int r = 0; r < 4; ++r) acc[cl][m][n][r] = tot[cl][m][n][r] + cor[cl][m][n][r];
   // lane (c16, q) of sub-tile (m, n) holds rows 16 m + 4 q + j (j = 0..3) of chain 16 n + c16
   if (out_list) {
     // scattered to the listed chains' rows (Out [.][D], NMX_LAYOUT_CHAIN_ROWS; one K-split): 4

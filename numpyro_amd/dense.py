@@ -415,7 +415,7 @@ def assemble_inverse_mass_matrix(sites, dense_mass, inverse_mass_matrix):
 
 
 # --------------------------------------------------------------------------------------- per chain
-CHAIN_DENSE_MAX_D = 256
+CHAIN_DENSE_MAX_D = 4096  # nmx_chain_matvec_tri / nmx_chain_welford_ws (dense_chain.hip)
 
 
 class MassBlocks:
@@ -534,16 +534,34 @@ class ChainWhitening:
         return self.T.transpose(-1, -2)  # tril_inv
 
     def mass_matrix_sqrt(self):
-        # tril_inv^-1 per chain (hmc_util.py:226-231 cov_inv_sqrt)
-        eye = torch.eye(self.D, dtype=torch.float64, device=self.device).expand(self.C, self.D, self.D)
-        if self.blocks is not None:  # block-triangular up to the blocks' coordinate order
-            return torch.linalg.solve(self.T.transpose(-1, -2), eye)
-        return torch.linalg.solve_triangular(self.T.transpose(-1, -2), eye, upper=False)
+        # tril_inv^-1 per chain (hmc_util.py:226-231 cov_inv_sqrt), in chunks of chains: batched
+        # hipBLAS trsm fails to allocate its workspace for large right-hand sides (256 chains of
+        # dim 512 x 512 identities), as for the pooled matrix's column chunks (Whitening.tinv)
+        out = torch.empty(self.C, self.D, self.D, dtype=torch.float64, device=self.device)
+        eye = torch.eye(self.D, dtype=torch.float64, device=self.device)
+        step = max(1, (1 << 22) // (self.D * self.D))
+        for a in range(0, self.C, step):
+            Lt = self.T[a:a + step].transpose(-1, -2)
+            rhs = eye.expand(Lt.shape[0], self.D, self.D)
+            if self.blocks is not None:  # block-triangular up to the blocks' coordinate order
+                out[a:a + step] = torch.linalg.solve(Lt, rhs)
+            else:
+                out[a:a + step] = torch.linalg.solve_triangular(Lt, rhs, upper=False)
+        return out
+
+    def tri(self, forward):
+        """nmx_chain_matvec_tri's triangle flag: T_c upper triangular (one dense block) lets the
+        large-dim products skip the zero rows of T_c^T (forward) / T_c (backward)."""
+        return 0 if self.blocks is not None else (1 if forward else 2)
+
+    def matvec(self, forward, x, out, list_, count, phase, num_chains, ldc, stream):
+        """out[:, c] = T_c x[:, c] (forward) or T_c^T x[:, c] on raw pointers (nmx_chain_matvec_tri)."""
+        check(lib().nmx_chain_matvec_tri(ptr(self.fwd if forward else self.bwd), self.D, x, out, ldc, list_, count,
+                                         phase, int(num_chains), self.tri(forward), stream), "nmx_chain_matvec_tri")
 
     def to_model(self, w, out, phase=None, num_chains=None, stream=0):
         """out[:, c] = T_c w[:, c] for [D, ldc] buffers (chains < C)."""
-        check(lib().nmx_chain_matvec(ptr(self.fwd), self.D, ptr(w), ptr(out), w.shape[-1], None, None, ptr(phase),
-                                     int(num_chains or self.C), stream), "nmx_chain_matvec")
+        self.matvec(True, ptr(w), ptr(out), None, None, ptr(phase), num_chains or self.C, w.shape[-1], stream)
 
     def to_whitened(self, z):
         """w_c = T_c^-1 z_c for z [D, C]."""
@@ -581,7 +599,6 @@ class ChainWhitenedPotential(Potential):
 
     def evaluate(self, ev, stream):
         wt = self.whitening
-        L = lib()
         key = (ev.active_idx, ev.active_count, ev.pe, ev.phase, ev.num_chains)
         b = self._batches.get(key)
         if b is None:
@@ -589,11 +606,9 @@ class ChainWhitenedPotential(Potential):
                           active_count=ev.active_count, num_chains=ev.num_chains, ldc=ev.ldc)
             self._batches[key] = b
         b.num_chains = ev.num_chains
-        check(L.nmx_chain_matvec(ptr(wt.fwd), self.dim, ev.z, ptr(self.zb), ev.ldc, ev.active_idx, ev.active_count,
-                                 ev.phase, ev.num_chains, stream), "nmx_chain_matvec")
+        wt.matvec(True, ev.z, ptr(self.zb), ev.active_idx, ev.active_count, ev.phase, ev.num_chains, ev.ldc, stream)
         self.base.evaluate(b, stream)
-        check(L.nmx_chain_matvec(ptr(wt.bwd), self.dim, ptr(self.gb), ev.grad, ev.ldc, ev.active_idx,
-                                 ev.active_count, ev.phase, ev.num_chains, stream), "nmx_chain_matvec")
+        wt.matvec(False, ptr(self.gb), ev.grad, ev.active_idx, ev.active_count, ev.phase, ev.num_chains, ev.ldc, stream)
 
 
 class ChainWelford:
@@ -604,13 +619,15 @@ class ChainWelford:
         self.D, self.C = int(dim), int(num_chains)
         self.mean = torch.zeros(self.C, self.D, dtype=torch.float32, device=device)
         self.m2 = torch.zeros(self.C, self.D, self.D, dtype=torch.float32, device=device)
+        nb = lib().nmx_chain_welford_work_bytes(self.D, self.C)  # dim > 256: delta vectors [C][2][D]
+        self.work = torch.empty(nb, dtype=torch.uint8, device=device) if nb else None
         self.n = 0
 
     def add(self, z, stream=0):
         """z: [D, ldc] model-space draws of every chain."""
         self.n += 1
-        check(lib().nmx_chain_welford(ptr(z), self.D, z.shape[-1], self.C, self.n, ptr(self.mean), ptr(self.m2),
-                                      stream), "nmx_chain_welford")
+        check(lib().nmx_chain_welford_ws(ptr(z), self.D, z.shape[-1], self.C, self.n, ptr(self.mean), ptr(self.m2),
+                                         ptr(self.work), stream), "nmx_chain_welford_ws")
 
     def finalize(self, regularize=True, blocks=None):
         """final_fn (hmc_util.py:198-237) per chain: cov [C, D, D] float64 (masked to the

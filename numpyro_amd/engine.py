@@ -398,9 +398,8 @@ class Engine:
         wt = self.potential.whitening
         a, b = torch.empty_like(eps), torch.empty_like(eps)
         if self.chain_dense:
-            for m, x, o in ((wt.bwd, eps, a), (wt.fwd, a, b), (wt.bwd, b, a)):
-                check(lib().nmx_chain_matvec(ptr(m), self.D, ptr(x), ptr(o), self.ldc, None, None, None, self.C, s),
-                      "nmx_chain_matvec")
+            for fwd, x, o in ((False, eps, a), (True, a, b), (False, b, a)):
+                wt.matvec(fwd, ptr(x), ptr(o), None, None, None, self.C, self.ldc, s)
         else:
             for fwd, x, o in ((False, eps, a), (True, a, b), (False, b, a)):
                 wt.product(fwd, ptr(x), ptr(o), None, None, None, self.C, self.ldc, s)

@@ -183,6 +183,23 @@ def init_to_uniform(site=None, radius=2):
     return ("uniform", float(radius))
 
 
+def _flatten_init(pot, init_params, num_chains):
+    """init_params (a dict of sites with a leading chain dimension, or [C, D] / [D]) -> [C, D];
+    for one chain of a potential_fn the reference's unbatched values are accepted too."""
+    import torch
+
+    from ..potentials import TorchPotential
+
+    if isinstance(pot, TorchPotential) and num_chains == 1:
+        if isinstance(init_params, dict):
+            init_params = {k: torch.as_tensor(v)[None] for k, v in init_params.items()}
+        else:
+            init_params = torch.as_tensor(init_params).reshape(1, -1)
+    elif isinstance(pot, TorchPotential) and not isinstance(init_params, dict):
+        init_params = torch.as_tensor(init_params).reshape(num_chains, -1)
+    return pot.flatten(init_params) if isinstance(init_params, dict) else init_params
+
+
 class HMC(MCMCKernel):
     """Hamiltonian Monte Carlo with fixed trajectory length (numpyro/infer/hmc.py:541-822)."""
 
@@ -228,8 +245,9 @@ class HMC(MCMCKernel):
         if model is not None and not (isinstance(model, FusedModel) or callable(model)):
             raise TypeError("`model` must be a model function (numpyro_amd.sample / plate / distributions, "
                             "mapped onto a fused kernel by numpyro_amd.frontend) or a fused model")
-        if potential_fn is not None and not isinstance(potential_fn, Potential):
-            raise TypeError("`potential_fn` must be a numpyro_amd.potentials.Potential")
+        if potential_fn is not None and not (isinstance(potential_fn, Potential) or callable(potential_fn)):
+            raise TypeError("`potential_fn` must be a callable of the unconstrained parameters (torch "
+                            "operations) or a numpyro_amd.potentials.Potential")
         self._model = model
         self._potential_fn = potential_fn
         self._step_size = float(step_size)
@@ -244,7 +262,9 @@ class HMC(MCMCKernel):
         self._init_strategy = init_strategy
         self._regularize_mass_matrix = regularize_mass_matrix
         self._find_heuristic_step_size = bool(find_heuristic_step_size)
-        self._potential = potential_fn
+        # a plain callable becomes a TorchPotential once init_params show its argument structure
+        # (bind_potential_fn); a Potential is used as given
+        self._potential = potential_fn if isinstance(potential_fn, Potential) else None
         self._sample_fn = None
 
     @property
@@ -278,7 +298,34 @@ class HMC(MCMCKernel):
             inverse_mass_matrix=self._inverse_mass_matrix,
             find_heuristic_step_size=self._find_heuristic_step_size)
 
+    def bind_potential_fn(self, init_params, num_chains):
+        """A callable ``potential_fn`` (hmc.py:127-130: a function of one chain's unconstrained
+        values) is wrapped as a TorchPotential whose site structure is that of ``init_params``
+        (required with ``potential_fn``, hmc.py:754-757); batched init_params carry a leading
+        chain dimension when num_chains > 1.  No-op for models and Potential objects."""
+        fn = self._potential_fn
+        if fn is None or isinstance(fn, Potential):
+            return
+        if init_params is None:
+            if self._potential is None:
+                raise ValueError("Valid value of `init_params` must be provided with `potential_fn`.")
+            return
+        import torch
+
+        from ..potentials import TorchPotential
+
+        def one(v):
+            v = torch.as_tensor(v)
+            return v[0] if num_chains > 1 else v
+
+        example = {k: one(v) for k, v in init_params.items()} if isinstance(init_params, dict) else one(init_params)
+        old = self._potential
+        if old is None or old.sites != TorchPotential(fn, example).sites:
+            self._potential = TorchPotential(fn, example)
+
     def potential(self, model_args=(), model_kwargs=None) -> Potential:
+        if self._potential_fn is not None and self._potential is None:
+            raise ValueError("Valid value of `init_params` must be provided with `potential_fn`.")
         if isinstance(self._model, FusedModel):
             self._potential = self._model.potential(*model_args, **(model_kwargs or {}))
         elif self._model is not None:
@@ -327,11 +374,12 @@ class HMC(MCMCKernel):
             else:
                 num_chains = 1
         seed = key_to_seed(keys)
+        self.bind_potential_fn(init_params, int(num_chains))
         eng = self.make_engine(int(num_chains), model_args, model_kwargs, device=device,
                                chain_offset=chain_offset)
         ip = None
         if init_params is not None:
-            ip = eng.potential.flatten(init_params) if isinstance(init_params, dict) else init_params
+            ip = _flatten_init(eng.potential, init_params, int(num_chains))
             ip = torch.as_tensor(ip, dtype=torch.float32)
             if ip.dim() == 1:
                 ip = ip[None, :].expand(eng.C, -1)

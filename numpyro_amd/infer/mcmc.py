@@ -124,7 +124,8 @@ class MCMC:
 
     # ------------------------------------------------------------------ engine
     def _get_engine(self, args, kwargs):
-        key = (id(self.sampler), tuple(id(a) for a in args), tuple(sorted((k, id(v)) for k, v in kwargs.items())))
+        key = (id(self.sampler), tuple(id(a) for a in args), tuple(sorted((k, id(v)) for k, v in kwargs.items())),
+               id(getattr(self.sampler, "_potential", None)) if getattr(self.sampler, "_potential_fn", None) else 0)
         if self._engine is None or self._engine_key != key:
             dev = self.device if self.device is not None or not self.devices else self.devices[0]
             self._engine = self.sampler.make_engine(self.local_chains, args, kwargs, device=dev,
@@ -165,10 +166,16 @@ class MCMC:
                 lo, hi = shard_chains(self.local_chains, g, len(devs))
                 if pot_fn is not None and g > 0:
                     # a user potential object binds to one device: the other shards get copies
-                    # (a pickled potential is unbound)
-                    from ..engine import Engine
+                    # (a pickled potential is unbound; a torch potential_fn wrapper is copied: its
+                    # function need not pickle)
+                    import copy
 
-                    eng = Engine(pickle.loads(pickle.dumps(pot_fn)), hi - lo, self.sampler.options(), device=dev,
+                    from ..engine import Engine
+                    from ..potentials import TorchPotential
+
+                    pot = self.sampler._potential
+                    pot = copy.copy(pot) if isinstance(pot, TorchPotential) else pickle.loads(pickle.dumps(pot))
+                    eng = Engine(pot, hi - lo, self.sampler.options(), device=dev,
                                  chain_offset=self.chain_lo + lo, sync_chains=self.sync_chains)
                 else:
                     eng = self.sampler.make_engine(hi - lo, args, kwargs, device=dev, chain_offset=self.chain_lo + lo,
@@ -230,6 +237,9 @@ class MCMC:
                                  f"available: {native.COLLECT}")
         self._collected = tuple(collect)
         seed = key_to_seed(rng_key)
+        bind = getattr(self.sampler, "bind_potential_fn", None)
+        if bind is not None and resume is None:
+            bind(init_params, self.local_chains)
         devs = self._run_devices()
         if devs is not None:
             return self._run_multi(devs, seed, args, kwargs, init_params, n_iter, lower, resume)
@@ -243,10 +253,10 @@ class MCMC:
             else:
                 ip = None
                 if init_params is not None:
-                    ip = init_params
-                    if isinstance(ip, dict):
-                        ip = eng.potential.flatten(ip)
-                    ip = torch.as_tensor(ip, dtype=torch.float32)
+                    from .hmc import _flatten_init
+
+                    ip = torch.as_tensor(_flatten_init(eng.potential, init_params, self.local_chains),
+                                         dtype=torch.float32)
                     if ip.dim() == 1:
                         ip = ip[None, :].expand(eng.C, -1)
                     if ip.shape[0] == self.num_chains and self.local_chains != self.num_chains:
@@ -279,10 +289,10 @@ class MCMC:
         G = len(engines)
         ip_all = None
         if resume is None and init_params is not None:
-            ip_all = init_params
-            if isinstance(ip_all, dict):
-                ip_all = engines[0].potential.flatten(ip_all)
-            ip_all = torch.as_tensor(ip_all, dtype=torch.float32)
+            from .hmc import _flatten_init
+
+            ip_all = torch.as_tensor(_flatten_init(engines[0].potential, init_params, self.local_chains),
+                                     dtype=torch.float32)
             if ip_all.dim() == 1:
                 ip_all = ip_all[None, :].expand(self.local_chains, -1)
             if ip_all.shape[0] != self.local_chains:
@@ -366,7 +376,10 @@ class MCMC:
         return out
 
     def get_samples(self, group_by_chain=False):
-        return self._site_arrays(group_by_chain)
+        out = self._site_arrays(group_by_chain)
+        if getattr(self._model_potential(), "array_site", False) and self.postprocess_fn is None:
+            return out["z"]  # potential_fn over one array: the samples are that array (mcmc.py:761-786)
+        return out
 
     def get_extra_fields(self, group_by_chain=False):
         out = {}

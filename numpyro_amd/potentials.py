@@ -386,3 +386,107 @@ multivariate_normal = FusedModel(
     "x ~ MultivariateNormal(loc, covariance_matrix | precision_matrix)")
 
 LOG_2PI = math.log(2 * math.pi)
+
+
+# ------------------------------------------------------------------ generic (torch) potential
+class _DevicePtr:
+    """A raw device buffer as a torch tensor (the __cuda_array_interface__ protocol, which torch
+    imports without a copy): the engine hands potentials raw pointers (nmx_eval_batch)."""
+
+    def __init__(self, p, shape, typestr, strides=None):
+        self.__cuda_array_interface__ = {"data": (int(p), False), "shape": tuple(shape), "typestr": typestr,
+                                         "strides": strides, "version": 2}
+
+
+def _wrap(p, shape, dtype, device):
+    typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+    return torch.as_tensor(_DevicePtr(p, shape, typestr), device=device)
+
+
+class TorchPotential(Potential):
+    """A user ``potential_fn`` (numpyro/infer/hmc.py:127-130): ``U = fn(z)`` over ONE chain's
+    unconstrained values -- a dict {site: tensor} like ``init_params`` (ravel_pytree order: sorted
+    names) or a single tensor -- written with torch operations.  ``U`` and ``dU/dz`` of the
+    evaluated chains come from ``torch.func.vmap(torch.func.grad_and_value(fn))``, the analogue of
+    the reference's vmapped ``jax.value_and_grad(potential_fn)`` (hmc_util.py:242-252,
+    hmc.py:797).  This is the generic path: torch kernels on the compacted list of chains that
+    need a leaf, with no fused HIP potential -- a model with a registered fused kernel (the
+    ``numpyro_amd.potentials`` FusedModels, or a traced model the front end maps onto one) is the
+    fast path.  No host synchronisation: the listed chains are gathered and their results
+    scattered back on the device, positions past the list's count leaving the arena untouched.
+    A function that ``vmap`` cannot trace (data-dependent Python control flow) is evaluated one
+    chain at a time instead (correct, slow)."""
+
+    def __init__(self, fn, example):
+        self.fn = fn
+        if isinstance(example, dict):
+            self.array_site = False
+            names = sorted(example)
+            self.sites = [(k, tuple(torch.as_tensor(example[k]).shape), REAL) for k in names]
+        else:
+            self.array_site = True
+            self.sites = [("z", tuple(torch.as_tensor(example).shape), REAL)]
+        self.dim = int(sum(int(np.prod(s, dtype=np.int64)) for _, s, _ in self.sites))
+        if self.dim <= 0:
+            raise ValueError("potential_fn: init_params hold no coordinates")
+        self._vmap_ok = None
+
+    def structure(self, flat):
+        """[..., D] -> fn's argument structure (dict of sites, or the single tensor)."""
+        if self.array_site:
+            return flat.reshape(*flat.shape[:-1], *self.sites[0][1])
+        return self.unflatten(flat)
+
+    def _value_and_grad(self, zc):
+        """(U [n], dU/dz [n, D]) of the rows of zc [n, D]."""
+        def u(zf):
+            return self.fn(self.structure(zf))
+
+        if self._vmap_ok is not False:
+            try:
+                g, v = torch.func.vmap(torch.func.grad_and_value(u))(zc)
+                self._vmap_ok = True
+                return v.to(torch.float32), g.to(torch.float32)
+            except Exception:  # noqa: BLE001  (a function vmap cannot trace: evaluated per chain)
+                if self._vmap_ok:
+                    raise
+                self._vmap_ok = False
+        vals, grads = [], []
+        for row in zc:
+            x = row.detach().clone().requires_grad_(True)
+            val = torch.as_tensor(u(x), dtype=torch.float32)
+            (gr,) = torch.autograd.grad(val, x)
+            vals.append(val.detach())
+            grads.append(gr)
+        return torch.stack(vals), torch.stack(grads)
+
+    def evaluate(self, ev, stream):
+        dev, D, ldc = self.device, self.dim, int(ev.ldc)
+        st = torch.cuda.ExternalStream(stream, device=dev) if stream else torch.cuda.default_stream(dev)
+        with torch.cuda.stream(st), torch.no_grad():
+            Z = _wrap(ev.z, (D, ldc), torch.float32, dev)
+            G = _wrap(ev.grad, (D, ldc), torch.float32, dev)
+            PE = _wrap(ev.pe, (ldc,), torch.float32, dev)
+            n = min(int(ev.num_chains), ldc)
+            pos = torch.arange(n, device=dev)
+            if ev.active_idx:
+                chains = _wrap(ev.active_idx, (ldc,), torch.int32, dev)[:n].long().clamp(0, ldc - 1)
+                valid = pos < _wrap(ev.active_count, (1,), torch.int32, dev).long()
+            else:
+                chains = pos
+                valid = (_wrap(ev.phase, (ldc,), torch.int32, dev)[:n] >= native.PH_LEAF) if ev.phase \
+                    else torch.ones(n, dtype=torch.bool, device=dev)
+            zc = Z.t()[chains]  # [n, D]
+        with torch.cuda.stream(st):
+            u, g = self._value_and_grad(zc)
+        with torch.cuda.stream(st), torch.no_grad():
+            # positions past the count (or not selected) write the first valid position's values to
+            # its own chain -- identical duplicates -- or, with none valid, chain 0's old values
+            first = torch.argmax(valid.to(torch.int32))
+            anyv = valid.any()
+            tgt = torch.where(valid, chains, chains[first])
+            old_g, old_u = G.t()[chains[first]], PE[chains[first]]
+            fill_g = torch.where(anyv, g[first], old_g)
+            fill_u = torch.where(anyv, u[first], old_u)
+            G.t()[tgt] = torch.where(valid[:, None], g, fill_g[None, :])
+            PE[tgt] = torch.where(valid, u, fill_u)

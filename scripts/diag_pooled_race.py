@@ -16,8 +16,6 @@ linalg_lock replaced by a no-op), the configuration of the failing round-5 run.
 usage: python scripts/diag_pooled_race.py [--reps K] [--dim D] [--unlocked] [--out FILE]
 """
 import argparse
-import contextlib
-import hashlib
 import json
 import os
 import sys
@@ -28,13 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from numpyro_amd import potentials as P  # noqa: E402
-from numpyro_amd import shard  # noqa: E402
-from numpyro_amd.engine import Engine  # noqa: E402
 from numpyro_amd.infer import MCMC, NUTS  # noqa: E402
-
-
-def h(t):
-    return hashlib.sha1(t.detach().contiguous().cpu().numpy().tobytes()).hexdigest()[:16]
 
 
 def main():
@@ -46,44 +38,19 @@ def main():
     ap.add_argument("--out", default="gpurun_out/diag_pooled_race.json")
     a = ap.parse_args()
 
-    rec = []  # per window end: {rank, stage: hash}
-    orig_reduce = shard.DeviceGroup.all_reduce_sum
-    orig_reexpress = Engine._reexpress
-    orig_init = shard.DeviceGroup.__init__
-
-    def init(self, size):
-        orig_init(self, size)
-        if a.unlocked:
-            self.linalg_lock = contextlib.nullcontext()
-
-    def reduce(self, rank, tensors):
-        out = orig_reduce(self, rank, tensors)
-        rec.append({"rank": rank, "stage": "moments", "n": float(out[0].item()), "s1": h(out[1]), "s2": h(out[2])})
-        return out
-
-    def reexpress(self, imm, mu, s):
-        rank = self.device_group[1] if self.device_group is not None else 0
-        e = {"rank": rank, "stage": "window_end", "cov": h(imm), "mean": h(mu) if mu is not None else None}
-        orig_reexpress(self, imm, mu, s)
-        torch.cuda.synchronize()
-        wt = self.potential.whitening
-        e.update(T=h(wt.T), tinv=h(wt.tinv()), fwd_t=h(wt.fwd_t), w=h(self.view("z")[:, :self.C]))
-        rec.append(e)
-
-    shard.DeviceGroup.__init__ = init
-    shard.DeviceGroup.all_reduce_sum = reduce
-    Engine._reexpress = reexpress
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    import pooled_stages as PS
 
     reps = []
     for r in range(a.reps):
-        rec.clear()
         t0 = time.time()
-        mcmc = MCMC(NUTS(P.funnel, dense_mass="pooled", max_tree_depth=6), num_warmup=30, num_samples=4,
-                    num_chains=a.chains, devices=["cuda:0", "cuda:0"], progress_bar=False)
-        mcmc.run(5, a.dim, extra_fields=("num_steps",))
+        with PS.recording(unlocked=a.unlocked) as rec:
+            mcmc = MCMC(NUTS(P.funnel, dense_mass="pooled", max_tree_depth=6), num_warmup=30, num_samples=4,
+                        num_chains=a.chains, devices=["cuda:0", "cuda:0"], progress_bar=False)
+            mcmc.run(5, a.dim, extra_fields=("num_steps",))
         x = mcmc.get_samples(True)["x"]
         ns = mcmc.get_extra_fields(True)["num_steps"]
-        reps.append({"records": list(rec), "x": h(x), "ns": h(ns), "x_t": x.cpu(), "s": time.time() - t0})
+        reps.append({"records": list(rec), "x": PS.h(x), "ns": PS.h(ns), "x_t": x.cpu(), "s": time.time() - t0})
         print(f"rep {r}: {reps[-1]['s']:.1f} s, draws {reps[-1]['x']}", flush=True)
 
     def stages(rp, rank):

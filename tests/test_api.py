@@ -26,7 +26,9 @@ def test_kernel_argument_validation():
     with pytest.raises(NotImplementedError):
         NUTS(lambda: None).potential()  # no sample sites: no fused kernel for this structure
     with pytest.raises(TypeError):
-        NUTS(potential_fn=lambda z: z)
+        NUTS(potential_fn=3.0)
+    with pytest.raises(ValueError, match="init_params"):  # hmc.py:754-757
+        NUTS(potential_fn=lambda z: (z ** 2).sum()).potential()
     with pytest.raises(ValueError):
         NUTS(P.eight_schools, dense_mass=[("mu", 3)])  # groups of site names (hmc.py:239-252)
     with pytest.raises(NotImplementedError):
@@ -298,3 +300,45 @@ def test_euclidean_kinetic_grad_keeps_the_momentum_structure():
     # tuple momentum stays a tuple
     gt = kg(torch.tensor([1.0, 2.0, 3.0]), (torch.tensor([1.0]), torch.tensor([1.0, 1.0])))
     assert isinstance(gt, tuple) and gt[1].tolist() == [2.0, 3.0]
+
+
+def test_torch_potential_value_and_grad_on_the_host():
+    """potential_fn over a pytree (hmc.py:127-130) as a TorchPotential: the site structure comes
+    from one chain's init_params (sorted names, ravel_pytree order), U and dU/dz of a batch of
+    flat positions from torch.func (vmapped grad_and_value), and a function vmap cannot trace
+    (Python control flow on values) falls back to per-chain autograd with the same results."""
+    import torch
+
+    from numpyro_amd.infer.hmc import _flatten_init
+
+    def fn(z):
+        return 0.5 * (z["b"] ** 2).sum() + (z["a"] - 1.0).pow(2).sum() * 2.0
+
+    ex = {"b": torch.zeros(2, 2), "a": torch.zeros(3)}
+    pot = P.TorchPotential(fn, ex)
+    assert pot.dim == 7 and [n for n, _, _ in pot.sites] == ["a", "b"] and not pot.array_site
+    zc = torch.randn(5, 7)
+    u, g = pot._value_and_grad(zc)
+    a, b = zc[:, :3], zc[:, 3:]
+    torch.testing.assert_close(u, 0.5 * (b ** 2).sum(1) + 2.0 * ((a - 1.0) ** 2).sum(1))
+    torch.testing.assert_close(g, torch.cat([4.0 * (a - 1.0), b], 1))
+    assert pot._vmap_ok is True
+
+    def branchy(z):  # data-dependent control flow: not vmappable
+        return (z ** 2).sum() if float(z[0]) > 0 else (2.0 * z ** 2).sum()
+
+    pb = P.TorchPotential(branchy, torch.zeros(4))
+    assert pb.array_site and pb.dim == 4
+    zc = torch.tensor([[1.0, 2.0, 0.0, 1.0], [-1.0, 1.0, 1.0, 0.0]])
+    u, g = pb._value_and_grad(zc)
+    assert pb._vmap_ok is False
+    torch.testing.assert_close(u, torch.tensor([6.0, 6.0]))
+    torch.testing.assert_close(g, torch.stack([2.0 * zc[0], 4.0 * zc[1]]))
+    # init_params: batched dicts / arrays, and one chain's unbatched values
+    flat = _flatten_init(pot, {"a": torch.ones(4, 3), "b": torch.zeros(4, 2, 2)}, 4)
+    assert flat.shape == (4, 7) and float(flat[:, :3].sum()) == 12.0
+    assert _flatten_init(pot, {"a": torch.ones(3), "b": torch.zeros(2, 2)}, 1).shape == (1, 7)
+    assert _flatten_init(pb, torch.zeros(4), 1).shape == (1, 4)
+    k = NUTS(potential_fn=fn)
+    k.bind_potential_fn({"a": torch.ones(6, 3), "b": torch.zeros(6, 2, 2)}, 6)
+    assert isinstance(k.potential(), P.TorchPotential) and k.potential().dim == 7

@@ -149,9 +149,10 @@ def test_gemm_chains_x3_matches_fp64(device, D, C, tri, split):
 def test_gemm_chains_x3_error_is_a_float32_gemms(device):
     """The split-bf16 product's rounding is that of a float32 GEMM (BLAS sgemm in NumPy) on the
     same float32 operands, both against float64: at D = 5038 (BASELINE config 3's whitening) the
-    median over chains of the largest relative error is within 2.5x sgemm's (1.7x measured; 4x
-    when the five correction products shared the main accumulator, which is what the c3 parity
-    leg's draw drift was made of -- scripts/bnn_accuracy.py)."""
+    median over chains of the largest relative error is within 1.25x sgemm's.  History: 4x when
+    the five correction products shared the main accumulator (round 5's c3 draw drift), 1.7x
+    with one main accumulator over all of K (the MFMA rounds its running sum every few products),
+    ~0.4x modelled with the 256-deep block sums of round 6."""
     D, C, tri = 5038, 128, 1
     rs = np.random.RandomState(11)
     lib = native.lib()
@@ -174,7 +175,7 @@ def test_gemm_chains_x3_error_is_a_float32_gemms(device):
     dev = np.median(np.abs(out.cpu().numpy().astype(np.float64) - y64).max(0) / sc)
     ref = np.median(np.abs((A32 @ x32).astype(np.float64) - y64).max(0) / sc)
     print(f"[x3 accuracy D={D}] device {dev:.3g} vs sgemm {ref:.3g} ({dev / ref:.2f}x)")
-    assert dev <= 2.5 * ref, (dev, ref)
+    assert dev <= 1.25 * ref, (dev, ref)
 
 
 @pytest.mark.parametrize("tri", [0, 1, 2])
@@ -622,7 +623,7 @@ def test_per_chain_dense_needs_pooled_when_too_large(device):
         mcmc.run(0, 10000)
 
 
-@pytest.mark.parametrize("D,C", [(3, 64), (55, 130), (256, 70)])
+@pytest.mark.parametrize("D,C", [(3, 64), (55, 130), (256, 70), (257, 40), (1100, 33)])
 def test_chain_matvec_matches_fp64(device, D, C):
     """nmx_chain_matvec: out[a][c] = sum_b M[c][b][a] in[b][c] for listed chains (others
     untouched) and for the phase-selected dense batch; f32 fma-chain error bound."""
@@ -652,6 +653,103 @@ def test_chain_matvec_matches_fp64(device, D, C):
                                       native.ptr(phase), C, native.stream_ptr()))
     o = out.cpu().numpy().astype(np.float64)
     assert np.all(np.abs(o[:, :C:2] - ref[:, ::2]) <= bound[:, ::2]) and np.all(np.isnan(o[:, 1:C:2]))
+
+
+@pytest.mark.parametrize("D,C", [(300, 37), (1030, 20)])
+def test_chain_matvec_triangular_skips_zero_rows(device, D, C):
+    """nmx_chain_matvec_tri (dim > 256: one workgroup per chain and 256 outputs): with T_c upper
+    triangular the forward product (M = T_c^T) skips rows b < a and the backward (M = T_c) rows
+    b > a -- bitwise the full products (the skipped terms are exact zeros), and within the f32
+    fma-chain bound of float64."""
+    lib = native.lib()
+    rs = np.random.RandomState(D)
+    ldc = (C + 63) // 64 * 64
+    T = np.triu(rs.randn(C, D, D)).astype(np.float32)
+    x = rs.randn(D, ldc).astype(np.float32)
+    dx = torch.from_numpy(x).to(device)
+    for tri, M in ((1, np.ascontiguousarray(T.transpose(0, 2, 1))), (2, T)):
+        dM = torch.from_numpy(M).to(device)
+        outs = []
+        for t in (0, tri):
+            out = torch.full((D, ldc), float("nan"), device=device)
+            native.check(lib.nmx_chain_matvec_tri(native.ptr(dM), D, native.ptr(dx), native.ptr(out), ldc, None, None,
+                                                  None, C, t, native.stream_ptr()))
+            outs.append(out.cpu().numpy())
+        assert np.array_equal(outs[0][:, :C], outs[1][:, :C]), tri
+        ref = np.einsum("cba,bc->ac", M.astype(np.float64), x[:, :C].astype(np.float64))
+        bound = 1e-6 * np.einsum("cba,bc->ac", np.abs(M).astype(np.float64), np.abs(x[:, :C]).astype(np.float64))
+        assert np.all(np.abs(outs[1][:, :C] - ref) <= bound + 1e-6), tri
+
+
+@pytest.mark.parametrize("D,C", [(300, 9), (700, 5)])
+def test_chain_welford_large_dim_matches_oracle(device, D, C):
+    """nmx_chain_welford_ws above dim 256 (the two-launch form): every chain's mean and m2 after
+    a few draws equal the oracle's f32 welford_covariance(diagonal=False) update_fn
+    (hmc_util.py:172-196) to f32 rounding."""
+    rs = np.random.RandomState(D)
+    ldc = 64
+    W = native.lib().nmx_chain_welford_work_bytes(D, C)
+    assert W == C * 2 * D * 4
+    from numpyro_amd.dense import ChainWelford
+    cw = ChainWelford(D, C, device)
+    _, upd, _ = H.welford_covariance(diagonal=False)
+    st = [(np.zeros(D, np.float32), np.zeros((D, D), np.float32), 0) for _ in range(C)]
+    for _ in range(4):
+        z = rs.randn(D, ldc).astype(np.float32)
+        cw.add(torch.from_numpy(z).to(device), stream=native.stream_ptr())
+        st = [upd(z[:, c], st[c]) for c in range(C)]
+    mean, m2 = cw.mean.cpu().numpy(), cw.m2.cpu().numpy()
+    for c in range(C):
+        np.testing.assert_allclose(mean[c], st[c][0], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(m2[c], st[c][1], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("D,C,K", [(512, 256, 24), (1024, 256, 12)])
+def test_per_chain_dense_large_dim_matches_oracle(device, D, C, K):
+    """Per-chain dense mass above dim 256 (the reference's vmapped init_kernel, hmc.py:790-798:
+    every chain adapts its own matrix; no pooled deviation): MVN targets of dim 512 and 1024 with
+    256 chains, W = 150 (one middle window), max_tree_depth 6.  (1) teacher-forced: the oracle's
+    dense Welford + final_fn over each checked chain's device draws of the window reproduces its
+    adapted inverse mass matrix; (2) from the post-warmup state the oracle's dense-mass NUTS takes
+    the device's next three trees, every parting located at a rounding-level decision (the first
+    K chains are traced and checked)."""
+    seed, W = 23, 150
+    cov = _corr_cov(D, 5) / D * 8 + 0.1 * np.eye(D)
+    ref = OP.MVN(np.linalg.inv(cov))
+    mcmc = MCMC(NUTS(P.multivariate_normal, dense_mass=True, max_tree_depth=6), num_warmup=W, num_samples=3,
+                num_chains=C, progress_bar=False)
+    mcmc.warmup(seed, None, cov, collect_warmup=True)
+    eng = mcmc._engine
+    assert eng.chain_dense and not eng.crow and eng.D == D
+    draws = mcmc.get_samples(group_by_chain=True)["x"][:K].cpu().numpy().reshape(K, W, D)
+    st = mcmc.post_warmup_state
+    imm = st.adapt_state.inverse_mass_matrix[:K].cpu().numpy().astype(np.float64)
+    _, upd, fin = H.welford_covariance(diagonal=False)
+    for c in range(K):
+        wst = (np.zeros(D, np.float32), np.zeros((D, D), np.float32), 0)
+        for t in range(75, 100):
+            wst = upd(draws[c, t], wst)
+        np.testing.assert_allclose(imm[c], fin(wst, regularize=True)[0], rtol=1e-4, atol=1e-7, err_msg=f"chain {c}")
+    eng.set_trace(K, W, 3)
+    mcmc.run(seed, None, cov, extra_fields=("num_steps",))
+    tr = eng.trace_records()
+    ns_dev = mcmc.get_extra_fields(True)["num_steps"][:K].cpu().numpy()
+    zs = mcmc.get_samples(True)["x"][:K].cpu().numpy()
+    z0, g0 = st.z["x"][:K].cpu().numpy(), st.z_grad[:K].cpu().numpy()
+    pe0, ss = st.potential_energy[:K].cpu().numpy(), st.adapt_state.step_size[:K].cpu().numpy()
+    hist = []
+    for c in range(K):
+        o = H.NUTSOracle(PC.f32(ref.pe_grad), D, W, step_size=float(ss[c]), adapt_step_size=False,
+                         adapt_mass_matrix=False, dense_mass=True, inverse_mass_matrix=imm[c].astype(np.float32),
+                         max_tree_depth=6)
+        wa = o.wa_init((z0[c],), None, np.float32(ss[c]), inverse_mass_matrix=imm[c].astype(np.float32),
+                       mass_matrix_size=D)
+        s0 = H.HMCState(W, z0[c].astype(np.float32), g0[c].astype(np.float32), np.float32(pe0[c]), None, None, None,
+                        0, np.float32(0), np.float32(0), False, wa, (seed, c))
+        hist.append(PC.traced(o, s0, 3))
+    par = PR.compare_traced(hist, tr, ns_dev, zs, atol=1e-3, rtol=1e-3)
+    print(f"[per-chain dense D={D}] device trees {ns_dev.tolist()}")
+    PC.report(par, f"per-chain dense mvn D={D}", frac=0.9)
 
 
 @pytest.mark.parametrize("model", ["mvn", "logreg"])

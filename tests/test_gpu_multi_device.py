@@ -75,7 +75,15 @@ def pooled_run(devices):
 
 
 def test_parallel_pooled_dense_equals_torchrun(device, tmp_path):
-    x2, n2 = pooled_run(TWO)
+    """The in-process two-device pooled run equals the 2-rank torchrun bitwise.  Both record the
+    window ends' stage hashes (tests/pooled_stages.py: reduced moments, finalized covariance,
+    T, T^-1, re-expressed positions per rank), so a divergence names the first stage where the
+    two paths part (round 5 saw one unexplained rank-1 rounding divergence; 56 later repetitions
+    with every stage hashed found none)."""
+    import pooled_stages as PS
+
+    with PS.recording() as rec:
+        x2, n2 = pooled_run(TWO)
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
@@ -85,8 +93,12 @@ def test_parallel_pooled_dense_equals_torchrun(device, tmp_path):
                     "--master-addr", "127.0.0.1", "--master-port", str(port),
                     os.path.join(ROOT, "tests", "dist_pooled_worker.py"), str(out)], check=True, timeout=600, env=env)
     ref = torch.load(out, weights_only=True)
-    assert torch.equal(ref["ns"], n2.cpu())
-    assert torch.equal(ref["x"], x2.cpu())
+    where = {r: PS.first_difference(PS.by_rank(rec, r), PS.by_rank(ref["stages"], r)) for r in (0, 1)}
+    print(f"[pooled] stages per rank: {len(PS.by_rank(rec, 0))} / {len(PS.by_rank(rec, 1))} records; "
+          f"first difference vs torchrun: {where}")
+    assert torch.equal(ref["ns"], n2.cpu()), where
+    assert torch.equal(ref["x"], x2.cpu()), where
+    assert where == {0: None, 1: None}
     one_x, one_n = pooled_run(None)  # one engine pools in one GEMM: equal to rounding, not bitwise
     print(f"[pooled] one engine vs two: {float((one_x.cpu() - x2.cpu()).abs().max()):.2e} max |dx|, "
           f"{int((one_n.cpu() == n2.cpu()).sum())}/{n2.numel()} equal tree sizes")
