@@ -818,6 +818,16 @@ class Engine:
         del old
 
     # ------------------------------------------------------------------ accessors
+    def model_gradient(self, z):
+        """grad U at model-space unconstrained positions z [D, ldc] (every chain < C): the model's
+        own potential kernel on a dense batch, as during sampling (MCMC's z_grad extra field)."""
+        g = torch.zeros_like(z)
+        pe = torch.zeros(self.ldc, dtype=torch.float32, device=self.device)
+        ev = EvalBatch(z=ptr(z), grad=ptr(g), pe=ptr(pe), phase=None, active_idx=None, active_count=None,
+                       num_chains=self.C, ldc=self.ldc)
+        self.model_potential.evaluate(ev, stream_ptr())
+        return g
+
     def model_state(self):
         """(z [C, D], grad U(z) [C, D]) in model coordinates (un-whitened for dense mass)."""
         z, g = self.chain_state("z"), self.chain_state("zgrad")

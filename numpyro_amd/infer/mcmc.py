@@ -20,6 +20,14 @@ from ..random import key_to_seed
 from .hmc import restore_state, snapshot_state
 
 _FIELD_ALIASES = {"adapt_state.step_size": "step_size", "i": "i"}
+# HMCState fields (hmc.py:31-48) the device does not collect per transition but that follow from
+# what it does: the gradient at each collected draw (the model's potential evaluated again at the
+# unconstrained draws after the run -- the same per-chain kernel, so the sampler's own gradient
+# for real-valued sites), the configured trajectory length, the momentum carried between
+# transitions (None: a fresh momentum is drawn every transition, as in the reference unless a
+# state carries r), and the mass matrices of sampling draws (constant after warmup)
+_DERIVED_FIELDS = ("z_grad", "trajectory_length", "r", "adapt_state.inverse_mass_matrix",
+                   "adapt_state.mass_matrix_sqrt", "adapt_state.mass_matrix_sqrt_inv")
 
 
 from ..shard import shard_chains  # noqa: E402  (re-exported: contiguous chain shard per rank)
@@ -224,18 +232,30 @@ class MCMC:
 
     def _run(self, rng_key, args, kwargs, extra_fields, init_params, n_iter, lower, resume=None):
         assert isinstance(extra_fields, (tuple, list))
-        collect = []
+        collect, derived = [], []
         for f in (self._sample_field,) + tuple(self._default_fields) + tuple(extra_fields):
             f = _FIELD_ALIASES.get(f, f)
             if f == self._sample_field or f in native.COLLECT:
                 if f not in collect:
                     collect.append(f)
+            elif f in _DERIVED_FIELDS:
+                if f.startswith("adapt_state.m") or f.startswith("adapt_state.i"):
+                    if lower < self.num_warmup and n_iter > 0 and resume is None:
+                        raise ValueError(f"extra field {f!r}: collected for sampling draws only (the matrices "
+                                         "change at the adaptation window ends during warmup)")
+                if f not in derived:
+                    derived.append(f)
             elif f.startswith("~"):
                 continue
             else:
                 raise ValueError(f"extra field {f!r} is not collected by the device engine; "
-                                 f"available: {native.COLLECT}")
+                                 f"available: {native.COLLECT + list(_DERIVED_FIELDS)}")
         self._collected = tuple(collect)
+        self._derived = tuple(derived)
+        self._derived_cache = {}
+        # z_grad is evaluated at the unconstrained draws: collect them unconstrained and apply
+        # the support transforms on the host (_site_arrays)
+        self._host_constrain = "z_grad" in derived and self.postprocess_fn is None
         seed = key_to_seed(rng_key)
         bind = getattr(self.sampler, "bind_potential_fn", None)
         if bind is not None and resume is None:
@@ -245,7 +265,7 @@ class MCMC:
             return self._run_multi(devs, seed, args, kwargs, init_params, n_iter, lower, resume)
         eng = self._get_engine(args, kwargs)
         self._args, self._kwargs = tuple(args), dict(kwargs)
-        eng.constrain_samples = self.postprocess_fn is None
+        eng.constrain_samples = self.postprocess_fn is None and not self._host_constrain
         dev = eng.device
         with torch.cuda.device(dev):
             if resume is not None:
@@ -309,7 +329,7 @@ class MCMC:
         def work(g):
             eng = engines[g]
             try:
-                eng.constrain_samples = self.postprocess_fn is None
+                eng.constrain_samples = self.postprocess_fn is None and not self._host_constrain
                 with torch.cuda.device(eng.device):
                     if parts is not None:
                         self._restore(eng, parts[g])
@@ -362,6 +382,12 @@ class MCMC:
         C = self.local_chains
         S = self._samples.shape[0]
         flat = self._samples[:, :, :C].permute(2, 0, 1)  # [C, S, D]
+        if getattr(self, "_host_constrain", False):
+            from ..potentials import POSITIVE
+
+            codes = pot.transform_codes().to(flat.device)
+            if bool((codes == POSITIVE).any()):
+                flat = torch.where(codes == POSITIVE, torch.exp(flat), flat)
         out = pot.unflatten(flat)
         if self.postprocess_fn is not None:
             # draws are unconstrained here (Engine.constrain_samples = False)
@@ -394,7 +420,55 @@ class MCMC:
             if not group_by_chain:
                 v = v.reshape(-1)
             out["adapt_state.step_size" if f == "step_size" else f] = v
+        for f in getattr(self, "_derived", ()):
+            out[f] = self._derived_field(f, group_by_chain)
         return out
+
+    def _derived_field(self, f, group_by_chain):
+        """The _DERIVED_FIELDS values, [C, S, ...] (or flattened over chains and draws)."""
+        C, S = self.local_chains, self._samples.shape[0]
+        eng = self._engine
+        if f == "r":
+            return None
+        if f == "trajectory_length":
+            tl = self.sampler.options().trajectory_length if self.sampler.options().algo == native.ALGO_HMC else None
+            if tl is None:
+                return None
+            v = torch.full((C, S), float(tl), dtype=torch.float32, device=self._samples.device)
+            return v if group_by_chain else v.reshape(-1)
+        if f == "z_grad":
+            if "z_grad" not in self._derived_cache:
+                if self._engines is not None:
+                    raise NotImplementedError("extra field 'z_grad' with chains over several devices")
+                g = torch.empty_like(self._samples)  # [S, D, ldc]
+                for k in range(S):
+                    g[k] = eng.model_gradient(self._samples[k].contiguous())
+                self._derived_cache["z_grad"] = g
+            pot = self._model_potential()
+            gv = self._derived_cache["z_grad"][:, :, :C].permute(2, 0, 1)  # [C, S, D]
+            out = pot.unflatten(gv)
+            if getattr(pot, "array_site", False):
+                out = out["z"]
+                return out if group_by_chain else out.reshape(C * S, *out.shape[2:])
+            return out if group_by_chain else {k: v.reshape(C * S, *v.shape[2:]) for k, v in out.items()}
+        # adapt_state mass matrices: the post-warmup matrices of every sampling draw
+        imm, msq, msq_inv = (self._last_state.adapt_state.inverse_mass_matrix,
+                             self._last_state.adapt_state.mass_matrix_sqrt,
+                             self._last_state.adapt_state.mass_matrix_sqrt_inv)
+        m = {"adapt_state.inverse_mass_matrix": imm, "adapt_state.mass_matrix_sqrt": msq,
+             "adapt_state.mass_matrix_sqrt_inv": msq_inv}[f]
+
+        # one matrix shared by every chain (pooled, or a given dense matrix that is not adapted)
+        # or one per chain (diagonal [C, D], per-chain dense [C, D, D])
+        shared = eng is not None and eng.dense and not eng.chain_dense
+
+        def per_draw(v):
+            v = torch.as_tensor(v)
+            v = v[None].expand(C, *v.shape) if shared else v
+            v = v[:, None].expand(C, S, *v.shape[1:])
+            return v if group_by_chain else v.reshape(C * S, *v.shape[2:])
+
+        return {k: per_draw(v) for k, v in m.items()} if isinstance(m, dict) else per_draw(m)
 
     def gather_samples(self, group_by_chain=False):
         """get_samples over the chains of every rank (all_gather; identical to get_samples

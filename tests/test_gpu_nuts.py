@@ -826,3 +826,46 @@ def test_covtype_full_size_recovers_ref_params(device):
           f"mean z^2 {np.mean(zerr ** 2):.2f}")
     assert np.all(np.abs(zerr) <= 5.0), np.argsort(-np.abs(zerr))[:5]
     assert np.mean(zerr ** 2) <= 3.0
+
+
+def test_derived_extra_fields(device):
+    """HMCState fields the device does not collect per transition (hmc.py:31-48): z_grad is the
+    model's potential evaluated again at the unconstrained draws -- the same per-chain kernel, so
+    the last draw's gradient equals last_state.z_grad bitwise and every draw's matches the float64
+    oracle's gradient to f32 rounding; r is None (fresh momentum every transition), NUTS has no
+    trajectory_length (None), HMC's is its configured value; the sampling draws' inverse mass
+    matrix is the post-warmup one.  Samples are unchanged by asking for z_grad (positive sites
+    constrained on the host instead of the device: to the ulp)."""
+    args = (8, datasets.EIGHT_SCHOOLS_SIGMA, datasets.EIGHT_SCHOOLS_Y)
+    C, W, S = 16, 60, 12
+    plain = MCMC(NUTS(P.eight_schools), num_warmup=W, num_samples=S, num_chains=C, progress_bar=False)
+    plain.run(3, *args)
+    mcmc = MCMC(NUTS(P.eight_schools), num_warmup=W, num_samples=S, num_chains=C, progress_bar=False)
+    mcmc.run(3, *args, extra_fields=("z_grad", "trajectory_length", "r", "adapt_state.inverse_mass_matrix"))
+    ef = mcmc.get_extra_fields(group_by_chain=True)
+    assert ef["r"] is None and ef["trajectory_length"] is None
+    zg = ef["z_grad"]
+    assert set(zg) == {"mu", "tau", "theta"} and zg["theta"].shape == (C, S, 8)
+    pot = mcmc._engine.model_potential
+    flat = torch.cat([zg[n].reshape(C, S, -1) for n, _, _ in pot.sites], dim=2)  # [C, S, D]
+    assert torch.equal(flat[:, -1].cpu(), mcmc.last_state.z_grad.cpu())
+    imm = ef["adapt_state.inverse_mass_matrix"]
+    assert imm.shape == (C, S, 10) and torch.equal(imm[:, 0].cpu(), mcmc.last_state.adapt_state.inverse_mass_matrix.cpu())
+    for k, v in plain.get_samples(True).items():
+        torch.testing.assert_close(mcmc.get_samples(True)[k].cpu(), v.cpu(), rtol=1e-6, atol=0)
+    ref = OP.EightSchools(datasets.EIGHT_SCHOOLS_Y, datasets.EIGHT_SCHOOLS_SIGMA)
+    s = mcmc.get_samples(True)
+    for c in range(C):
+        for t in range(S):
+            zu = np.concatenate([[float(s["mu"][c, t])], [np.log(float(s["tau"][c, t]))],
+                                 s["theta"][c, t].cpu().numpy()])
+            g64 = ref.pe_grad(zu.astype(np.float64))[1]
+            np.testing.assert_allclose(flat[c, t].cpu().numpy(), g64, rtol=1e-4, atol=1e-4)
+    h = MCMC(HMC(P.eight_schools, trajectory_length=1.5), num_warmup=20, num_samples=4, num_chains=4,
+             progress_bar=False)
+    h.run(1, *args, extra_fields=("trajectory_length",))
+    tl = h.get_extra_fields()["trajectory_length"]
+    assert tl.shape == (16,) and torch.all(tl == 1.5)
+    with pytest.raises(ValueError):
+        MCMC(NUTS(P.eight_schools), num_warmup=10, num_samples=2, num_chains=4, progress_bar=False).warmup(
+            0, *args, collect_warmup=True, extra_fields=("adapt_state.inverse_mass_matrix",))
