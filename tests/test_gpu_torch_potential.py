@@ -48,22 +48,23 @@ def test_torch_potential_matches_the_fused_diag_normal(device):
 
 
 def test_torch_potential_banana_moments(device):
-    """x1 ~ N(0, 1), x2 | x1 ~ N(x1^2, 0.5): no fused kernel has this structure.  E[x1] = 0,
-    E[x2] = 1, Var[x2] = Var[x1^2] + 0.25 = 2.25 (256 chains x 300 draws)."""
+    """x1 ~ N(0, 1), x2 | x1 ~ N(x1^2 / 2, 1): no fused kernel has this structure.  E[x1] = 0,
+    E[x2] = 1/2, Var[x1] = 1, Var[x2] = Var[x1^2] / 4 + 1 = 1.5 (256 chains x 500 draws; the
+    tolerances are several standard errors of these estimates at that sample size)."""
     def banana(z):
         x1, x2 = z[0], z[1]
-        return 0.5 * x1 ** 2 + 0.5 * ((x2 - x1 ** 2) / 0.5) ** 2
+        return 0.5 * x1 ** 2 + 0.5 * (x2 - 0.5 * x1 ** 2) ** 2
 
-    C = 256
-    mcmc = MCMC(NUTS(potential_fn=banana), num_warmup=300, num_samples=300, num_chains=C, progress_bar=False)
+    C, S = 256, 500
+    mcmc = MCMC(NUTS(potential_fn=banana), num_warmup=500, num_samples=S, num_chains=C, progress_bar=False)
     mcmc.run(11, init_params=torch.zeros(C, 2))
     x = mcmc.get_samples()
-    assert torch.is_tensor(x) and x.shape == (C * 300, 2)  # an array z comes back as an array
+    assert torch.is_tensor(x) and x.shape == (C * S, 2)  # an array z comes back as an array
     m = x.double().mean(0).cpu().numpy()
     v = x.double().var(0).cpu().numpy()
     print(f"[banana] mean {m}, var {v}")
-    assert abs(m[0]) < 0.05 and abs(m[1] - 1.0) < 0.08
-    assert abs(v[0] - 1.0) < 0.1 and abs(v[1] - 2.25) < 0.3
+    assert abs(m[0]) < 0.05 and abs(m[1] - 0.5) < 0.06
+    assert abs(v[0] - 1.0) < 0.1 and abs(v[1] - 1.5) < 0.2
 
 
 def test_torch_potential_needs_init_params_and_runs_dense(device):
@@ -78,5 +79,5 @@ def test_torch_potential_needs_init_params_and_runs_dense(device):
     err = (x.mean(0).cpu() - MU.double()).abs() / SD.double()
     print(f"[torch potential dense] standardized mean error {err.numpy()}")
     assert float(err.max()) < 0.15
-    imm = mcmc.post_warmup_state.adapt_state.inverse_mass_matrix
+    imm = mcmc.last_state.adapt_state.inverse_mass_matrix
     assert imm.shape == (C, 5, 5)
