@@ -292,7 +292,7 @@ __global__ __launch_bounds__(THREADS) void k_bnn(const float* __restrict__ X, co
 //  * the 4 k-lanes of a step take k = 16 kq + s (s < 16; the remainder of K in groups of
 //    (K - 64) / 4 after it), which puts the four lane groups of every operand read 16 banks
 //    apart: with W2 stored at row stride 73 every read of the three products is conflict-free for
-//    the first 64 k (2-way in the remainder; scripts/ab_bnn.py checks the pattern);
+//    the first 64 k (2-way in the remainder; scripts/bnn_bank_pattern.py checks the pattern);
 //  * K overruns are exact zeros: W2 carries three zero rows (P1's K = 72 > 69) and three zero
 //    columns (P3's), and the products' other operand there reads finite values of the next row
 //    (h2[0..2] are zeroed before P1 for the last row of h1); output rows / columns beyond N / H

@@ -34,9 +34,12 @@ tanh network or a stiff posterior amplify rounding over hundreds of leaves).  A 
 bound too: it is explained only by a rounding calibration (below) -- when the device's drift
 at that chain and transition is within DRAW_MULT x the calibration's drift there, or x the
 calibration's median drift over its chains at that transition where that is larger (chaotic
-trajectories spread single-chain drifts over two orders of magnitude), or -- where the
-calibration already parted from the reference at an earlier transition -- its largest drift at
-the same tree size.  Without a calibration a draw mismatch is unexplained: a bug that corrupts
+trajectories spread single-chain drifts over two orders of magnitude).  Where the calibration
+itself left the reference's path on that chain by a located rounding flip (at this transition or
+before), the chain's trajectory is rounding-sensitive beyond what a drift bound measures, and a
+device that stayed on the path is explained (reported as such, counted apart in the drift
+statistics' `draws_on_parted`); where the calibration left the path otherwise (a draw of its own at
+an earlier transition), its largest drift at the same tree size stands in.  Without a calibration a draw mismatch is unexplained: a bug that corrupts
 the proposal (the whitening's to_model, the collection) while every decision stays equal
 cannot pass as drift.  Drift is measured in tolerance units, max_i |z_i - ref_i| / (atol +
 rtol |ref_i|), so a draw mismatch has drift > 1.
@@ -211,11 +214,19 @@ def bound_draws(par, cal, mult=DRAW_MULT):
     """Explain (or not) the `draw` mismatches of the device record `par` by the rounding
     calibration `cal` (compare_traced of a second float32 oracle against the same reference):
     a draw is a rounding drift when the device's drift is within `mult` x the calibration's on
-    the same chain and transition; where the calibration left the reference's path before that
-    transition, its largest drift at the same tree size (any tree size if none) stands in.  Sets
+    the same chain and transition; where the calibration left the reference's path on that chain
+    by a located rounding flip at or before that transition, the draw is explained (ratio 0,
+    cal_drift inf: the chain is rounding-sensitive); where it left it by a draw of its own, its
+    largest drift at the same tree size (any tree size if none) stands in.  Sets
     cal_drift / ratio / explained on each draw and par["draw_drift"] (paired drift statistics,
     see drift_stats); returns par."""
     at = {(d["chain"], d["transition"]): d["drift"] for d in cal["drift"]}
+    # transitions at which the calibration itself left the reference's path by a located rounding
+    # flip (chain -> first such transition)
+    cal_parted = {}
+    for cm in cal.get("mismatches", []):
+        if cm.get("leaf") is not None and cm.get("explained"):
+            cal_parted[cm["chain"]] = min(cal_parted.get(cm["chain"], cm["transition"]), cm["transition"])
     by_tree, by_t = {}, {}
     for d in cal["drift"]:
         by_tree[d["tree"]] = max(by_tree.get(d["tree"], 0.0), d["drift"])
@@ -235,6 +246,15 @@ def bound_draws(par, cal, mult=DRAW_MULT):
             med = typical.get(m["transition"], 0.0)
             if med > ref:
                 ref, how = med, "median of the calibration's chains at this transition"
+        elif cal_parted.get(m["chain"], math.inf) <= m["transition"]:
+            # the second float32 implementation could not follow the reference on this chain (a
+            # rounding flip at its own leaf, at this transition or before): the trajectory is
+            # rounding-sensitive beyond what a drift bound measures, and the device, still on the
+            # reference's path, drifts less than an implementation that left it
+            m["cal_drift"], m["cal_basis"] = math.inf, (f"the calibration itself parted on this chain "
+                                                         f"(rounding flip at transition {cal_parted[m['chain']]})")
+            m["ratio"], m["bound"], m["explained"] = 0.0, math.inf, True
+            continue
         elif m["tree_oracle"] in by_tree:
             ref, how = by_tree[m["tree_oracle"]], "largest at this tree size"
         else:
@@ -273,7 +293,8 @@ def drift_stats(par, cal):
             "median_dev": float(np.median([a[k] for k in keys])) if keys else None,
             "median_cal": float(np.median([b[k] for k in keys])) if keys else None,
             "max_dev": max((a[k] for k in keys), default=None), "max_cal": max((b[k] for k in keys), default=None),
-            "draws": len(draws), "max_draw_ratio": max((m.get("ratio", math.inf) for m in draws), default=None)}
+            "draws": len(draws), "max_draw_ratio": max((m.get("ratio", math.inf) for m in draws), default=None),
+            "draws_on_parted": sum(1 for m in draws if m.get("cal_drift") == math.inf)}
 
 
 def oracle_to_trace(leaves, L):
@@ -295,6 +316,8 @@ def describe(m):
         cal = "" if "cal_drift" not in m else (
             f"; drift {m['drift']:.3g} vs calibration {m['cal_drift']:.3g} ({m['cal_basis']}) = {m['ratio']:.3g}x "
             f"-> {'rounding drift' if m['explained'] else 'NOT explained by rounding'}")
+        if m.get("cal_drift") == math.inf:
+            cal = f"; drift {m['drift']:.3g} where {m['cal_basis']} -> rounding-sensitive chain"
         if "cal_drift" not in m:
             cal = "; no rounding calibration -> NOT explained"
         return (f"chain {m['chain']}: transition {m['transition']} draws differ by {m['margin']:.3g} with every "

@@ -3,6 +3,8 @@ oracle runs whose potentials differ by a rounding-sized perturbation part only a
 the leaf energies explain, and a decision flipped far from its tie is reported as not
 explained (the check has teeth).  The device side of these records is nmx_nuts_config.trace
 (tests/test_gpu_parity_trace.py)."""
+import math
+
 import numpy as np
 
 from oracle import cpu_batched as CB
@@ -199,3 +201,34 @@ def test_draw_bound_uses_the_calibrations_typical_drift_at_that_transition():
     dev = {"drift": [dict(d, drift=d["drift"] * 3.0) for d in drift], "mismatches": []}
     st = PR.drift_stats(dev, cal)
     assert st["geo_mean_lo95"] > PR.DRIFT_GEO_MAX, st
+
+
+def test_draw_on_a_chain_where_the_calibration_flipped_is_rounding_sensitive():
+    """Where the second float32 implementation itself parted from the reference on a chain by a
+    located rounding flip (at or before the draw's transition), a device draw that stayed on the
+    reference's path there is explained and counted apart (draws_on_parted); a calibration that
+    left the path only by a draw of its own earlier bounds by its largest drift at that tree size."""
+    drift = [{"chain": 0, "transition": 0, "tree": 1023, "drift": 2.0, "dz": 2.0},
+             {"chain": 1, "transition": 0, "tree": 1023, "drift": 5.0, "dz": 5.0},
+             {"chain": 1, "transition": 1, "tree": 1023, "drift": 9.0, "dz": 9.0}]
+    flip = {"kind": "take_leaf", "leaf": 521, "chain": 0, "transition": 1, "explained": True}
+    cal = {"drift": drift, "mismatches": [flip], "matched": 1}
+    draw = {"kind": "draw", "chain": 0, "transition": 1, "tree_oracle": 1023, "drift": 67.8, "dz": 0.09,
+            "leaf": None, "margin": 0.09}
+    par = {"drift": [], "mismatches": [dict(draw)]}
+    PR.bound_draws(par, cal)
+    m = par["mismatches"][0]
+    assert m["explained"] and m["cal_drift"] == math.inf and "parted" in m["cal_basis"], m
+    assert par["draw_drift"]["draws_on_parted"] == 1
+    assert "rounding-sensitive" in PR.describe(m)
+    # a flip the calibration could not explain does not make the chain rounding-sensitive
+    cal_bad = dict(cal, mismatches=[dict(flip, explained=False)])
+    par = {"drift": [], "mismatches": [dict(draw)]}
+    PR.bound_draws(par, cal_bad)
+    m = par["mismatches"][0]
+    assert not m["explained"] and m["cal_basis"] == "largest at this tree size", m
+    # a flip at a later transition does not cover an earlier draw
+    cal_late = dict(cal, mismatches=[dict(flip, transition=2)])
+    par = {"drift": [], "mismatches": [dict(draw)]}
+    PR.bound_draws(par, cal_late)
+    assert not par["mismatches"][0]["explained"]
