@@ -152,6 +152,9 @@ def report(par, label, cal=None, frac=None):
         PR.bound_draws(par, cal)
     for m in par["mismatches"]:
         print(f"[{label}] " + PR.describe(m))
+    if cal is not None:
+        for m in cal["mismatches"]:
+            print(f"[{label}] calibration: " + PR.describe(m))
     w = par["worst_dE"]
     print(f"[{label}] {par['matched']}/{par['chains']} chains reproduce the reference over {par['transitions']} "
           f"chain-transitions; leaf-energy discrepancy <= {par['max_dE_err']:.2e} (relative {par['max_dE_rel']:.2e}"
