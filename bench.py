@@ -172,7 +172,7 @@ def _headline_draw_calibration(par, draws, X, y, hist, dev_trace, dev_ns, dev_z,
     del r64
     sub32 = [hist[c][:T] for c in chains]
     ctr, cns, cz = _oracle_trace(sub32, dev_trace.shape[2])
-    cal = PR.compare_traced(h64, ctr, cns, cz, atol=1e-4)
+    cal = PR.compare_traced(h64, ctr, cns, cz, atol=1e-4, through_draws=True)
     dev = PR.compare_traced(h64, dev_trace[:T, chains], dev_ns[chains, :T], dev_z[chains, :T], atol=1e-4)
     PR.bound_draws(dev, cal)
     for m in par["mismatches"]:
@@ -326,7 +326,7 @@ def cpu_baseline_config(sp, eng, seed, dev_ns, dev_z, seconds, dev_trace):
     ctr, cns, cz = _oracle_trace(hist32, L)
     if to_model is not None:
         cz = np.stack([[to_model(w) for w in cc] for cc in cz])
-    cal = PR.compare_traced(hist64, ctr, cns, cz, atol=1e-3, rtol=1e-3, to_model=to_model)
+    cal = PR.compare_traced(hist64, ctr, cns, cz, atol=1e-3, rtol=1e-3, to_model=to_model, through_draws=True)
     PR.bound_draws(cal, cal)
     # the C restatement over the same transitions (float32 potentials in C, double reductions in the
     # sampler): a third implementation, reported beside the calibration

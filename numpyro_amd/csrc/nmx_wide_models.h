@@ -21,17 +21,42 @@
 
 #include "nmx_common.h"
 
-// digamma for x > 0: recurrence up to x >= 6, then the asymptotic series.
-__device__ __forceinline__ double nmx_digamma(double x) {  // x > 0: recurrence to x >= 6, asymptotic series
-  double acc = 0.0;
-  while (x < 6.0) {
-    acc -= 1.0 / x;
-    x += 1.0;
+// The StudentT normaliser's two differences at x = nu / 2 > 0, in double:
+//   L = lgamma(x) - lgamma(x + 1/2),  Psi = digamma(x) - digamma(x + 1/2).
+// The recurrence lgamma(x) = lgamma(x + 1) - log x (digamma: - 1/x) shifts x to X >= 8, keeping
+// the shifts as one product ratio prod (x+k) / (x+k+1/2) and one fraction sum 1/2 / ((x+k)(x+k+1/2))
+// (one log and one division for all of them); at X the Stirling series of both functions are
+// differenced analytically: log(X + 1/2) = log X + log1p(1/(2X)), log1p by its atanh series (t <=
+// 1/33: six terms).  Absolute error <= 2e-13 over x in [0.02, 60] against scipy's gammaln /
+// digamma (tests/test_sv_fin_series.py restates the series) -- what the float64 lgamma / digamma pair gave, at one log
+// instead of two lgammas, two digamma recurrences and their divisions: the SV leaf's serial
+// section (wave 0) was 31% of the persistent kernel's leaf (profiles/r06/sv_phase_stamps.txt).
+__device__ __forceinline__ void nmx_lgamma_digamma_half_diff(double x, double& L, double& Psi) {
+  double X = x, pn = 1.0, pd = 1.0, num = 0.0, den = 1.0;
+  while (X < 8.0) {
+    const double h = X + 0.5, q = X * h;
+    pn *= X;
+    pd *= h;
+    num = num * q + 0.5 * den;
+    den *= q;
+    X += 1.0;
   }
-  const double inv = 1.0 / x, inv2 = inv * inv;
-  const double series =
-      inv2 * (1.0 / 12.0 - inv2 * (1.0 / 120.0 - inv2 * (1.0 / 252.0 - inv2 * (1.0 / 240.0 - inv2 / 132.0))));
-  return acc + log(x) - 0.5 * inv - series;
+  const double inv = 1.0 / X, H = X + 0.5, invh = 1.0 / H;
+  const double u = 0.5 * inv, t = u / (2.0 + u), t2 = t * t;
+  const double l1p =
+      2.0 * t * (1.0 + t2 * (1.0 / 3 + t2 * (1.0 / 5 + t2 * (1.0 / 7 + t2 * (1.0 / 9 + t2 * (1.0 / 11))))));
+  // lgamma's Stirling tail 1/(12z) - 1/(360z^3) + ... and digamma's -1/(12z^2) + 1/(120z^4) - ...
+  auto lser = [](double iz) {
+    const double iz2 = iz * iz;
+    return iz * (1.0 / 12 - iz2 * (1.0 / 360 - iz2 * (1.0 / 1260 - iz2 * (1.0 / 1680 - iz2 / 1188))));
+  };
+  auto pser = [](double iz) {
+    const double iz2 = iz * iz;
+    return iz2 * (1.0 / 12 - iz2 * (1.0 / 120 - iz2 * (1.0 / 252 - iz2 * (1.0 / 240 - iz2 / 132))));
+  };
+  const double r = pn / pd;
+  L = -0.5 * log(X * r * r) - X * l1p + 0.5 + lser(inv) - lser(invh);
+  Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num / den;
 }
 
 // Stochastic volatility (examples/stochastic_volatility.py:57-65), z = (a = log nu, s[T],
@@ -123,19 +148,19 @@ struct NmxWideSV {
   // dU/da is a small difference of O(T) terms.  In float32 their rounding moved dU/da by ~1e-4
   // relative and the draws 5-40x further from the float64 reference than a float32 NumPy
   // implementation's (round-5 parity calibration, tests/test_gpu_nuts.py fixed-step SV); in double
-  // the scalar section costs a few dozen FP64 instructions per chain-leaf (wave 0 only).
+  // the scalar section costs a few hundred FP64 instructions per chain-leaf (wave 0 only).
   __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
     const double a = g.a, b = g.b, nu = exp(a), Tf = (double)T;
     const double sig = exp(b), inv_sig2 = exp(-2.0 * b);
     const double s0 = sums[0], s1 = sums[1], s2 = sums[2], s3 = sums[3];
-    const double lg = lgamma(0.5 * nu) - lgamma(0.5 * (nu + 1.0));
+    double lg, dig;
+    nmx_lgamma_digamma_half_diff(0.5 * nu, lg, dig);
     // log p
     double lp = 3.912023005428146 - 50.0 * sig + b;                 // Exponential(50) + log|J|
     lp += -0.5 * s0 * inv_sig2 - Tf * b - Tf * 0.9189385332046727;  // GaussianRandomWalk
     lp += -2.302585092994046 - 0.1 * nu + a;                        // Exponential(0.1) + log|J|
     lp += -0.5 * (nu + 1.0) * s1 - s3 - Tf * (0.5 * a + 0.5723649429247001 + lg);  // StudentT(nu, 0, e^s)
-    const double dig = nmx_digamma(0.5 * nu) - nmx_digamma(0.5 * (nu + 1.0));
-    const double ga = nu * (-0.1 - 0.5 * s1 + 0.5 * (nu + 1.0) / nu * s2 - 0.5 * Tf / nu - 0.5 * Tf * dig) + 1.0;
+    const double ga = nu * (-0.1 - 0.5 * s1 - 0.5 * Tf * dig) + 0.5 * (nu + 1.0) * s2 - 0.5 * Tf + 1.0;
     const double gb = -50.0 * sig + 1.0 + s0 * inv_sig2 - Tf;
     gs[0] = (float)-ga;
     gs[1] = (float)-gb;

@@ -49,7 +49,9 @@ algorithm apart is measured, not assumed: `compare_traced` run between the refer
 (potential in rounded float64, the most accurate float32 NUTS) and a second oracle whose
 potential is a float32 implementation (oracle/batched.py's NumPy batch, or float32 sums) gives
 the spread rounding alone produces -- matched chains, located partings, the drift of every
-transition whose decisions agree, the relative leaf-energy discrepancy.  The device is compared
+transition whose decisions agree (followed through the calibration's own draw mismatches,
+compare_traced(through_draws=True): a draw leaves a chain on the reference's path), the relative
+leaf-energy discrepancy.  The device is compared
 with the same reference; `bound_draws` explains (or not) its draw mismatches by the
 calibration's drift, and `like_calibration` requires its whole record to be of the
 calibration's order: drift distributions compared pairwise on the (chain, transition) pairs both
@@ -150,7 +152,8 @@ def _drift(z, ref, atol, rtol):
     return float(np.max(d / den)) if np.all(den > 0) else float(np.max(d))
 
 
-def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, max_delta_energy=1000.0):
+def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_model=None, max_delta_energy=1000.0,
+                   through_draws=False):
     """Per-chain parity of oracle histories (oracle.cpu_batched.run_chains(record=True): entries
     (state, decisions, leaves)) with the device's transitions from the same state, each
     mismatch located at its parting leaf.  dev_trace [T, chains, L, 8] is the engine's decision
@@ -162,8 +165,16 @@ def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_mod
     chain's `draw` mismatch): {chain, transition, tree, drift (tolerance units), dz}.
     `worst_dE` locates the largest leaf-energy discrepancy on the common leaves (chain,
     transition, leaf, the two delta energies, the leaf's potential energy and the discrepancy
-    relative to |U_leaf| + |dE|, the magnitude the energies' rounding scales with)."""
-    matched, transitions, max_dz, max_de, mism, drift = 0, 0, 0.0, 0.0, [], []
+    relative to |U_leaf| + |dE|, the magnitude the energies' rounding scales with).
+
+    through_draws (for a rounding calibration): a chain's comparison goes on past its first
+    `draw` mismatch (same tree, every decision equal: still on the reference's path), recording
+    the drift of each later transition whose decisions agree, up to a located parting (not recorded
+    again: one mismatch per chain either way; such partings are listed in `partings_after_draw`).
+    A device draw at a later transition on that chain then has the calibration's own drift there as
+    its bound, or -- where the calibration flipped there -- the chain counts as rounding-sensitive
+    (bound_draws)."""
+    matched, transitions, max_dz, max_de, mism, drift, later = 0, 0, 0.0, 0.0, [], [], []
     worst, max_rel = None, 0.0
     for c, h in enumerate(hist):
         T = min(len(h), dev_num_steps.shape[1], dev_trace.shape[0])
@@ -191,13 +202,23 @@ def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_mod
                 max_rel = max(max_rel, rel)
             if st.num_steps != int(dev_num_steps[c, t]) or dz > atol:
                 loc = locate(dev, leaves, max_delta_energy)
+                same_tree = st.num_steps == int(dev_num_steps[c, t])
                 if loc is None:
                     loc = {"leaf": None, "kind": "draw", "dev": None, "oracle": None, "u": None, "margin": dz,
                            "bound": atol, "dE_err": max(de) if de else 0.0, "explained": False, "drift": dr}
                     drift.append({"chain": c, "transition": t, "tree": int(st.num_steps), "drift": dr, "dz": dz})
+                elif not ok:
+                    # through_draws: a located parting after the chain's draw ends its record (kept
+                    # apart: bound_draws reads it as the calibration leaving the path there)
+                    later.append({"chain": c, "transition": t, "kind": loc["kind"], "leaf": loc["leaf"],
+                                  "explained": loc["explained"]})
+                    break
                 loc.update(chain=c, transition=t, tree_dev=int(dev_num_steps[c, t]), tree_oracle=int(st.num_steps))
-                mism.append(loc)
+                if ok:
+                    mism.append(loc)
                 ok = False
+                if through_draws and loc["kind"] == "draw" and same_tree:
+                    continue
                 break
             drift.append({"chain": c, "transition": t, "tree": int(st.num_steps), "drift": dr, "dz": dz})
             max_dz = max(max_dz, dz)
@@ -207,7 +228,7 @@ def compare_traced(hist, dev_trace, dev_num_steps, dev_z, atol, rtol=0.0, to_mod
             matched += 1
     return {"chains": len(hist), "transitions": transitions, "matched": matched, "max_abs_dz": max_dz,
             "max_dE_err": max_de, "max_dE_rel": max_rel, "worst_dE": worst, "drift": drift,
-            "mismatches": mism, "explained": sum(1 for m in mism if m["explained"])}
+            "mismatches": mism, "explained": sum(1 for m in mism if m["explained"]), "partings_after_draw": later}
 
 
 def bound_draws(par, cal, mult=DRAW_MULT):
@@ -224,7 +245,7 @@ def bound_draws(par, cal, mult=DRAW_MULT):
     # transitions at which the calibration itself left the reference's path by a located rounding
     # flip (chain -> first such transition)
     cal_parted = {}
-    for cm in cal.get("mismatches", []):
+    for cm in cal.get("mismatches", []) + cal.get("partings_after_draw", []):
         if cm.get("leaf") is not None and cm.get("explained"):
             cal_parted[cm["chain"]] = min(cal_parted.get(cm["chain"], cm["transition"]), cm["transition"])
     by_tree, by_t = {}, {}

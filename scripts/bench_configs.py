@@ -1,6 +1,7 @@
 """Throughput of the BASELINE.json secondary configs (one GPU), plus kernel microbenchmarks.
 
     python scripts/bench_configs.py gemm  [D] [C]          # nmx_gemm_chains alone
+    python scripts/bench_configs.py chainmv [D] [--chains C]  # per-chain dense matvec (HBM)
     python scripts/bench_configs.py funnel [--dim 10000 --chains 4096 --warmup W --steps K]
     python scripts/bench_configs.py sv     [--chains 1024 ...]
     python scripts/bench_configs.py bnn    [--chains 2048 ...]
@@ -70,6 +71,40 @@ def bench_gemm(D, C, reps=10, tri=0, x3=False):
     print(json.dumps({"kernel": "k_gemm_x3" if x3 else "k_gemm_chains", "triangle": tri, "D": D, "C": C, "ms": round(ms, 4),
                       "useful_tflops": round(tf, 2), "frac": round(tf / PEAK_F32_TFLOPS, 3), "max_rel_err": err}),
           flush=True)
+
+
+def bench_chain_matvec(D, C, reps=10):
+    """nmx_chain_matvec_tri (per-chain dense mass, every chain listed): HBM-bound, each chain's
+    triangle of T_c (2 D^2 B f32 of the D^2 stored) read once per product, plus the in / out
+    vectors; reported against 8 TB/s on that algorithmic basis."""
+    dev = torch.device("cuda:0")
+    lib = native.lib()
+    ldc = (C + 63) // 64 * 64
+    M = torch.triu(torch.randn(C, D, D, device=dev)).transpose(1, 2).contiguous()  # T_c^T, T_c upper
+    x = torch.randn(D, ldc, device=dev)
+    y = torch.empty(D, ldc, device=dev)
+    s = native.stream_ptr()
+    out = {}
+    for tri in (0, 1):
+        def run():
+            native.check(lib.nmx_chain_matvec_tri(native.ptr(M), D, native.ptr(x), native.ptr(y), ldc, None, None,
+                                                  None, C, tri, s))
+        for _ in range(2):
+            run()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            run()
+        b.record()
+        b.synchronize()
+        ms = a.elapsed_time(b) / reps
+        mbytes = (4.0 * D * D if tri == 0 else 2.0 * D * (D + 1)) * C + 8.0 * D * C
+        ref = torch.einsum("cba,bc->ac", M[:4].double(), x[:, :4].double())
+        err = float((y[:, :4].double() - ref).abs().max() / ref.abs().max())
+        out["full" if tri == 0 else "triangular"] = {"ms": round(ms, 4), "GBs": round(mbytes / (ms * 1e-3) / 1e9, 1),
+                                                     "frac": round(mbytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 3),
+                                                     "max_rel_err": err}
+    print(json.dumps({"kernel": "nmx_chain_matvec_tri", "D": D, "C": C, **out}), flush=True)
 
 
 class Timed:
@@ -188,6 +223,9 @@ def main():
             bench_gemm(D, C, x3=x3)
             bench_gemm(D, C, tri=1, x3=x3)
             bench_gemm(D, C, tri=2, x3=x3)
+    elif a.what == "chainmv":
+        for D in ([int(a.rest[0])] if a.rest else [512, 1024, 2048, 4096]):
+            bench_chain_matvec(D, a.chains or (256 if D <= 1024 else 64))
     elif a.what == "funnel":
         D = a.dim
         # dense: two triangular products z = T w, g = T^T g_z (D^2 FLOP each per chain)

@@ -155,6 +155,9 @@ def report(par, label, cal=None, frac=None):
     if cal is not None:
         for m in cal["mismatches"]:
             print(f"[{label}] calibration: " + PR.describe(m))
+        for m in cal.get("partings_after_draw", []):
+            print(f"[{label}] calibration: chain {m['chain']}: after its draw, parts at transition {m['transition']} "
+                  f"leaf {m['leaf']} on {m['kind']} ({'rounding flip' if m['explained'] else 'NOT explained'})")
     w = par["worst_dE"]
     print(f"[{label}] {par['matched']}/{par['chains']} chains reproduce the reference over {par['transitions']} "
           f"chain-transitions; leaf-energy discrepancy <= {par['max_dE_err']:.2e} (relative {par['max_dE_rel']:.2e}"

@@ -121,7 +121,7 @@ def test_engine_matches_oracle_fixed_step(device, algo, model, dim):
     par = PR.compare_traced(hist, tr, ns, z, to_model=constrain, **tol)
     ctr, cns, cz = PC.as_trace(PC.oracle_runs(PC.second_f32(model, dim, ref), dim, C, T, seed, step, z0, **kw))
     cal = PR.compare_traced(hist, ctr, cns, np.stack([[constrain(w) for w in cc] for cc in cz]), to_model=constrain,
-                            **tol)
+                            through_draws=True, **tol)
     PC.report(par, f"fixed-step {algo} {model} D={dim}", cal=cal, frac=frac)
     # the trace's layout: a NUTS transition records every leaf of its tree, the last one ends it;
     # an HMC transition records its Metropolis decision as leaf 0
@@ -172,7 +172,7 @@ def test_covtype_full_size_nuts_matches_oracle(device):
     _, hist32, _, _ = CB.run_chains(CB.LogRegBatch(X, y), *resume(), T, record=True)
     par = PR.compare_traced(hist, tr, ns, z, atol=1e-4)
     ctr, cns, cz = PC.as_trace(hist32)
-    cal = PR.compare_traced(hist, ctr, cns, cz, atol=1e-4)
+    cal = PR.compare_traced(hist, ctr, cns, cz, atol=1e-4, through_draws=True)
     print(f"[covtype 581012x55] {evals} oracle leapfrogs per side")
     PC.report(par, "covtype full size", cal=cal)
     assert par["matched"] >= C - 1

@@ -55,7 +55,7 @@ def test_dense_chain_step_matches_oracle_dense_mass(device):
     hist = _oracle_runs(_f32(ref.pe_grad), D, C, T, seed, step, None, **kw)
     par = PR.compare_traced(hist, tr, ns, z, atol=2e-3, rtol=2e-3)
     ctr, cns, cz = _as_trace(_oracle_runs(_second_f32("funnel", D, ref), D, C, T, seed, step, None, **kw))
-    cal = PR.compare_traced(hist, ctr, cns, cz, atol=2e-3, rtol=2e-3)
+    cal = PR.compare_traced(hist, ctr, cns, cz, atol=2e-3, rtol=2e-3, through_draws=True)
     _report(par, "dense chain-row step funnel D=600", cal=cal)
 
 
@@ -101,5 +101,5 @@ def test_bnn_pooled_dense_config3_matches_oracle(device):
     par = PR.compare_traced(hist, eng.trace_records(), ns, zdev, atol=1e-3, rtol=1e-3, to_model=to_model)
     ctr, cns, cz = _as_trace(hist32)
     cal = PR.compare_traced(hist, ctr, cns, np.stack([[to_model(w) for w in cc] for cc in cz]), atol=1e-3,
-                            rtol=1e-3, to_model=to_model)
+                            rtol=1e-3, to_model=to_model, through_draws=True)
     _report(par, "bnn pooled dense D=5038", cal=cal)

@@ -232,3 +232,42 @@ def test_draw_on_a_chain_where_the_calibration_flipped_is_rounding_sensitive():
     par = {"drift": [], "mismatches": [dict(draw)]}
     PR.bound_draws(par, cal_late)
     assert not par["mismatches"][0]["explained"]
+
+
+def test_calibration_drift_is_followed_through_its_own_draws():
+    """compare_traced(through_draws=True) keeps recording a chain's drift after its first `draw`
+    mismatch (same decisions, draws apart) while the decisions keep agreeing, with one mismatch per
+    chain as before; so a device draw later on that chain is bounded by the calibration's own drift
+    there."""
+    rs = np.random.RandomState(4)
+    X = rs.randn(500, 5).astype(np.float32)
+    y = (rs.rand(500) < 0.5).astype(np.float32)
+    r32 = OP.LogisticRegression(X, y, dtype=np.float32)
+    r64 = OP.LogisticRegression(X, y, dtype=np.float64)
+    f64 = lambda z: tuple(np.asarray(v, np.float32) for v in r64.pe_grad(z))  # noqa: E731
+    T, n = 3, 8
+    ref = _run(f64, 5, n, 2, T, 0.1)
+    cal_tr, cal_ns, cal_z = _as_device(_run(r32.pe_grad, 5, n, 2, T, 0.1), T)
+    plain = PR.compare_traced(ref, cal_tr, cal_ns, cal_z, atol=1e-7, rtol=0.0)
+    thru = PR.compare_traced(ref, cal_tr, cal_ns, cal_z, atol=1e-7, rtol=0.0, through_draws=True)
+    draws = [m for m in plain["mismatches"] if m["kind"] == "draw" and m["transition"] < T - 1]
+    assert draws, "the tolerance is below float32 drift: every chain has a draw mismatch"
+    assert len(thru["mismatches"]) == len(plain["mismatches"]) and thru["matched"] == plain["matched"]
+    keys = {(d["chain"], d["transition"]) for d in thru["drift"]}
+    for m in draws:
+        assert (m["chain"], m["transition"] + 1) in keys
+    assert len(thru["drift"]) > len(plain["drift"])
+
+
+def test_calibration_flip_after_its_draw_marks_the_chain_rounding_sensitive():
+    """A calibration that drew apart at transition 0 (a draw) and flipped a decision at transition 1
+    lists the flip in partings_after_draw; a device draw at transition 1 on that chain is then
+    explained as a rounding-sensitive chain."""
+    cal = {"drift": [{"chain": 0, "transition": 0, "tree": 1023, "drift": 2.1, "dz": 0.002}],
+           "mismatches": [{"kind": "draw", "leaf": None, "chain": 0, "transition": 0, "explained": False}],
+           "partings_after_draw": [{"chain": 0, "transition": 1, "kind": "take_leaf", "leaf": 17,
+                                    "explained": True}], "matched": 0}
+    par = {"drift": [], "mismatches": [{"kind": "draw", "chain": 0, "transition": 1, "tree_oracle": 1023,
+                                        "drift": 67.8, "dz": 0.09, "leaf": None, "margin": 0.09}]}
+    PR.bound_draws(par, cal)
+    assert par["mismatches"][0]["explained"] and par["draw_drift"]["draws_on_parted"] == 1
