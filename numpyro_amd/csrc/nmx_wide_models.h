@@ -41,7 +41,9 @@ __device__ __forceinline__ void nmx_lgamma_digamma_half_diff(double x, double& L
     den *= q;
     X += 1.0;
   }
-  const double inv = 1.0 / X, H = X + 0.5, invh = 1.0 / H;
+  // 1/X and 1/(X + 1/2) from one division, likewise pn/pd and num/den (double divisions are ~10
+  // dependent instructions each)
+  const double H = X + 0.5, rxh = 1.0 / (X * H), inv = H * rxh, invh = X * rxh;
   const double u = 0.5 * inv, t = u / (2.0 + u), t2 = t * t;
   const double l1p =
       2.0 * t * (1.0 + t2 * (1.0 / 3 + t2 * (1.0 / 5 + t2 * (1.0 / 7 + t2 * (1.0 / 9 + t2 * (1.0 / 11))))));
@@ -54,9 +56,9 @@ __device__ __forceinline__ void nmx_lgamma_digamma_half_diff(double x, double& L
     const double iz2 = iz * iz;
     return iz2 * (1.0 / 12 - iz2 * (1.0 / 120 - iz2 * (1.0 / 252 - iz2 * (1.0 / 240 - iz2 / 132))));
   };
-  const double r = pn / pd;
+  const double rpd = 1.0 / (pd * den), r = pn * den * rpd;
   L = -0.5 * log(X * r * r) - X * l1p + 0.5 + lser(inv) - lser(invh);
-  Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num / den;
+  Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num * pd * rpd;
 }
 
 // Stochastic volatility (examples/stochastic_volatility.py:57-65), z = (a = log nu, s[T],
@@ -151,7 +153,7 @@ struct NmxWideSV {
   // the scalar section costs a few hundred FP64 instructions per chain-leaf (wave 0 only).
   __device__ __forceinline__ float fin(const float* sums, const Glob& g, float* gs) const {
     const double a = g.a, b = g.b, nu = exp(a), Tf = (double)T;
-    const double sig = exp(b), inv_sig2 = exp(-2.0 * b);
+    const double sig = exp(b), inv_sig2 = 1.0 / (sig * sig);
     const double s0 = sums[0], s1 = sums[1], s2 = sums[2], s3 = sums[3];
     double lg, dig;
     nmx_lgamma_digamma_half_diff(0.5 * nu, lg, dig);

@@ -88,6 +88,20 @@ struct Arena {
   float* tot;
 };
 
+// Keeps a base pointer in SGPRs across a loop (the empty asm stops the compiler from hoisting the
+// field addresses derived from it, which overflowed the SGPRs) without losing its global address
+// space: the round trip goes through an address_space(1) value, so accesses through the pointer
+// still compile to global loads / stores with an SGPR base and a VGPR offset.  A plain generic
+// pointer through the asm became opaque and every arena access a flat one -- two VGPRs of
+// address each, and flat loads count against the LDS counter too, so each LDS read waited for
+// the HBM loads in flight (the persistent wide kernel: 76 flat loads and 127 flat stores).
+template <class T>
+__device__ __forceinline__ void pin_sgpr_global(T*& p) {
+  auto* g = (__attribute__((address_space(1))) T*)p;
+  asm volatile("" : "+s"(g));
+  p = (T*)g;
+}
+
 #define AI(f) reinterpret_cast<int32_t*>(a.sbase + (size_t)((f) - NMX_F_PHASE) * a.sstride)
 #define AF(f) reinterpret_cast<float*>(a.sbase + (size_t)((f) - NMX_F_PHASE) * a.sstride)
 #define AV(f) reinterpret_cast<float*>(a.vbase + (size_t)((f) - NMX_F_Z) * a.vstride)
@@ -1845,23 +1859,41 @@ __device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const A
   for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += BC * NT) {
     PRowG xg[BC];
     typename M::RowIn mi[BC];
+    // the batch's loads, grouped by their (wave-uniform) condition, every row of the batch
+    // included: a row past hi reads row hi - 1 (a valid address; the value is never used).  Per-row
+    // guards around the loads split them into small blocks, and the compiler drained the first
+    // row's loads (s_waitcnt vmcnt(0)) before issuing the rest: two memory round trips per batch.
+    uint32_t offq[BC];
 #pragma unroll
     for (int q = 0; q < BC; ++q) {
-      const int d = d0 + q * NT;
-      if (d < hi) {
-        const uint32_t off = base + ((uint32_t)d << 2);
-        if constexpr (NUTS) {
-          xg[q].rs_old = A.k == 0 ? 0.0f : nmx_at(AV(NMX_F_RSUM_SUB), off);
-          if (A.tree_chk) {
-            xg[q].rst = nmx_at(AV(NMX_F_RSUM), off);
-            xg[q].ro = nmx_at((A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR)), off);
-          }
-          if (A.imin <= A.imax) {
-            xg[q].ckr = nmx_at(a.ckr + A.imin * v.ck_stride, off);
-            xg[q].ckrs = nmx_at(a.ckrs + A.imin * v.ck_stride, off);
-          }
+      const int d = min(d0 + q * NT, hi - 1);
+      offq[q] = base + ((uint32_t)d << 2);
+      m.row_load_data(d, mi[q]);
+    }
+    if constexpr (NUTS) {
+      if (A.k != 0) {
+#pragma unroll
+        for (int q = 0; q < BC; ++q) xg[q].rs_old = nmx_at(AV(NMX_F_RSUM_SUB), offq[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < BC; ++q) xg[q].rs_old = 0.0f;
+      }
+      if (A.tree_chk) {
+        const float* RO = A.dirR ? AV(NMX_F_RL) : AV(NMX_F_RR);
+#pragma unroll
+        for (int q = 0; q < BC; ++q) {
+          xg[q].rst = nmx_at(AV(NMX_F_RSUM), offq[q]);
+          xg[q].ro = nmx_at(RO, offq[q]);
         }
-        m.row_load_data(d, mi[q]);
+      }
+      if (A.imin <= A.imax) {
+        const float* CK = a.ckr + A.imin * v.ck_stride;
+        const float* CKS = a.ckrs + A.imin * v.ck_stride;
+#pragma unroll
+        for (int q = 0; q < BC; ++q) {
+          xg[q].ckr = nmx_at(CK, offq[q]);
+          xg[q].ckrs = nmx_at(CKS, offq[q]);
+        }
       }
     }
 #pragma unroll
@@ -2132,6 +2164,20 @@ __device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float s
 // keeps the first three in lds itself (wave 0 writes them after its lanes read every wave sum;
 // the KE sums after the scalar logic, with a barrier before the next leaf's wave sums) and the
 // prefetched inputs in wave 0's registers.
+// The persistent wide kernel's serial section (wave 0: the potential's finish and the NUTS
+// scalar logic, while the chain's other waves wait at a barrier) runs at raised wave priority, so
+// the SIMD's arbiter issues it ahead of the row work of the other chains' waves sharing the SIMD
+// (their phases are throughput-bound; the serial section is the chain's critical path).
+#ifndef NMX_PX_PRIO
+#define NMX_PX_PRIO 1
+#endif
+__device__ __forceinline__ void nmx_serial_prio(bool on) {
+#if NMX_PX_PRIO
+  if (on) __builtin_amdgcn_s_setprio(3);
+  else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 template <int NT, class M, bool CARRY>
 struct PersistShared {
   static constexpr int NW = NT / 64, NR = NPART + M::NSUM;
@@ -2207,7 +2253,11 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     Arena al = Pk.a;
     size_t ck_stride = (size_t)D * ldc;
 #ifndef NMX_DEBUG  // (the debug build's checks leave some of them in VGPRs: no SGPR constraint there)
-    asm volatile("" : "+s"(al.sbase), "+s"(al.vbase), "+s"(al.ckr), "+s"(al.ckrs), "+s"(al.sstride), "+s"(al.vstride));
+    pin_sgpr_global(al.sbase);
+    pin_sgpr_global(al.vbase);
+    pin_sgpr_global(al.ckr);
+    pin_sgpr_global(al.ckrs);
+    asm volatile("" : "+s"(al.sstride), "+s"(al.vstride));
     asm volatile("" : "+s"(ck_stride));
 #endif
     const VecCtx v{&al, ldc, D, ck_stride, cfg.unit_mass != 0};
@@ -2258,6 +2308,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
       if (!CARRY && pl) lds_pre[lane] = pv;
       __syncthreads();
       if (wv == 0) {
+        nmx_serial_prio(true);
         // lane e: entry e's total over the waves (in wave order)
         float tot = 0.0f;
         if (lane < NR && entry_used(A, is_nuts, lane)) {
@@ -2312,6 +2363,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     }
     // scalar logic: wave 0 on the LDS state (lane 0 writes back)
     if (wv == 0) {
+      nmx_serial_prio(true);
       ChainScalars S = Ssh;
       if (A.leaf) A.pe_eval = lds_tot[NR];
       leaf_phase(cfg, S, A, A.leaf ? 0.5f * lds_tot[0] : 0.0f, seed, gch);
@@ -2325,6 +2377,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         sh.wfn = A.wfn;
         if (A.fin_done) atomicAdd(&a.counters[0], 1);
       }
+      nmx_serial_prio(false);
     }
     __syncthreads();  // decisions published
     const int act = uni_i(sh.act);
@@ -2385,7 +2438,8 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
   }
   if (tid == 0) {
     Arena al = Pk.a;  // addresses recomputed here, not kept live from load_scalars through the loop
-    asm volatile("" : "+s"(al.sbase), "+s"(al.sstride));
+    pin_sgpr_global(al.sbase);
+    asm volatile("" : "+s"(al.sstride));
     store_scalars(al, c, Ssh);
   }
 }

@@ -10,7 +10,7 @@ src = open(os.path.join(ROOT, "numpyro_amd", "csrc", "nuts.hip")).read()
 a = src.index("void k_wide_persistent(StepArgs Pk, M m, int max_steps) {")
 b = src.index("// ---- launched per-chain step for a chain-row arena")
 body = src[a:b]
-NPH = 9
+NPH = 10
 
 
 def st(i):
@@ -31,6 +31,7 @@ ins("        wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);\n      }\n", "     
 ins("      if (!CARRY && pl) lds_pre[lane] = pv;\n      __syncthreads();\n", "      " + st(3))
 ins("      if (!CARRY && pl) lds_pre[lane] = pv;\n", "      " + st(2), before=True)
 ins("    // scalar logic: wave 0 on the LDS state (lane 0 writes back)\n", "    " + st(4), before=True)
+ins("        const float pe = m.fin(sums, gl, gs);\n", "        " + st(9))
 ins("    __syncthreads();  // decisions published\n", "    " + st(5), before=True)
 ins("    __syncthreads();  // decisions published\n", "    " + st(6))
 ins("      if (D2.start_iter) {\n        const float t = wave_sum(ke0);\n", "      " + st(7), before=True)

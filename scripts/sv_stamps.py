@@ -20,10 +20,11 @@ import bench_configs as BC  # noqa: E402
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 S = int(sys.argv[4]) if len(sys.argv) > 4 else 10
-NPH = 9
+NPH = 10
 NAMES = ["loop top (prev. iteration tail)", "leaf rows + wave sums", "U-turn checkpoint levels",
-         "barrier: every wave's rows", "potential finish (wave 0)", "scalar NUTS logic (wave 0)",
-         "barrier: decisions published", "apply rows", "barrier: rows written"]
+         "barrier: every wave's rows", "finish: scalar-site rows (wave 0)", "scalar NUTS logic (wave 0)",
+         "barrier: decisions published", "apply rows", "barrier: rows written",
+         "(of the finish) sums + fin()"]
 r = datasets.sp500_synthetic()
 BC.run_model("stochastic_volatility", P.stochastic_volatility, (r,), C, W, S, bytes_per_leapfrog=2 * (r.size + 2) * 4)
 buf = np.zeros((8192, 2, NPH + 2), np.uint64)

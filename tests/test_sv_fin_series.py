@@ -20,8 +20,9 @@ def half_diff(x):
         num = num * q + 0.5 * den
         den *= q
         X += 1.0
-    inv, H = 1.0 / X, X + 0.5
-    invh = 1.0 / H
+    H = X + 0.5
+    rxh = 1.0 / (X * H)
+    inv, invh = H * rxh, X * rxh
     u = 0.5 * inv
     t = u / (2.0 + u)
     t2 = t * t
@@ -35,9 +36,10 @@ def half_diff(x):
         iz2 = iz * iz
         return iz2 * (1 / 12 - iz2 * (1 / 120 - iz2 * (1 / 252 - iz2 * (1 / 240 - iz2 / 132))))
 
-    r = pn / pd
+    rpd = 1.0 / (pd * den)
+    r = pn * den * rpd
     L = -0.5 * math.log(X * r * r) - X * l1p + 0.5 + lser(inv) - lser(invh)
-    Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num / den
+    Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num * pd * rpd
     return L, Psi
 
 
