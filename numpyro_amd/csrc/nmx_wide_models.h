@@ -21,6 +21,41 @@
 
 #include "nmx_common.h"
 
+// A double constant materialized at its use: the compiler otherwise hoists the 64-bit constants
+// of a double polynomial out of the persistent kernel's leaf loop and, at 128 VGPRs, spills them
+// to scratch -- and each reload in the serial section waited (vmcnt(0)) for every global store
+// the wave still had in flight from its rows.
+__device__ __forceinline__ double nmx_kd(double c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
+// log(y) for a finite y > 0 in double: y = m 2^e, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s),
+// s = (m - 1) / (m + 1) (|s| <= 0.172: ten series terms), e ln 2 in two parts.  Within 2 ulp of
+// libm over 1e-30..1e30 (tests/test_sv_fin_series.py restates it); replaces ocml's log, whose
+// hoisted coefficients were the spilled constants above.
+__device__ __forceinline__ double nmx_log_f64(double y) {
+  int e = __builtin_amdgcn_frexp_exp(y);
+  double m = __builtin_amdgcn_frexp_mant(y);  // [0.5, 1)
+  if (m < nmx_kd(0.70710678118654752440)) {
+    m *= 2.0;
+    e -= 1;
+  }
+  const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+  double p = nmx_kd(1.0 / 21);
+  p = nmx_kd(1.0 / 19) + s2 * p;
+  p = nmx_kd(1.0 / 17) + s2 * p;
+  p = nmx_kd(1.0 / 15) + s2 * p;
+  p = nmx_kd(1.0 / 13) + s2 * p;
+  p = nmx_kd(1.0 / 11) + s2 * p;
+  p = nmx_kd(1.0 / 9) + s2 * p;
+  p = nmx_kd(1.0 / 7) + s2 * p;
+  p = nmx_kd(1.0 / 5) + s2 * p;
+  p = nmx_kd(1.0 / 3) + s2 * p;
+  const double ed = (double)e;
+  return ed * nmx_kd(6.93147180369123816490e-01) + (2.0 * s + (2.0 * s * s2 * p + ed * nmx_kd(1.90821492927058770002e-10)));
+}
+
 // The StudentT normaliser's two differences at x = nu / 2 > 0, in double:
 //   L = lgamma(x) - lgamma(x + 1/2),  Psi = digamma(x) - digamma(x + 1/2).
 // The recurrence lgamma(x) = lgamma(x + 1) - log x (digamma: - 1/x) shifts x to X >= 8, keeping
@@ -57,7 +92,7 @@ __device__ __forceinline__ void nmx_lgamma_digamma_half_diff(double x, double& L
     return iz2 * (1.0 / 12 - iz2 * (1.0 / 120 - iz2 * (1.0 / 252 - iz2 * (1.0 / 240 - iz2 / 132))));
   };
   const double rpd = 1.0 / (pd * den), r = pn * den * rpd;
-  L = -0.5 * log(X * r * r) - X * l1p + 0.5 + lser(inv) - lser(invh);
+  L = -0.5 * nmx_log_f64(X * r * r) - X * l1p + 0.5 + lser(inv) - lser(invh);
   Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num * pd * rpd;
 }
 

@@ -1841,7 +1841,7 @@ __device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float 
 // per row in flight instead of the arena form's eleven: larger batches fit the registers, fewer
 // dependent memory rounds per leaf.  Same arithmetic as persist_leaf_rows.
 #ifndef NMX_PX_BC
-#define NMX_PX_BC 3
+#define NMX_PX_BC 4  // SV 8192 chains: 2 / 3 / 4 rows 40.0 / 40.0 / 40.3M (profiles/r06/sv_phase_stamps.txt)
 #endif
 struct PRowG {
   float rs_old, rst, ro, ckr, ckrs;

@@ -31,7 +31,8 @@ ins("        wave_sums_to_lds<NW, NR>(red, lds, A, is_nuts);\n      }\n", "     
 ins("      if (!CARRY && pl) lds_pre[lane] = pv;\n      __syncthreads();\n", "      " + st(3))
 ins("      if (!CARRY && pl) lds_pre[lane] = pv;\n", "      " + st(2), before=True)
 ins("    // scalar logic: wave 0 on the LDS state (lane 0 writes back)\n", "    " + st(4), before=True)
-ins("        const float pe = m.fin(sums, gl, gs);\n", "        " + st(9))
+ins("        const float pe = m.fin(sums, gl, gs);\n",
+    '        asm volatile("" :: "v"(pe), "v"(gs[0]), "v"(gs[1]));  // fin() complete before the stamp\n        ' + st(9))
 ins("    __syncthreads();  // decisions published\n", "    " + st(5), before=True)
 ins("    __syncthreads();  // decisions published\n", "    " + st(6))
 ins("      if (D2.start_iter) {\n        const float t = wave_sum(ke0);\n", "      " + st(7), before=True)
