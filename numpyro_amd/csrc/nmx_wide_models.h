@@ -148,7 +148,9 @@ struct NmxWideSV {
     x.sp = t > 0 ? nmx_at(z, off - ldc4) : 0.0f;
     x.sn = t + 1 < T ? nmx_at(z, off + ldc4) : 0.0f;
   }
-  __device__ __forceinline__ void row_load_data(int d, RowIn& x) const { x.r = ret[d - 1]; }
+  // (a 32-bit byte offset from the SGPR base: ret[d - 1] took a 64-bit per-lane address, which the
+  // persistent kernel hoisted per row and spilled)
+  __device__ __forceinline__ void row_load_data(int d, RowIn& x) const { x.r = nmx_at(ret, (uint32_t)(d - 1) << 2); }
   __device__ __forceinline__ float row(const float* z, uint32_t off, uint32_t ldc4, int d, const Glob& g,
                                        float* sums) const {
     RowIn x;

@@ -1048,8 +1048,18 @@ __device__ __forceinline__ float apply_block(const VecCtx& v, const Act& A, floa
 }
 
 // Momentum normals of coordinates 4 blk .. 4 blk + 3 (one Philox call per block of 4).
+// The key words pass through an empty asm so the Philox key schedule (ten rounds of two keys) is
+// computed at the draw: hoisted out of the persistent wide kernel's leaf loop, the 20 round keys
+// held SGPRs for the whole launch and pushed its spills into VGPR lanes.  Same values as nmx_rng.
 __device__ __forceinline__ void momentum_block(uint64_t seed, uint32_t gch, int it, int blk, float (&n)[4]) {
-  const nmx_u4 x = nmx_rng(seed, gch, (uint32_t)it, NMX_EV_MOMENTUM, blk, 0);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  nmx_u4 c;
+  c.x = gch;
+  c.y = (uint32_t)it;
+  c.z = ((uint32_t)NMX_EV_MOMENTUM << 24) | ((uint32_t)blk & 0x00FFFFFFu);
+  c.w = 0;
+  const nmx_u4 x = nmx_philox4x32_10(c, k0, k1);
   nmx_box_muller(x.x, x.y, n[0], n[1]);
   nmx_box_muller(x.z, x.w, n[2], n[3]);
 }
