@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--cpu-chains", type=int, default=64, help="chains of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sync-chains", action="store_true", help="reference lockstep schedule")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
     p.add_argument("--configs", default="c2,c3,c4",
                    help="BASELINE.json secondary configs measured after the headline (comma list of c2 funnel-10k "
                         "dense, c3 BNN dense, c4 stochastic volatility; 'none' skips); c2/c3 are one-GPU configs "
