@@ -2122,32 +2122,24 @@ __device__ __forceinline__ const float* spre_src(const VecCtx& v, const Act& A, 
   return (f < 5 + MAXD ? a.ckr : a.ckrs) + l * v.ck_stride;
 }
 
-// The arena stores of a scalar-site row's leaf (momentum, subtree r_sum, checkpoint), deferred to
-// the end of the serial section (spre_store): issued where spre_leaf computes them, every later
-// scratch reload in the section waited (vmcnt(0)) for them to complete.
-struct SpreSt {
-  float r, rs, g;
-  int dirR, ck, imax;
-};
-
-// leaf_load + leaf_store of one scalar-site row from its prefetched inputs (same arithmetic; the
-// arena stores go to st for spre_store)
+// leaf_load + leaf_store of one scalar-site row from its prefetched inputs (same arithmetic)
 template <bool NUTS, bool CARRY = false>
-__device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float seff, float g, const float* pre,
-                                          float* red, SpreSt& st, const Front& fr = {}, int d = 0) {
+__device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float seff, uint32_t off, float g,
+                                          const float* pre, float* red, const Front& fr = {}, int d = 0) {
+  const Arena& a = *v.a;
   const float es = A.dirR ? seff : -seff;
   const float half = 0.5f * es;
   const float r = pre[0] - half * g;
-  if constexpr (CARRY) fr.r[d] = r;
-  st.r = r;
-  st.dirR = A.dirR;
-  st.ck = NUTS && (A.k & 1) == 0;
-  st.imax = A.imax;
+  front_r<CARRY>(v, A, fr, off, d) = r;
   const float im = v.unit ? 1.0f : pre[1];
   red[0] += (im * r) * r;
   if constexpr (NUTS) {
     const float rs = (A.k == 0) ? r : pre[2] + r;
-    st.rs = rs;
+    nmx_at(AV(NMX_F_RSUM_SUB), off) = rs;
+    if ((A.k & 1) == 0) {
+      nmx_at(a.ckr + A.imax * v.ck_stride, off) = r;
+      nmx_at(a.ckrs + A.imax * v.ck_stride, off) = rs;
+    }
 #pragma unroll
     for (int i = 0; i < MAXD; ++i) {
       if (i >= A.imin && i <= A.imax) {
@@ -2165,22 +2157,6 @@ __device__ __forceinline__ void spre_leaf(const VecCtx& v, const Act& A, float s
       const float rss2 = rst - (rlv + rrv) / 2.0f;
       red[1 + 2 * MAXD] += (im * rlv) * rss2;
       red[2 + 2 * MAXD] += (im * rrv) * rss2;
-    }
-  }
-}
-
-template <bool NUTS, bool CARRY>
-__device__ __forceinline__ void spre_store(const VecCtx& v, uint32_t off, const SpreSt& st) {
-  const Arena& a = *v.a;
-  if constexpr (!CARRY) {
-    nmx_at(AV(NMX_F_G_EVAL), off) = st.g;
-    nmx_at((st.dirR ? AV(NMX_F_RR) : AV(NMX_F_RL)), off) = st.r;
-  }
-  if constexpr (NUTS) {
-    nmx_at(AV(NMX_F_RSUM_SUB), off) = st.rs;
-    if (st.ck) {
-      nmx_at(a.ckr + st.imax * v.ck_stride, off) = st.r;
-      nmx_at(a.ckrs + st.imax * v.ck_stride, off) = st.rs;
     }
   }
 }
@@ -2309,8 +2285,6 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
     // every wave has read the state before wave 0's scalar logic rewrites it (a leaf's
     // reduction barrier orders this too)
     if (!A.leaf) __syncthreads();
-    const bool leaf_now = A.leaf;
-    SpreSt sst[M::NSCALAR];  // the scalar-site rows' arena stores, issued after the scalar logic
     if (A.leaf) {
       const float seff = uni_f(Ssh.step_eff);
       // the scalar-site rows' inputs are prefetched: by the last wave into lds_pre after its rows,
@@ -2366,6 +2340,7 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
 #pragma unroll
           for (int i = 0; i < M::NSCALAR; ++i) {
             const int d = m.scalar_row(i);
+            const uint32_t off = base + ((uint32_t)d << 2);
             float prer[CARRY ? SPRE : 1];
             const float* pre;
             if constexpr (CARRY) {
@@ -2376,10 +2351,10 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
               fr.g[d] = gs[i];
             } else {
               pre = lds_pre + i * SPRE;
+              nmx_at(AV(NMX_F_G_EVAL), off) = gs[i];
             }
-            sst[i].g = gs[i];
-            if (is_nuts) spre_leaf<true, CARRY>(v, A, seff, gs[i], pre, rs, sst[i], fr, d);
-            else spre_leaf<false, CARRY>(v, A, seff, gs[i], pre, rs, sst[i], fr, d);
+            if (is_nuts) spre_leaf<true, CARRY>(v, A, seff, off, gs[i], pre, rs, fr, d);
+            else spre_leaf<false, CARRY>(v, A, seff, off, gs[i], pre, rs, fr, d);
           }
 #pragma unroll
           for (int e = 0; e < NPART; ++e)
@@ -2411,14 +2386,6 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
         sh.slot = A.slot;
         sh.wfn = A.wfn;
         if (A.fin_done) atomicAdd(&a.counters[0], 1);
-        if (leaf_now) {
-#pragma unroll
-          for (int i = 0; i < M::NSCALAR; ++i) {
-            const uint32_t off = base + ((uint32_t)m.scalar_row(i) << 2);
-            if (is_nuts) spre_store<true, CARRY>(v, off, sst[i]);
-            else spre_store<false, CARRY>(v, off, sst[i]);
-          }
-        }
       }
       nmx_serial_prio(false);
     }
