@@ -484,6 +484,9 @@ __global__ __launch_bounds__(256) void k_x3_split_b_rows(const float* __restrict
 #define NMX_GEMM_RW 4
 #endif
 // 1: the 256 x 128 tile for launches it fills (nmx_gemm_chains_x3); 0: always RW x CT (A/B)
+#ifndef NMX_GEMM_BIG_MIN
+#define NMX_GEMM_BIG_MIN 512  // big-tile workgroups a launch must have to take the 256 x 128 tile
+#endif
 #ifndef NMX_GEMM_BIG
 #define NMX_GEMM_BIG 1
 #endif
@@ -923,7 +926,7 @@ int gemm_chains_x3(const void* Ap, int lda, int D, const float* In, const int32_
   // D = 10000, C = 4096) when that grid still gives two workgroups per CU, else 128 x 64 (two
   // workgroups per CU: better for few chains or small D)
   // (K-split launches keep the 128 x 64 tile: their split points depend on the tile's K range)
-  const bool big = NMX_GEMM_BIG && ks == 1 && (int64_t)((lda + 255) / 256) * ((num_chains + 127) / 128) >= 512;
+  const bool big = NMX_GEMM_BIG && ks == 1 && (int64_t)((lda + 255) / 256) * ((num_chains + 127) / 128) >= NMX_GEMM_BIG_MIN;
   if (big) {
     if (int st = launch_gemm_x3<4, 2, 8>(Ap, lda, D, split, Out, bias, triangle, ldc, phase, active_count,
                                          num_chains, workspace, ks, s, out_list, pe_in, pe_out))
