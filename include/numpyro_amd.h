@@ -487,6 +487,9 @@ int nmx_selftest_mfma(const float* A, const float* B, float* C, int K, void* str
  * the device in libnumpyro_amd_debug.so.  Returns 1 in the debug build, 0 in the release build,
  * a negative status on a launch error. */
 int nmx_selftest_dcheck(int value, void* stream);
+/* nmx_expf_unchecked (the stochastic-volatility row's exp, nmx_wide_models.h) and the device expf
+ * at n points: fast[i], ref[i] (bitwise equal for |x| <= 87). */
+int nmx_selftest_expf(const float* x, float* fast, float* ref, int n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -96,6 +96,20 @@ __device__ __forceinline__ void nmx_lgamma_digamma_half_diff(double x, double& L
   Psi = -l1p - 0.5 * inv + 0.5 * invh - pser(inv) + pser(invh) - num * pd * rpd;
 }
 
+// expf(x) by the same reduction the compiler's expf uses (x log2 e in two parts, 2^frac by
+// v_exp_f32, ldexp) without its overflow / underflow selects: bitwise expf's value for |x| <= 87
+// (SV's -2 s), four VALU fewer per row; beyond that the value saturates the same way (ldexp), and
+// a non-finite s gives NaN where expf gives inf -- either way the leaf's energy is not finite and
+// the trajectory diverges.
+__device__ __forceinline__ float nmx_expf_unchecked(float x) {
+  const float l2e = __int_as_float(0x3fb8aa3b), l2e_lo = __int_as_float(0x32a5705f);
+  float t = x * l2e;
+  asm volatile("" : "+v"(t));  // t is the rounded product, as in expf (else (t - n) became fma(x, l2e, -n))
+  const float n = __builtin_rintf(t);
+  const float c = __builtin_fmaf(x, l2e_lo, __builtin_fmaf(x, l2e, -t));
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f((t - n) + c), (int)n);
+}
+
 // Stochastic volatility (examples/stochastic_volatility.py:57-65), z = (a = log nu, s[T],
 // b = log sigma): rows 1..T are s_t (t = row - 1), scalar rows 0 (a) and T + 1 (b).
 // Sums: sum d_t^2, sum log1p(q_t), sum q_t / (1 + q_t), sum s_t.
@@ -163,14 +177,15 @@ struct NmxWideSV {
     const float dd = s - sp;
     const float dn = t + 1 < T ? sn - s : 0.0f;
     const float r = x.r;
-    const float q = r * r * expf(-2.0f * s) * g.inv_nu;
 #if NMX_SV_FAST
+    const float q = r * r * nmx_expf_unchecked(-2.0f * s) * g.inv_nu;
     const float u = 1.0f + q;
     const float qq = q * __builtin_amdgcn_rcpf(u);
     const float l1q = (u == 1.0f || !(u < INFINITY)) ? q
                                                      : __builtin_amdgcn_logf(u) * 0.6931471805599453f *
                                                            (q * __builtin_amdgcn_rcpf(u - 1.0f));
 #else
+    const float q = r * r * expf(-2.0f * s) * g.inv_nu;
     const float qq = q / (1.0f + q);
     const float l1q = log1pf(q);
 #endif

@@ -2,6 +2,7 @@
 // vectors and the gfx950 f32 MFMA fragment layout that the potential kernels rely on.
 #include "nmx_common.h"
 #include "nmx_api_internal.h"
+#include "nmx_wide_models.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -66,4 +67,18 @@ extern "C" int nmx_selftest_dcheck(int value, void* stream) {
 #else
   return 0;
 #endif
+}
+
+// nmx_expf_unchecked (the SV row's exp) against the device expf, element by element
+__global__ void k_expf_probe(const float* x, float* fast, float* ref, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fast[i] = nmx_expf_unchecked(x[i]);
+  ref[i] = expf(x[i]);
+}
+
+extern "C" int nmx_selftest_expf(const float* x, float* fast, float* ref, int n, void* stream) {
+  if (n <= 0 || !x || !fast || !ref) return nmx_fail(NMX_ERR_INVALID, "expf probe: bad arguments");
+  hipLaunchKernelGGL(k_expf_probe, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, fast, ref, n);
+  return nmx_check_launch("k_expf_probe");
 }

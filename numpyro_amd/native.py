@@ -118,6 +118,7 @@ SIGNATURES: dict[str, tuple] = {
     "nmx_selftest_philox": (c_int, [c_vp, c_vp, c_int, c_vp]),
     "nmx_selftest_mfma": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_selftest_dcheck": (c_int, [c_int, c_vp]),
+    "nmx_selftest_expf": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp]),
     "nmx_nuts_arena_bytes": (c_size, [c_int, c_int, c_int, c_int]),
     "nmx_nuts_num_slices": (c_int, [c_int]),
     "nmx_nuts_field_info": (c_int, [c_int, c_int, c_int, c_int, c_int, _P(c_size), _P(c_size)]),

@@ -239,6 +239,25 @@ def test_compacted_active_list_is_bitwise_equal_to_dense(device, which):
     assert np.all(np.isnan(pe_l[others]))
 
 
+def test_sv_row_exp_is_bitwise_expf(device):
+    """The SV row's exp (nmx_expf_unchecked: expf's reduction without its range selects) equals the
+    device expf bit for bit over |x| <= 87, the range -2 s of a stochastic-volatility row spans."""
+    import torch
+
+    from numpyro_amd import native
+
+    rs = np.random.RandomState(0)
+    xs = np.concatenate([np.linspace(-87.0, 87.0, 200001), rs.uniform(-30, 30, 100000),
+                         rs.standard_normal(100000) * 1e-3, [0.0, -0.0, 1e-30, -1e-30]]).astype(np.float32)
+    x = torch.from_numpy(xs).to(device)
+    fast, ref = torch.empty_like(x), torch.empty_like(x)
+    native.check(native.lib().nmx_selftest_expf(native.ptr(x), native.ptr(fast), native.ptr(ref), x.numel(),
+                                                native.stream_ptr()))
+    torch.cuda.synchronize()
+    same = (fast.view(torch.int32) == ref.view(torch.int32)).cpu().numpy()
+    assert same.all(), f"{(~same).sum()} of {same.size} differ, first at x = {xs[~same][:5]}"
+
+
 def test_stochastic_volatility_matches_oracle(device):
     """examples/stochastic_volatility.py model at the SP500 length (T = 2517, D = 2519).
     U sums ~3T terms of magnitude up to ~10 with cancellation, so the fp32 tolerance is
