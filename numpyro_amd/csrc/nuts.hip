@@ -1298,6 +1298,12 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
 #ifndef NMX_PX_B
 #define NMX_PX_B 2  // rows per thread in flight in the persistent wide kernel (profiles/r03/ab_persistent_occ.txt)
 #endif
+#ifndef NMX_PX_BA
+// rows per thread in flight in the persistent wide kernel's apply phase: SV 8192 chains 1 / 2 / 3 /
+// 4 rows 42.7 / 41.9 / 39.7 / 33.9M (profiles/r06/sv_phase_stamps.txt: fewer values live across the
+// phase's LDS round trips)
+#define NMX_PX_BA 1
+#endif
 #ifndef NMX_PX_BL
 #define NMX_PX_BL NMX_PX_B  // the same in its leaf phase
 #endif
@@ -3223,11 +3229,11 @@ int launch_persistent_nt(const StepArgs& args, const M& m, int max_steps, hipStr
   const dim3 grid(args.cfg.num_chains);
   if (persist_carry(args.cfg.dim, NT, (sizeof(PersistShared<NT, M, true>) + 15) / 16 * 16)) {
     const size_t lds = (size_t)16 * args.cfg.dim;
-    if (const int st = nmx_lds_limit((const void*)k_wide_persistent<NT, NMX_PX_B, M, true>, lds, s, "run_wide"))
+    if (const int st = nmx_lds_limit((const void*)k_wide_persistent<NT, NMX_PX_BA, M, true>, lds, s, "run_wide"))
       return st;
-    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, true>), grid, dim3(NT), lds, s, args, m, max_steps);
+    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_BA, M, true>), grid, dim3(NT), lds, s, args, m, max_steps);
   } else {
-    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_B, M, false>), grid, dim3(NT), 0, s, args, m, max_steps);
+    hipLaunchKernelGGL((k_wide_persistent<NT, NMX_PX_BA, M, false>), grid, dim3(NT), 0, s, args, m, max_steps);
   }
   return NMX_OK;
 }
@@ -3258,10 +3264,10 @@ extern "C" int nmx_debug_persist_occupancy(int dim, int* blocks_per_cu, int* car
   *carry = cr;
   hipError_t e;
   if (cr)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_B, NmxWideSV, true>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_BA, NmxWideSV, true>,
                                                      256, (size_t)16 * dim);
   else
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_B, NmxWideSV, false>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_wide_persistent<256, NMX_PX_BA, NmxWideSV, false>,
                                                      256, 0);
   return e == hipSuccess ? NMX_OK : nmx_fail(NMX_ERR_HIP, "occupancy: %s", hipGetErrorString(e));
 }
