@@ -909,8 +909,14 @@ __device__ __forceinline__ void apply_load(const VecCtx& v, const Act& A, uint32
   if (A.start_iter || A.prep_leaf) x.im = v.unit ? 1.0f : (CARRY ? fr.im[d] : nmx_at(AV(NMX_F_INV_MASS), off));
   if (A.prep_leaf) {
     const int nd = A.new_dir;
-    if (CARRY && !turn_around(A)) x.rfn = fr.r[d];  // the frontier keeps growing
-    else x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+    if constexpr (CARRY) {
+      // the frontier keeps growing: its momentum from LDS, read unconditionally (written as one
+      // conditional LDS-or-arena load, the two became a flat load through a selected address)
+      x.rfn = fr.r[d];
+      if (turn_around(A)) x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+    } else {
+      x.rfn = nmx_at((nd ? AV(NMX_F_RR) : AV(NMX_F_RL)), off);
+    }
     if (turn_around(A)) {
       x.zfn = nmx_at((nd ? AV(NMX_F_ZR) : AV(NMX_F_ZL)), off);
       x.gfn = nmx_at((nd ? AV(NMX_F_GR) : AV(NMX_F_GL)), off);
@@ -1297,6 +1303,9 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void k_wide_v1(WideArgs W) {
     // (rows in pairs: 134 VGPRs, 3 waves; SV launched -2.4%, funnel-10k diag -3.5%)
 #ifndef NMX_PX_B
 #define NMX_PX_B 2  // rows per thread in flight in the persistent wide kernel (profiles/r03/ab_persistent_occ.txt)
+#endif
+#ifndef NMX_PX_FAST_APPLY
+#define NMX_PX_FAST_APPLY 1  // the persistent wide kernel's mid-trajectory apply loop (persist_apply_prep_rows)
 #endif
 #ifndef NMX_PX_BA
 // rows per thread in flight in the persistent wide kernel's apply phase: SV 8192 chains 1 / 2 / 3 /
@@ -1856,6 +1865,16 @@ __device__ __forceinline__ void prow_store(const VecCtx& v, const Act& A, float 
 // BC rows' worth of them go out first, then each row reads its LDS inputs and runs.  Five floats
 // per row in flight instead of the arena form's eleven: larger batches fit the registers, fewer
 // dependent memory rounds per leaf.  Same arithmetic as persist_leaf_rows.
+// A thread's first model row, recomputed at each use: hoisted out of the leaf loop (as a 64-bit
+// induction start) it was spilled, and its scratch reload before the apply loop put an
+// s_waitcnt vmcnt(0) at the loop's back edge -- every apply row then waited for its own stores.
+template <class M>
+__device__ __forceinline__ int first_row(const M& m) {
+  int d0 = m.lo() + (int)threadIdx.x;
+  asm volatile("" : "+v"(d0));
+  return d0;
+}
+
 #ifndef NMX_PX_BC
 #define NMX_PX_BC 4  // SV 8192 chains: 2 / 3 / 4 rows 40.0 / 40.0 / 40.3M (profiles/r06/sv_phase_stamps.txt)
 #endif
@@ -1872,7 +1891,7 @@ __device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const A
   float acc[3 + M::NSUM];
 #pragma unroll
   for (int i = 0; i < 3 + M::NSUM; ++i) acc[i] = 0.0f;
-  for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += BC * NT) {
+  for (int d0 = first_row(m); d0 < hi; d0 += BC * NT) {
     PRowG xg[BC];
     typename M::RowIn mi[BC];
     // the batch's loads, grouped by their (wave-uniform) condition, every row of the batch
@@ -1961,7 +1980,7 @@ __device__ __forceinline__ void persist_leaf_rows(const VecCtx& v, const Act& A,
   float acc[3 + M::NSUM];
 #pragma unroll
   for (int i = 0; i < 3 + M::NSUM; ++i) acc[i] = 0.0f;
-  for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B * NT) {
+  for (int d0 = first_row(m); d0 < hi; d0 += B * NT) {
     PRow x[B];
     typename M::RowIn mi[B];
 #pragma unroll
@@ -2018,7 +2037,7 @@ __device__ __forceinline__ void persist_ckpt_levels(const VecCtx& v, const Act& 
     const float* CK = a.ckr + i * v.ck_stride;
     const float* CKS = a.ckrs + i * v.ck_stride;
     float dl = 0.0f, dr = 0.0f;
-    for (int d0 = m.lo() + (int)threadIdx.x; d0 < hi; d0 += B2 * NT) {
+    for (int d0 = first_row(m); d0 < hi; d0 += B2 * NT) {
       float r[B2], rs[B2], im[B2], rl[B2], rls[B2];
 #pragma unroll
       for (int q = 0; q < B2; ++q) {
@@ -2089,7 +2108,7 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
       }
     }
   };
-  rows(m.lo() + (int)threadIdx.x, NT, hi, std::integral_constant<int, B>{});
+  rows(first_row(m), NT, hi, std::integral_constant<int, B>{});
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < M::NSCALAR; ++i) {
@@ -2100,6 +2119,38 @@ __device__ __forceinline__ float persist_apply_rows(const VecCtx& v, const Act& 
   return ke0;
 }
 
+
+// The apply phase of a mid-trajectory leaf (CARRY): the next half step and position of the
+// frontier (prep_leaf, no turn-around), the proposal copy when the leaf is taken, nothing else --
+// apply_load / apply_store's arithmetic on the same values, without their rare branches.  In the
+// general loop the rare branches' conditional arena loads were merged into selects on registers a
+// previous row may still have been loading, and every row waited (s_waitcnt vmcnt(0)) for all
+// stores in flight; this loop has no global load at all.
+template <int NT, class M>
+__device__ __forceinline__ void persist_apply_prep_rows(const VecCtx& v, const Act& A, const M& m, float step_eff,
+                                                        uint32_t base, const Front& fr) {
+  const Arena& a = *v.a;
+  const float es = A.new_dir ? step_eff : -step_eff;
+  const float half = 0.5f * es;
+  auto row = [&](int d) {
+    const float ze = fr.z[d], ge = fr.g[d];
+    if (A.take_leaf) {
+      const uint32_t off = base + ((uint32_t)d << 2);
+      nmx_at(AV(NMX_F_ZSUB), off) = ze;
+      nmx_at(AV(NMX_F_GSUB), off) = ge;
+    }
+    const float im = v.unit ? 1.0f : fr.im[d];
+    const float rh = fr.r[d] - half * ge;
+    fr.r[d] = rh;
+    fr.z[d] = ze + es * (im * rh);
+  };
+  const int hi = m.hi();
+  for (int d = first_row(m); d < hi; d += NT) row(d);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < M::NSCALAR; ++i) row(m.scalar_row(i));
+  }
+}
 
 // wave-uniform copies of values every lane holds alike (LDS reads look divergent to the
 // compiler; as scalars they stay out of the vector registers)
@@ -2415,7 +2466,11 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_wide_persistent(StepArgs Pk,
       constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE |
                           ACT_START | ACT_PREP;
       float ke0 = 0.0f;
-      if (act & VEC) {
+      constexpr int RARE = ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_WF_UPDATE |
+                           ACT_FINALIZE | ACT_START;
+      if (CARRY && NMX_PX_FAST_APPLY && (act & ACT_PREP) && !(act & RARE) && D2.new_dir == D2.dirR) {
+        persist_apply_prep_rows<NT>(v, D2, m, uni_f(Ssh.step_eff), base, fr);
+      } else if (act & VEC) {
         float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc
                                                                          : nullptr;
         ke0 = persist_apply_rows<NT, B, CARRY>(v, D2, m, uni_f(Ssh.step_eff), base, c, seed, gch, uni_i(Ssh.it), samp,

@@ -10,7 +10,7 @@ src = open(os.path.join(ROOT, "numpyro_amd", "csrc", "nuts.hip")).read()
 a = src.index("void k_wide_persistent(StepArgs Pk, M m, int max_steps) {")
 b = src.index("// ---- launched per-chain step for a chain-row arena")
 body = src[a:b]
-NPH = 10
+NPH = 12
 
 
 def st(i):
@@ -35,7 +35,9 @@ ins("        const float pe = m.fin(sums, gl, gs);\n",
     '        asm volatile("" :: "v"(pe), "v"(gs[0]), "v"(gs[1]));  // fin() complete before the stamp\n        ' + st(9))
 ins("    __syncthreads();  // decisions published\n", "    " + st(5), before=True)
 ins("    __syncthreads();  // decisions published\n", "    " + st(6))
-ins("      if (D2.start_iter) {\n        const float t = wave_sum(ke0);\n", "      " + st(7), before=True)
+ins("      if (D2.start_iter) {\n        const float t = wave_sum(ke0);\n",
+    "      { const unsigned long long t_ = __builtin_amdgcn_s_memtime(), d_ = t_ - tp_; acc_[7] += d_;\n"
+    "        if (act & ACT_TAKE_LEAF) { acc_[10] += d_; acc_[11] += 1; } tp_ = t_; }\n", before=True)
 ins("      __syncthreads();  // this leaf's rows are written: the next leaf reads its neighbours' positions\n",
     "      " + st(8))
 ins("  if (tid == 0) {\n    Arena al = Pk.a;  // addresses recomputed here",

@@ -20,11 +20,11 @@ import bench_configs as BC  # noqa: E402
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 S = int(sys.argv[4]) if len(sys.argv) > 4 else 10
-NPH = 10
+NPH = 12
 NAMES = ["loop top (prev. iteration tail)", "leaf rows + wave sums", "U-turn checkpoint levels",
          "barrier: every wave's rows", "finish: scalar-site rows (wave 0)", "scalar NUTS logic (wave 0)",
          "barrier: decisions published", "apply rows", "barrier: rows written",
-         "(of the finish) sums + fin()"]
+         "(of the finish) sums + fin()", "(of apply) take_leaf leaves", "(count) take_leaf leaves"]
 r = datasets.sp500_synthetic()
 BC.run_model("stochastic_volatility", P.stochastic_volatility, (r,), C, W, S, bytes_per_leapfrog=2 * (r.size + 2) * 4)
 buf = np.zeros((8192, 2, NPH + 2), np.uint64)
@@ -35,9 +35,15 @@ for w, nm in ((0, "wave 0"), (1, "wave 1")):
     nit = buf[:n, w, NPH].astype(np.float64)
     nleaf = buf[:n, w, NPH + 1].astype(np.float64)
     ok = nleaf > 0
-    tot = acc[ok].sum(axis=1)
+    tot = acc[ok][:, :10].sum(axis=1)
     print(f"{nm}: {int(ok.sum())} workgroups, median {np.median(nit[ok]):.0f} iterations / "
           f"{np.median(nleaf[ok]):.0f} leaves per launch, median {np.median(tot / nleaf[ok]):.0f} cycles per leaf")
     per = np.median(acc[ok] / nleaf[ok, None], axis=0)
-    for i in range(NPH):
-        print(f"  {NAMES[i]:34s} {per[i]:8.0f} cycles/leaf {100 * per[i] / per.sum():5.1f}%")
+    for i in range(10):
+        print(f"  {NAMES[i]:34s} {per[i]:8.0f} cycles/leaf {100 * per[i] / per[:10].sum():5.1f}%")
+    tl = buf[:n, w, 11].astype(np.float64)
+    ok2 = ok & (tl > 0) & (nleaf > tl)
+    a_tl = np.median(acc[ok2, 10] / tl[ok2])
+    a_other = np.median((acc[ok2, 7] - acc[ok2, 10]) / (nleaf[ok2] - tl[ok2]))
+    print(f"  apply rows per leaf: take_leaf {a_tl:.0f} cycles, other leaves {a_other:.0f}; "
+          f"take_leaf fraction {np.median(tl[ok2] / nleaf[ok2]):.2f}")
