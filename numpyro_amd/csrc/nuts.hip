@@ -1875,8 +1875,16 @@ __device__ __forceinline__ int first_row(const M& m) {
   return d0;
 }
 
+#ifndef NMX_PX_PIPE
+// persist_leaf_rows_carry software-pipelined over two batches (A/B: 55.6-56.1M with two buffers of
+// 2 rows vs 57.2-57.5M unpipelined at SV 8192 chains -- the other chains' waves already cover the
+// store drain; profiles/r06/sv_phase_stamps.txt)
+#define NMX_PX_PIPE 0
+#endif
 #ifndef NMX_PX_BC
-#define NMX_PX_BC 4  // SV 8192 chains: 2 / 3 / 4 rows 40.0 / 40.0 / 40.3M (profiles/r06/sv_phase_stamps.txt)
+// rows per batch of the carry form's leaf rows: SV 8192 chains 2 / 3 / 4 rows 40.0 / 40.0 / 40.3M
+// (before the apply loop's fix), 3 / 4 / 5: 42.5 / 42.7 / 42.8M (profiles/r06/sv_phase_stamps.txt)
+#define NMX_PX_BC 4
 #endif
 struct PRowG {
   float rs_old, rst, ro, ckr, ckrs;
@@ -1891,13 +1899,11 @@ __device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const A
   float acc[3 + M::NSUM];
 #pragma unroll
   for (int i = 0; i < 3 + M::NSUM; ++i) acc[i] = 0.0f;
-  for (int d0 = first_row(m); d0 < hi; d0 += BC * NT) {
-    PRowG xg[BC];
-    typename M::RowIn mi[BC];
-    // the batch's loads, grouped by their (wave-uniform) condition, every row of the batch
-    // included: a row past hi reads row hi - 1 (a valid address; the value is never used).  Per-row
-    // guards around the loads split them into small blocks, and the compiler drained the first
-    // row's loads (s_waitcnt vmcnt(0)) before issuing the rest: two memory round trips per batch.
+  // a batch's loads, grouped by their (wave-uniform) condition, every row of the batch included: a
+  // row past hi reads row hi - 1 (a valid address; the value is never used).  Per-row guards around
+  // the loads split them into small blocks, and the compiler drained the first row's loads
+  // (s_waitcnt vmcnt(0)) before issuing the rest.
+  auto load = [&](int d0, PRowG (&xg)[BC], typename M::RowIn (&mi)[BC]) {
     uint32_t offq[BC];
 #pragma unroll
     for (int q = 0; q < BC; ++q) {
@@ -1931,6 +1937,8 @@ __device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const A
         }
       }
     }
+  };
+  auto compute = [&](int d0, const PRowG (&xg)[BC], typename M::RowIn (&mi)[BC]) {
 #pragma unroll
     for (int q = 0; q < BC; ++q) {
       const int d = d0 + q * NT;
@@ -1950,7 +1958,34 @@ __device__ __forceinline__ void persist_leaf_rows_carry(const VecCtx& v, const A
         prow_store<NUTS, true, 1>(v, A, seff, off, x, g, acc, dl, dr, fr, d);
       }
     }
+  };
+#if NMX_PX_PIPE
+  // software-pipelined over two register buffers: batch b + 1's loads go out before batch b's
+  // stores, so the wait for them does not also wait for those stores (loads and stores share
+  // vmcnt, in order) -- one batch per memory round instead of a full store drain per batch
+  PRowG xa[BC], xb[BC];
+  typename M::RowIn ma[BC], mb[BC];
+  int d0 = first_row(m);
+  if (d0 < hi) load(d0, xa, ma);
+  while (d0 < hi) {
+    int d1 = d0 + BC * NT;
+    if (d1 < hi) load(d1, xb, mb);
+    compute(d0, xa, ma);
+    d0 = d1;
+    if (d0 >= hi) break;
+    d1 = d0 + BC * NT;
+    if (d1 < hi) load(d1, xa, ma);
+    compute(d0, xb, mb);
+    d0 = d1;
   }
+#else
+  for (int d0 = first_row(m); d0 < hi; d0 += BC * NT) {
+    PRowG xg[BC];
+    typename M::RowIn mi[BC];
+    load(d0, xg, mi);
+    compute(d0, xg, mi);
+  }
+#endif
   red[0] += acc[0];
   red[1 + 2 * MAXD] += acc[1];
   red[2 + 2 * MAXD] += acc[2];
