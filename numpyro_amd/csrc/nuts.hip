@@ -2187,6 +2187,46 @@ __device__ __forceinline__ void persist_apply_prep_rows(const VecCtx& v, const A
   }
 }
 
+// The same mid-trajectory apply on the arena (k_chain_step, no LDS frontier): B rows' loads, then
+// their stores -- apply_load / apply_store's prep-leaf arithmetic without the generic loop's merged
+// rare-branch loads (each of its rows waited for every store in flight).
+template <int NT, int B, class M>
+__device__ __forceinline__ void apply_prep_rows_arena(const VecCtx& v, const Act& A, const M& m, float step_eff,
+                                                      uint32_t base) {
+  const Arena& a = *v.a;
+  const float es = A.new_dir ? step_eff : -step_eff;
+  const float half = 0.5f * es;
+  const float* RF = A.new_dir ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  float* RW = A.new_dir ? AV(NMX_F_RR) : AV(NMX_F_RL);
+  float* ZE = AV(NMX_F_Z_EVAL);
+  const int hi = m.hi();
+  for (int d0 = first_row(m); d0 < hi; d0 += B * NT) {
+    float ze[B], ge[B], im[B], rf[B];
+    uint32_t offq[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int d = min(d0 + q * NT, hi - 1);  // past hi: row hi - 1, loaded and not used
+      offq[q] = base + ((uint32_t)d << 2);
+      ze[q] = nmx_at(ZE, offq[q]);
+      ge[q] = nmx_at(AV(NMX_F_G_EVAL), offq[q]);
+      im[q] = v.unit ? 1.0f : nmx_at(AV(NMX_F_INV_MASS), offq[q]);
+      rf[q] = nmx_at(RF, offq[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (d0 + q * NT < hi) {
+        if (A.take_leaf) {
+          nmx_at(AV(NMX_F_ZSUB), offq[q]) = ze[q];
+          nmx_at(AV(NMX_F_GSUB), offq[q]) = ge[q];
+        }
+        const float rh = rf[q] - half * ge[q];
+        nmx_at(RW, offq[q]) = rh;
+        nmx_at(ZE, offq[q]) = ze[q] + es * (im[q] * rh);
+      }
+    }
+  }
+}
+
 // wave-uniform copies of values every lane holds alike (LDS reads look divergent to the
 // compiler; as scalars they stay out of the vector registers)
 __device__ __forceinline__ int uni_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -2711,7 +2751,11 @@ __global__ __launch_bounds__(NT, NMX_PX_OCC) void k_chain_step(StepArgs Pk) {
   constexpr int VEC = ACT_TAKE_LEAF | ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_START |
                       ACT_PREP;
   float ke0 = 0.0f;
-  if (act & VEC) {
+  constexpr int RARE = ACT_DONE_SUB | ACT_TAKE_BIASED | ACT_HMC_ACCEPT | ACT_ITER_DONE | ACT_WF_UPDATE |
+                       ACT_FINALIZE | ACT_START;
+  if (NMX_PX_FAST_APPLY && (act & ACT_PREP) && !(act & RARE) && D2.new_dir == D2.dirR) {
+    apply_prep_rows_arena<NT, B>(v, D2, rows, uni_f(sh_seff), base);
+  } else if (act & VEC) {
     float* const samp = (D2.iter_done && D2.slot >= 0 && P.samples) ? P.samples + (size_t)D2.slot * D * ldc : nullptr;
     ke0 = persist_apply_rows<NT, B>(v, D2, rows, uni_f(sh_seff), base, c, seed, gch, uni_i(sh_it), samp, P.transform,
                                     cfg);
